@@ -1,0 +1,159 @@
+/* izpi_gpu.h — C ABI of the MI355X path-tracing inner loop for izpi.
+ *
+ * Drop-in boundary: a Go `GPURenderer` implementing
+ * render.Renderer (internal/render/renderer.go:26-28) flattens the scene once and
+ * calls izpi_gpu_render per frame (or per tile batch), replacing
+ *   render.New(...).Render(ctx)      leader/leader.go:136-158, renderer.go:73-222
+ * and, per tile, the per-pixel loops
+ *   renderRectRGB                     render/rgb.go:12-57
+ *   renderRectSpectral / RenderPixelSpectral  render/spectral.go:14-106
+ * The per-sample Sampler interface (sampler.go:30-33) is deliberately NOT the
+ * boundary: cgo costs ~35 ns per call (hitable/bvh4_simd_arm64.go:14).
+ *
+ * Ownership: host arrays passed to izpi_gpu_upload_scene are read during the call
+ * only; the library owns all device buffers inside the opaque context. Output
+ * buffers are caller-allocated. Calls on one context are serialised by the caller;
+ * one context per GPU. No C++ exception or abort() crosses this ABI: every entry
+ * point returns an IZPI_* status and izpi_gpu_last_error() explains failures.
+ */
+#ifndef IZPI_GPU_H
+#define IZPI_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+#include "izpi_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct izpi_ctx izpi_ctx;
+
+/* Flattened scene, as the Go host holds it after transport.ToScene
+ * (transport/transport.go:53-92) and hitable.NewBVH4 (hitable/bvh4.go:517-593).
+ * Every per-triangle array is [num_tris][3] doubles unless noted. */
+typedef struct izpi_scene_desc {
+  uint32_t abi_version;      /* IZPI_ABI_VERSION */
+  uint32_t num_nodes;        /* len(BVH4.Nodes) */
+  uint32_t num_prims;        /* len(BVH4.Primitives) */
+  uint32_t num_tris, num_spheres, num_lights, num_materials, num_textures;
+  uint32_t num_spd;          /* entries in spd_wavelengths / spd_values */
+  uint32_t pad0;
+  uint64_t num_texels;       /* doubles in texels[] */
+  const izpi_bvh4_node* nodes;  /* BVH4.Nodes, root = 0 (bvh4.go:42-47) */
+  const uint32_t* prim_ref;     /* BVH4.Primitives (leaf order, bvh4.go:585-590) as IZPI_PRIM_REF */
+  /* hitable.Triangle fields (triangle.go:20-52) */
+  const double* tri_v0;
+  const double* tri_v1;
+  const double* tri_v2;
+  const double* tri_e1;        /* edge1 = v1 - v0 */
+  const double* tri_e2;        /* edge2 = v2 - v0 */
+  const double* tri_normal;    /* unit(edge1 x edge2) */
+  const double* tri_tangent;   /* normal-mapping frame */
+  const double* tri_bitangent;
+  const double* tri_uv;        /* [num_tris][6]: u0,v0,u1,v1,u2,v2 */
+  const double* tri_area;      /* [num_tris] */
+  const uint32_t* tri_mat;     /* [num_tris] material index */
+  /* hitable.Sphere fields (sphere.go:20-27) */
+  const double* sph_center0;   /* [num_spheres][3] */
+  const double* sph_center1;   /* [num_spheres][3] */
+  const double* sph_time;      /* [num_spheres][2]: time0, time1 */
+  const double* sph_radius;    /* [num_spheres] */
+  const uint32_t* sph_mat;     /* [num_spheres] */
+  /* Scene.Lights = every hitable whose material IsEmitter() (transport.go:67-72) */
+  const uint32_t* light_ref;   /* [num_lights] IZPI_PRIM_REF, transport order */
+  const izpi_material* materials;
+  const izpi_texture* textures;
+  const double* texels;        /* image textures, float64 NRGBA */
+  const double* spd_wavelengths;
+  const double* spd_values;
+  izpi_camera camera;
+} izpi_scene_desc;
+
+enum { IZPI_SAMPLER_COLOUR = 2, IZPI_SAMPLER_SPECTRAL = 5 }; /* sampler.go:13-20 */
+enum {
+  IZPI_OUT_CANVAS = 0, /* W*H*4 float64 NRGBA canvas; pixel (x,y) lands in row H-y (rgb.go:41) */
+  IZPI_OUT_PACKED = 1  /* tiles packed in request order, each (x1-x0+1)*(y1-y0+1)*4,
+                          row-major by sample row y then x; the row-H-y rule is applied
+                          by izpi_gpu_unpack_tiles */
+};
+
+typedef struct izpi_render_req {
+  uint32_t width, height;     /* canvas size = Renderer sizeX, sizeY */
+  uint32_t spp;               /* numSamples */
+  uint32_t max_depth;         /* maxDepth (main.go:25 default 50) */
+  uint32_t sampler;           /* IZPI_SAMPLER_* */
+  uint32_t out_layout;        /* IZPI_OUT_* */
+  uint32_t num_tiles;         /* 0 = whole frame in common.Tiles steps */
+  uint32_t num_bg_spd;        /* entries of the spectral background SPD (0 = black) */
+  const uint32_t* tiles;      /* [num_tiles][4] = x0,y0,x1,y1 inclusive (workUnit, renderer.go:56-70) */
+  const double* bg_spd_wavelengths; /* spectral background (Spectral.background) */
+  const double* bg_spd_values;
+  double background[3];       /* Colour background (leader.go:140: black) */
+  uint64_t seed;              /* master seed of the per-sample LCG streams */
+} izpi_render_req;
+
+/* Per-render counters. The traversal is bit-identical to the CPU restatement, so
+ * these equal the oracle's counts exactly (used for algorithmic bytes, §8(d)). */
+typedef struct izpi_render_stats {
+  uint64_t rays;          /* Sampler calls past the depth check == numRays (colour.go:38) */
+  uint64_t node_visits;   /* BVH4 node loads (bvh4.go:91), incl. dielectric path-length traversals */
+  uint64_t tri_tests;     /* Triangle.Hit calls inside traversal (bvh4.go:127) */
+  uint64_t sph_tests;     /* Sphere.Hit calls inside traversal */
+  uint64_t light_tri_tests; /* Triangle.PDFValue intersection tests (hitable_slice.go:98-105) */
+  uint64_t light_sph_tests; /* Sphere.PDFValue intersection tests */
+  uint64_t samples;       /* pixel samples evaluated */
+  double kernel_ms;       /* device time of the traversal kernel (k_trace), HIP events on the library stream */
+  double shade_ms;        /* device time of the shading kernel (k_shade) */
+  double total_ms;        /* device time of the whole render call (kernels + accumulation) */
+  uint32_t launches;      /* k_trace launches (wavefront iterations) in the call */
+  uint32_t pad;
+} izpi_render_stats;
+
+/* Hit record returned by izpi_gpu_trace: BVH4.Hit (bvh4.go:49-164) followed by
+ * the closest primitive's record (triangle.go:193-265 / sphere.go:63-95). */
+typedef struct izpi_hit {
+  double t, u, v;
+  double p[3];
+  double normal[3];
+  uint32_t prim_ref;  /* IZPI_PRIM_REF of the closest primitive, 0xFFFFFFFF on miss */
+  uint32_t hit;       /* 0/1 */
+} izpi_hit;
+
+/* Open a context on HIP device `device` (>=0). */
+int izpi_gpu_open(int device, izpi_ctx** out);
+int izpi_gpu_close(izpi_ctx* ctx);
+const char* izpi_gpu_last_error(izpi_ctx* ctx);
+
+/* Copy a flattened scene to the device (repacking to the GPU layouts of DESIGN.md). */
+int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* scene);
+
+/* Render into a caller-owned HOST buffer: W*H*4 doubles for IZPI_OUT_CANVAS.
+ * Pixels outside the requested tiles are left untouched (the caller zero-fills,
+ * like floatimage.NewFloat64NRGBA). This is the Renderer.Render drop-in. */
+int izpi_gpu_render(izpi_ctx* ctx, const izpi_render_req* req, double* out_host, izpi_render_stats* stats);
+
+/* Same, but `out_dev` is a DEVICE pointer (e.g. a framebuffer owned by the caller
+ * on this context's device). Used by multi-GPU runs that gather over RCCL. */
+int izpi_gpu_render_device(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats);
+
+/* Scatter packed tiles (IZPI_OUT_PACKED, device memory) into a W*H*4 canvas
+ * (device memory) applying the row = H - y rule of rgb.go:41 / spectral.go:36. */
+int izpi_gpu_unpack_tiles(izpi_ctx* ctx, const izpi_render_req* req, const double* packed_dev, double* canvas_dev);
+
+/* Bytes of device output izpi_gpu_render_device writes for `req`. */
+uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);
+
+/* Component entry points (parity tests of the path's pieces). All arrays host. */
+/* Closest hit through World (HitableSlice{BVH4}); rays are [n][8]: o[3], d[3], tmin, tmax. */
+int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out);
+/* RayAABB4 masks (bvh4_simd_generic.go:10-52): boxes [n][24] f32 (SoA as BVH4Node),
+ * rays [n][7] f32: org[3], invdir[3], tmax. */
+int izpi_gpu_ray_aabb4(izpi_ctx* ctx, const float* boxes, const float* rays, uint32_t n, uint8_t* masks);
+/* Go-math on device, op codes in izpi_amd/csrc/gomath.h order: 0 sin 1 cos 2 tan 3 exp
+ * 4 log 5 pow(x,y) 6 atan2(x,y) 7 asin 8 sqrt 9 div(x,y) 10 atan. */
+int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uint32_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

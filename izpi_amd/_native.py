@@ -1,0 +1,174 @@
+"""ctypes view of the C ABI in include/izpi_gpu.h and include/izpi_host.h.
+
+The structures below mirror the headers field for field; tests/test_abi.py checks
+their sizes against the compiled library's expectations. Loading fails loudly when
+the native library is missing: there is no Python fallback for the hot path.
+"""
+import ctypes as C
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB_PATH = ROOT / "izpi_amd" / "_lib" / "libizpi_gpu.so"
+
+c_double_p = C.POINTER(C.c_double)
+c_uint32_p = C.POINTER(C.c_uint32)
+c_float_p = C.POINTER(C.c_float)
+
+# ---- include/izpi_types.h
+IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE = range(6)
+IZPI_ABI_VERSION = 1
+PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
+TEX_CONSTANT, TEX_IMAGE, TEX_SPECTRAL_GAUSSIAN, TEX_SPECTRAL_TABULATED = 1, 3, 5, 7
+MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_LAMBERT, MAT_METAL, MAT_PBR = 1, 2, 4, 5, 6
+MATF_BEER_LAMBERT = 1
+SAMPLER_COLOUR, SAMPLER_SPECTRAL = 2, 5
+OUT_CANVAS, OUT_PACKED = 0, 1
+
+
+def prim_ref(kind, idx):
+    return (kind << 31) | idx
+
+
+class BVH4Node(C.Structure):
+    _fields_ = [("min_x", C.c_float * 4), ("min_y", C.c_float * 4), ("min_z", C.c_float * 4),
+                ("max_x", C.c_float * 4), ("max_y", C.c_float * 4), ("max_z", C.c_float * 4),
+                ("child", C.c_int32 * 4), ("prim_count", C.c_int32 * 4)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("spd_offset", C.c_uint32), ("spd_count", C.c_uint32), ("pad0", C.c_uint32),
+                ("texel_offset", C.c_uint64), ("value", C.c_double * 3),
+                ("peak", C.c_double), ("center", C.c_double), ("width_nm", C.c_double)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("albedo_tex", C.c_int32), ("spectral_tex", C.c_int32),
+                ("normal_tex", C.c_int32), ("roughness_tex", C.c_int32), ("metalness_tex", C.c_int32),
+                ("absorb_tex", C.c_int32), ("flags", C.c_uint32), ("ref_idx", C.c_double),
+                ("fuzz", C.c_double), ("rgb", C.c_double * 3), ("pad1", C.c_double)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("origin", C.c_double * 3), ("lower_left", C.c_double * 3), ("horizontal", C.c_double * 3),
+                ("vertical", C.c_double * 3), ("u", C.c_double * 3), ("v", C.c_double * 3),
+                ("lens_radius", C.c_double), ("time0", C.c_double), ("time1", C.c_double), ("exposure", C.c_double)]
+
+
+# ---- include/izpi_gpu.h
+class SceneDesc(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("num_nodes", C.c_uint32), ("num_prims", C.c_uint32),
+                ("num_tris", C.c_uint32), ("num_spheres", C.c_uint32), ("num_lights", C.c_uint32),
+                ("num_materials", C.c_uint32), ("num_textures", C.c_uint32), ("num_spd", C.c_uint32),
+                ("pad0", C.c_uint32), ("num_texels", C.c_uint64),
+                ("nodes", C.POINTER(BVH4Node)), ("prim_ref", c_uint32_p),
+                ("tri_v0", c_double_p), ("tri_v1", c_double_p), ("tri_v2", c_double_p),
+                ("tri_e1", c_double_p), ("tri_e2", c_double_p), ("tri_normal", c_double_p),
+                ("tri_tangent", c_double_p), ("tri_bitangent", c_double_p), ("tri_uv", c_double_p),
+                ("tri_area", c_double_p), ("tri_mat", c_uint32_p),
+                ("sph_center0", c_double_p), ("sph_center1", c_double_p), ("sph_time", c_double_p),
+                ("sph_radius", c_double_p), ("sph_mat", c_uint32_p),
+                ("light_ref", c_uint32_p), ("materials", C.POINTER(Material)), ("textures", C.POINTER(Texture)),
+                ("texels", c_double_p), ("spd_wavelengths", c_double_p), ("spd_values", c_double_p),
+                ("camera", Camera)]
+
+
+class RenderReq(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32),
+                ("sampler", C.c_uint32), ("out_layout", C.c_uint32), ("num_tiles", C.c_uint32),
+                ("num_bg_spd", C.c_uint32), ("tiles", c_uint32_p), ("bg_spd_wavelengths", c_double_p),
+                ("bg_spd_values", c_double_p), ("background", C.c_double * 3), ("seed", C.c_uint64)]
+
+
+class RenderStats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("sph_tests", C.c_uint64), ("light_tri_tests", C.c_uint64), ("light_sph_tests", C.c_uint64),
+                ("samples", C.c_uint64), ("kernel_ms", C.c_double), ("shade_ms", C.c_double),
+                ("total_ms", C.c_double), ("launches", C.c_uint32), ("pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+class Hit(C.Structure):
+    _fields_ = [("t", C.c_double), ("u", C.c_double), ("v", C.c_double), ("p", C.c_double * 3),
+                ("normal", C.c_double * 3), ("prim_ref", C.c_uint32), ("hit", C.c_uint32)]
+
+
+# ---- include/izpi_host.h
+class TriIn(C.Structure):
+    _fields_ = [("v0", C.c_double * 3), ("v1", C.c_double * 3), ("v2", C.c_double * 3),
+                ("uv", C.c_double * 6), ("material", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class SphereIn(C.Structure):
+    _fields_ = [("center", C.c_double * 3), ("radius", C.c_double), ("material", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class CameraIn(C.Structure):
+    _fields_ = [("look_from", C.c_double * 3), ("look_at", C.c_double * 3), ("vup", C.c_double * 3),
+                ("vfov", C.c_double), ("aspect", C.c_double), ("aperture", C.c_double), ("focus_dist", C.c_double),
+                ("time0", C.c_double), ("time1", C.c_double), ("exposure", C.c_double)]
+
+
+class SceneInput(C.Structure):
+    _fields_ = [("num_tris", C.c_uint32), ("num_spheres", C.c_uint32), ("num_materials", C.c_uint32),
+                ("num_textures", C.c_uint32), ("num_spd", C.c_uint32), ("pad0", C.c_uint32),
+                ("num_texels", C.c_uint64), ("tris", C.c_void_p), ("spheres", C.c_void_p),
+                ("materials", C.POINTER(Material)), ("textures", C.POINTER(Texture)), ("texels", c_double_p),
+                ("spd_wavelengths", c_double_p), ("spd_values", c_double_p), ("camera", CameraIn),
+                ("aspect_override", C.c_double), ("bvh_seed", C.c_uint64)]
+
+
+# Symbols include/izpi_gpu.h and include/izpi_host.h declare (checked by tests).
+EXPORTS = [
+    "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
+    "izpi_gpu_render_device", "izpi_gpu_unpack_tiles", "izpi_gpu_output_bytes", "izpi_gpu_trace",
+    "izpi_gpu_ray_aabb4", "izpi_gpu_gomath",
+    "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
+    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libizpi_gpu.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError("izpi native library missing: %s (run `python -m izpi_amd.build`)" % LIB_PATH)
+    try:  # bind to the HIP runtime torch already ships (same SONAME), not a second copy
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(str(LIB_PATH))
+    L.izpi_gpu_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    L.izpi_gpu_close.argtypes = [C.c_void_p]
+    L.izpi_gpu_last_error.argtypes = [C.c_void_p]
+    L.izpi_gpu_last_error.restype = C.c_char_p
+    L.izpi_gpu_upload_scene.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
+    L.izpi_gpu_render.argtypes = [C.c_void_p, C.POINTER(RenderReq), c_double_p, C.POINTER(RenderStats)]
+    L.izpi_gpu_render_device.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
+    L.izpi_gpu_unpack_tiles.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.c_void_p]
+    L.izpi_gpu_output_bytes.argtypes = [C.POINTER(RenderReq)]
+    L.izpi_gpu_output_bytes.restype = C.c_uint64
+    L.izpi_gpu_trace.argtypes = [C.c_void_p, c_double_p, C.c_uint32, C.POINTER(Hit)]
+    L.izpi_gpu_ray_aabb4.argtypes = [C.c_void_p, c_float_p, c_float_p, C.c_uint32, C.POINTER(C.c_uint8)]
+    L.izpi_gpu_gomath.argtypes = [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_uint32, c_double_p]
+    L.izpi_host_build_scene.argtypes = [C.POINTER(SceneInput), C.POINTER(C.c_void_p)]
+    L.izpi_host_scene_desc.argtypes = [C.c_void_p]
+    L.izpi_host_scene_desc.restype = C.POINTER(SceneDesc)
+    L.izpi_host_scene_stack_bound.argtypes = [C.c_void_p]
+    L.izpi_host_scene_stack_bound.restype = C.c_uint32
+    L.izpi_host_scene_build_ms.argtypes = [C.c_void_p]
+    L.izpi_host_scene_build_ms.restype = C.c_double
+    L.izpi_host_scene_free.argtypes = [C.c_void_p]
+    L.izpi_host_last_error.restype = C.c_char_p
+    L.izpi_host_tiles.argtypes = [C.c_uint32, C.c_uint32, c_uint32_p, C.c_uint32]
+    L.izpi_host_tiles.restype = C.c_uint32
+    L.izpi_host_gomath.argtypes = [C.c_int, C.c_double, C.c_double]
+    L.izpi_host_gomath.restype = C.c_double
+    _lib = L
+    return L

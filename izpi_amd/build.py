@@ -1,0 +1,72 @@
+"""Build the native pieces in-tree.
+
+* ``izpi_amd/_lib/libizpi_gpu.so`` — the product: gfx950 HIP kernels + C ABI
+  (include/izpi_gpu.h) + the C++ host scene producer (include/izpi_host.h).
+* ``oracle/_build/liboracle.so`` — TEST INFRASTRUCTURE only (CPU restatement).
+
+Both are compiled with ``-ffp-contract=off`` and without fast-math so that every
+``a*b+c`` rounds twice on host and device alike (Go on amd64 emits no FMA).
+"""
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "izpi_amd" / "csrc"
+LIBDIR = ROOT / "izpi_amd" / "_lib"
+LIB = LIBDIR / "libizpi_gpu.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "_build" / "liboracle.so"
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
+SOURCES = [CSRC / "izpi_gpu.hip", CSRC / "host_scene.cpp"]
+DEPS = SOURCES + [CSRC / "izpi_dev.h", CSRC / "gomath.h", CSRC / "cie_tables.h",
+                  ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h", ROOT / "include" / "izpi_types.h"]
+
+
+def _stale(target, deps):
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build_gpu(force=False, verbose=True):
+    if not force and not _stale(LIB, DEPS):
+        return LIB
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, "--offload-arch=%s" % ARCH, *COMMON_FLAGS, "-shared", "-o", str(tmp), *map(str, SOURCES)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force=False, verbose=True):
+    deps = [ORACLE_DIR / "izpi_oracle.cpp", ORACLE_DIR / "go_math_ref.h", ORACLE_DIR / "cie_tables_ref.h",
+            ROOT / "include" / "izpi_host.h", ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_types.h"]
+    if not force and not _stale(ORACLE_LIB, deps):
+        return ORACLE_LIB
+    make = shutil.which("make")
+    cmd = [make, "-C", str(ORACLE_DIR)] + (["-B"] if force else [])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, stdout=None if verbose else subprocess.DEVNULL)
+    return ORACLE_LIB
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    force = "--force" in argv
+    build_gpu(force=force)
+    build_oracle(force=force)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,236 @@
+// izpi_dev.h — device-side data layouts and per-lane primitives of the gfx950
+// path-tracing inner loop. Included only by izpi_gpu.hip.
+//
+// HBM layout (DESIGN.md §Data layout):
+//   GInner  128 B  inner BVH4 nodes: SoA f32 bounds of 4 children + encoded child refs.
+//                  (== hitable.BVH4Node, bvh4.go:23-39, with PrimitiveCount — always 0 in
+//                  inner nodes — replaced by nothing; leaf children become leaf refs).
+//   GLeaf   32 B   one per reference leaf node: its slot-0 bounds + primitive range.
+//                  A reference leaf node carries only slot 0 (bvh4.go:736-760), so the
+//                  re-test on visit (quirk A10) needs 32 B instead of a 128 B node load.
+//   GPrim   80 B   primitives in BVH leaf order: triangle v0,e1,e2 (the 72 B Hit reads,
+//                  triangle.go:198-218) or sphere c0,c1,r,t0,t1; + kind/index.
+//   shading data (normals, UVs, materials) stays in transport order and is read once per
+//   closest hit, after traversal (deferred hit record).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/izpi_gpu.h"
+#include "gomath.h"
+
+#define IZPI_DEV __device__ __forceinline__
+
+namespace izd {
+
+// child ref encoding inside GInner / the traversal stack
+//   r >= 0 : inner node index;   r == -1 : empty slot;   r <= -2 : leaf id (-r - 2)
+__host__ __device__ inline bool ref_is_leaf(int32_t r) { return r <= -2; }
+__host__ __device__ inline int32_t leaf_id(int32_t r) { return -r - 2; }
+
+struct alignas(16) GInner {
+  float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
+  int32_t child[4];
+  int32_t pad[4];
+};
+struct alignas(16) GLeaf {
+  float mn[3], mx[3];
+  int32_t start, count;
+};
+struct alignas(16) GPrim {
+  double a[9];      // tri: v0[3] e1[3] e2[3];  sphere: c0[3] c1[3] radius t0 t1
+  uint32_t kind;    // IZPI_PRIM_*
+  uint32_t index;   // transport-order index (shading data, lights)
+};
+// Light record (Scene.Lights entry, transport order): everything PDFValue/Random read.
+struct alignas(16) GLight {
+  double v0[3], v1[3], v2[3], e1[3], e2[3], n[3];  // triangle
+  double area;
+  double c0[3], c1[3], radius, t0, t1;             // sphere
+  uint32_t kind, index;
+};
+
+struct DevScene {
+  const GInner* inner;
+  const GLeaf* leaves;
+  const GPrim* prims;
+  const double* tri_normal;     // [nt][3]
+  const double* tri_uv;         // [nt][6]
+  const double* tri_tangent;    // [nt][3]
+  const double* tri_bitangent;  // [nt][3]
+  const uint32_t* tri_mat;
+  const uint32_t* sph_mat;
+  const GLight* lights;
+  const izpi_material* materials;
+  const izpi_texture* textures;
+  const uint32_t* mat_flags;    // per material: bit0 needs hit-record UVs (image textures)
+  const double* texels;
+  const double* spd_wl;
+  const double* spd_val;
+  int32_t root;                 // encoded ref of BVH4.Nodes[0]; -1 when empty
+  uint32_t num_lights;
+  izpi_camera cam;
+};
+
+struct RenderParams {
+  uint32_t width, height, spp, max_depth;
+  uint32_t chunk_spp;       // samples per pixel in this launch
+  uint32_t s0;              // first sample index of this launch
+  uint32_t num_pixels;      // pixels in the request
+  uint32_t tile_w, tile_h;  // all tiles equal-sized
+  uint32_t total_units;     // num_pixels * chunk_spp
+  uint32_t lanes;           // gridDim.x * blockDim.x
+  uint32_t num_bg_spd;
+  const uint32_t* tiles;    // [n][4]
+  const double* bg_wl;
+  const double* bg_val;
+  double background[3];
+  uint64_t seed;
+  double* out;              // [total_units][3] per-sample result
+  double* recs;             // [max_depth][6][lanes] unwinding records
+  uint32_t* head;           // work queue head
+  unsigned long long* counters;  // 6 counters
+  uint32_t* error;          // device-side guard flag
+};
+
+// ---------------------------------------------------------------- RNG
+// fastrandom.LCG (fastrandom.go:41-47): state = (a*state + c) mod 2^32 — with a
+// 64-bit seed the first step already reduces mod 2^32, so a uint32 state is exact.
+struct Lcg {
+  uint32_t s;
+  IZPI_DEV double next() {
+    s = 1664525u * s + 1013904223u;
+    return (double)s / 4294967296.0;
+  }
+};
+IZPI_DEV uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+#define IZPI_CAMERA_STREAM_SALT 0xD6E8FEB86659FD93ull
+
+// Go int(float64) on amd64 (CVTTSD2SQ): NaN / out of range -> INT64_MIN.
+IZPI_DEV int64_t go_int(double x) {
+  if (x != x || x >= 9223372036854775808.0 || x < -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)x;
+}
+
+// ------------------------------------------------------------- vec3
+struct V3 { double x, y, z; };
+IZPI_DEV V3 mk(double x, double y, double z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+IZPI_DEV V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
+IZPI_DEV V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+IZPI_DEV V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+IZPI_DEV V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+IZPI_DEV V3 smul(V3 a, double t) { return mk(a.x * t, a.y * t, a.z * t); }
+IZPI_DEV V3 sdiv(V3 a, double t) { return mk(a.x / t, a.y / t, a.z / t); }
+IZPI_DEV double dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+IZPI_DEV V3 cross(V3 a, V3 b) { return mk((a.y * b.z) - (a.z * b.y), -((a.x * b.z) - (a.z * b.x)), (a.x * b.y) - (a.y * b.x)); }
+IZPI_DEV double sqlen(V3 a) { return (a.x * a.x) + (a.y * a.y) + (a.z * a.z); }
+IZPI_DEV double length(V3 a) { return gm::sqrt(sqlen(a)); }
+IZPI_DEV V3 unit(V3 a) { return sdiv(a, length(a)); }
+IZPI_DEV V3 lerp(V3 a, V3 b, double t) {
+  return mk((1 - t) * a.x + t * b.x, (1 - t) * a.y + t * b.y, (1 - t) * a.z + t * b.z);
+}
+IZPI_DEV bool bad(double x) { return x != x || gm::is_inf(x, 0); }
+IZPI_DEV V3 denan(V3 v) { return mk(bad(v.x) ? 0.0 : v.x, bad(v.y) ? 0.0 : v.y, bad(v.z) ? 0.0 : v.z); }
+
+// onb.go:38-67
+struct Onb {
+  V3 u, v, w;
+  IZPI_DEV void build(V3 n) {
+    w = unit(n);
+    V3 a = gm::abs(w.x) > 0.9 ? mk(0, 1, 0) : mk(1, 0, 0);
+    v = unit(cross(w, a));
+    u = cross(w, v);
+  }
+  IZPI_DEV V3 local(V3 a) const { return add(add(smul(u, a.x), smul(v, a.y)), smul(w, a.z)); }
+};
+
+// vec3.go:119-138
+IZPI_DEV V3 random_cosine_direction(Lcg& r) {
+  double r1 = r.next();
+  double r2 = r.next();
+  double z = gm::sqrt(1 - r2);
+  double phi = 6.283185307179586 * r1;   // 2*math.Pi folded by the Go compiler
+  double x = gm::cos(phi) * 2 * gm::sqrt(r2);
+  double y = gm::sin(phi) * 2 * gm::sqrt(r2);
+  return mk(x, y, z);
+}
+IZPI_DEV V3 random_to_sphere(double radius, double dist2, Lcg& r) {
+  double r1 = r.next();
+  double r2 = r.next();
+  double z = 1 + r2 * (gm::sqrt(1 - radius * radius / dist2) - 1);
+  double phi = 6.283185307179586 * r1;
+  double x = gm::cos(phi) * gm::sqrt(1 - z * z);
+  double y = gm::sin(phi) * gm::sqrt(1 - z * z);
+  return mk(x, y, z);
+}
+// material.go:10-18
+IZPI_DEV V3 random_in_unit_sphere(Lcg& r) {
+  for (;;) {
+    double x = r.next(), y = r.next(), z = r.next();
+    V3 p = sub(smul(mk(x, y, z), 2.0), mk(1.0, 1.0, 1.0));
+    if (sqlen(p) < 1.0) return p;
+  }
+}
+
+// --------------------------------------------------- RayAABB4 (bvh4_simd_generic.go)
+// Comparisons written as the scalar twin's select form: never fminf/fmaxf (A14).
+IZPI_DEV float max32(float a, float b) { return a > b ? a : b; }
+IZPI_DEV float min32(float a, float b) { return a < b ? a : b; }
+IZPI_DEV bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float ox, float oy, float oz,
+                   float ix, float iy, float iz, float tmax) {
+  float t0x = (mnx - ox) * ix, t1x = (mxx - ox) * ix;
+  if (t0x > t1x) { float t = t0x; t0x = t1x; t1x = t; }
+  float t0y = (mny - oy) * iy, t1y = (mxy - oy) * iy;
+  if (t0y > t1y) { float t = t0y; t0y = t1y; t1y = t; }
+  float t0z = (mnz - oz) * iz, t1z = (mxz - oz) * iz;
+  if (t0z > t1z) { float t = t0z; t0z = t1z; t1z = t; }
+  float tn = max32(max32(t0x, t0y), t0z);
+  float tf = min32(min32(t1x, t1y), t1z);
+  return tn <= tf && tf >= 0 && tn <= tmax;
+}
+
+// ----------------------------------------------------- primitive tests
+// Möller–Trumbore acceptance of Triangle.Hit (triangle.go:193-221).
+IZPI_DEV bool tri_intersect(const double* a, V3 o, V3 d, double tmin, double tmax, double& t, double& u, double& v) {
+  const double eps = 1e-8;
+  V3 v0 = mk(a[0], a[1], a[2]), e1 = mk(a[3], a[4], a[5]), e2 = mk(a[6], a[7], a[8]);
+  V3 h = cross(d, e2);
+  double aa = dot(e1, h);
+  if (gm::abs(aa) < eps) return false;
+  double f = 1.0 / aa;
+  V3 s = sub(o, v0);
+  u = f * dot(s, h);
+  if (u < -eps || u > 1.0 + eps) return false;
+  V3 q = cross(s, e1);
+  v = f * dot(d, q);
+  if (v < -eps || u + v > 1.0 + eps) return false;
+  t = f * dot(e2, q);
+  if (t < tmin || t > tmax) return false;
+  return true;
+}
+// Sphere.center (sphere.go:495-497)
+IZPI_DEV V3 sph_center(const double* a, double time) {
+  V3 c0 = mk(a[0], a[1], a[2]), c1 = mk(a[3], a[4], a[5]);
+  return add(c0, smul(sub(c1, c0), ((time - a[7]) / (a[8] - a[7]))));
+}
+// Sphere.Hit acceptance (sphere.go:63-95): root 0 or 1; strict bounds.
+IZPI_DEV bool sph_intersect(const double* a, V3 o, V3 d, double time, double tmin, double tmax, double& t, int& root) {
+  V3 oc = sub(o, sph_center(a, time));
+  double aa = dot(d, d);
+  double b = dot(oc, d);
+  double c = dot(oc, oc) - (a[6] * a[6]);
+  double disc = (b * b) - (aa * c);
+  if (disc > 0) {
+    double temp = (-b - gm::sqrt(b * b - aa * c)) / aa;
+    if (temp < tmax && temp > tmin) { t = temp; root = 0; return true; }
+    temp = (-b + gm::sqrt(b * b - aa * c)) / aa;
+    if (temp < tmax && temp > tmin) { t = temp; root = 1; return true; }
+  }
+  return false;
+}
+
+}  // namespace izd

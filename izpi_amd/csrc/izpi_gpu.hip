@@ -1,0 +1,1559 @@
+// izpi_gpu.hip — MI355X (gfx950) path-tracing inner loop for izpi + its C ABI.
+//
+// Hot path restated as device code (reference files under /root/reference/internal):
+//   render/rgb.go:27-41, render/spectral.go:71-106   per-sample loop   -> k_render + k_accumulate
+//   camera/camera.go:61-89                           GetRay            -> camera_ray()
+//   sampler/colour.go:33-65, sampler/spectral.go:47-80  recursive sampler -> iterative bounce loop
+//                                                    with an explicit unwinding record per bounce
+//   hitable/bvh4.go:49-164                           BVH4.Hit          -> traverse()
+//   hitable/bvh4_simd_generic.go:10-52               RayAABB4          -> izd::slab()
+//   hitable/triangle.go:193-280,317-326, sphere.go:63-145  prims, PDFValue, Random
+//   material/*.go, pdf/*.go, texture/*.go, spectral/spectral.go:151-253
+//
+// Execution scheme: one persistent launch per chunk of samples.
+// Work unit = one pixel-sample path (its own LCG streams). Each wave keeps 64 paths
+// in flight; when a lane's path terminates it writes its radiance and the wave
+// refills idle lanes from a global atomic queue (__ballot + mbcnt compaction), so
+// SIMD lanes stay busy across samples of different lengths. Traversal stacks live in
+// LDS ([entry][lane] layout, conflict-free at equal depth). A second, HBM-bound
+// kernel sums the per-sample radiance of each pixel in sample order (bit-exact with
+// render/rgb.go:36's sequential col += ...) and writes the canvas.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/izpi_host.h"
+#include "izpi_dev.h"
+#include "cie_tables.h"
+
+using namespace izd;
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);                    \
+      return IZPI_ERR_HIP;                                                             \
+    }                                                                                  \
+  } while (0)
+
+__constant__ double c_cie_wl[IZPI_CIE_N] = IZPI_CIE_WAVELENGTHS_INIT;
+__constant__ double c_cie_x[IZPI_CIE_N] = IZPI_CIE_X_INIT;
+__constant__ double c_cie_y[IZPI_CIE_N] = IZPI_CIE_Y_INIT;
+__constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
+
+enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_N };
+
+
+// ======================================================= textures / spectra
+// texture.Constant / texture.ImageTxt (constant.go:20, image.go:73-101)
+IZPI_DEV V3 tex_rgb(const DevScene& sc, int32_t id, double u, double v) {
+  const izpi_texture& t = sc.textures[id];
+  if (t.kind == IZPI_TEX_IMAGE) {
+    int64_t i = go_int(u * (double)t.width);
+    int64_t j = go_int((1 - v) * ((double)t.height - 0.001));
+    if (i < 0) i = 0;
+    if (j < 0) j = 0;
+    if (i > (int64_t)t.width - 1) i = (int64_t)t.width - 1;
+    if (j > (int64_t)t.height - 1) j = (int64_t)t.height - 1;
+    const double* px = sc.texels + t.texel_offset + ((uint64_t)j * t.width + (uint64_t)i) * 4;
+    return mk(px[0], px[1], px[2]);
+  }
+  return mk(t.value[0], t.value[1], t.value[2]);
+}
+// texture.SpectralConstant.Value (spectral_constant.go:65-106)
+IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda) {
+  const izpi_texture& t = sc.textures[id];
+  if (t.kind == IZPI_TEX_SPECTRAL_TABULATED) {
+    const double* wl = sc.spd_wl + t.spd_offset;
+    const double* vl = sc.spd_val + t.spd_offset;
+    uint32_t n = t.spd_count;
+    if (n == 0) return 0.0;
+    if (lambda < wl[0]) return vl[0];
+    if (lambda > wl[n - 1]) return vl[n - 1];
+    for (uint32_t i = 0; i + 1 < n; i++) {
+      double w1 = wl[i], w2 = wl[i + 1];
+      if (lambda >= w1 && lambda <= w2) {
+        double tt = (lambda - w1) / (w2 - w1);
+        return vl[i] + tt * (vl[i + 1] - vl[i]);
+      }
+    }
+    return 0.0;
+  }
+  double exponent = -gm::pow((lambda - t.center) / t.width_nm, 2);
+  return t.peak * gm::exp(exponent);
+}
+// SpectralPowerDistribution.Value (spectral.go:151-181)
+IZPI_DEV double spd_value(const double* wl, const double* vl, uint32_t n, double w) {
+  if (n == 0) return 0.0;
+  if (w <= wl[0]) return vl[0];
+  if (w >= wl[n - 1]) return vl[n - 1];
+  for (uint32_t i = 0; i + 1 < n; i++) {
+    double w1 = wl[i], w2 = wl[i + 1];
+    if (w >= w1 && w <= w2) {
+      double t = (w - w1) / (w2 - w1);
+      return vl[i] + t * (vl[i + 1] - vl[i]);
+    }
+  }
+  return 0.0;
+}
+// spectral.SampleWavelength (spectral.go:184-224)
+IZPI_DEV void sample_wavelength(double random, double& lambda, double& pdf) {
+  double target = random * IZPI_CIE_Y_INTEGRAL;
+  double current = 0.0;
+  for (int i = 0; i < IZPI_CIE_N; i++) {
+    double y = c_cie_y[i];
+    if (current + y >= target) {
+      if (i > 0) {
+        double prev = current;
+        double t = (target - prev) / y;
+        lambda = c_cie_wl[i - 1] + t * (c_cie_wl[i] - c_cie_wl[i - 1]);
+        double iy = c_cie_y[i - 1] + t * (c_cie_y[i] - c_cie_y[i - 1]);
+        pdf = iy / IZPI_CIE_Y_INTEGRAL;
+        return;
+      }
+      lambda = c_cie_wl[i];
+      pdf = y / IZPI_CIE_Y_INTEGRAL;
+      return;
+    }
+    current += y;
+  }
+  lambda = 750;
+  pdf = c_cie_y[IZPI_CIE_N - 1] / IZPI_CIE_Y_INTEGRAL;
+}
+// spectral.GetCIEValues (spectral.go:227-253)
+IZPI_DEV void cie_values(double w, double& x, double& y, double& z) {
+  if (w <= c_cie_wl[0]) { x = c_cie_x[0]; y = c_cie_y[0]; z = c_cie_z[0]; return; }
+  if (w >= c_cie_wl[IZPI_CIE_N - 1]) { x = c_cie_x[IZPI_CIE_N - 1]; y = c_cie_y[IZPI_CIE_N - 1]; z = c_cie_z[IZPI_CIE_N - 1]; return; }
+  int index = 0;
+  for (int i = 0; i < IZPI_CIE_N; i++) if (c_cie_wl[i] >= w) { index = i; break; }
+  double w1 = c_cie_wl[index - 1], w2 = c_cie_wl[index];
+  double t = (w - w1) / (w2 - w1);
+  x = c_cie_x[index - 1] + t * (c_cie_x[index] - c_cie_x[index - 1]);
+  y = c_cie_y[index - 1] + t * (c_cie_y[index] - c_cie_y[index - 1]);
+  z = c_cie_z[index - 1] + t * (c_cie_z[index] - c_cie_z[index - 1]);
+}
+
+// ============================================================ wavefront state
+// Per-slot records in HBM (AoS, 16-B aligned so each is a few dwordx4 accesses).
+struct alignas(16) RayRec {   // the ray a slot wants traced next
+  double o[3], d[3];
+  double tmin, tmax, time;
+  uint32_t kind;              // RAY_MAIN (counts as a Sampler call) / RAY_PATHLEN
+  uint32_t pad;
+};
+struct alignas(16) HitOut {   // closest hit of that ray (deferred record)
+  double t, u, v;             // triangle barycentrics, or u = sphere root
+  int32_t prim;               // leaf-order primitive, -1 = miss
+  uint32_t pad;
+};
+struct alignas(16) PathSt {   // sampler state of the pixel-sample in this slot
+  double lambda, lpdf;        // wavelength and its pdf (spectral)
+  double pend[3];             // dielectric hit point while its path-length ray is traced
+  uint32_t rng, depth, unit, pad;
+};
+enum { RAY_MAIN = 0, RAY_PATHLEN = 1 };
+
+struct WaveParams {
+  RayRec* rays;
+  HitOut* hits;
+  PathSt* paths;
+  const uint32_t* q_in;       // slots to process this pass
+  const uint32_t* q_in_count;
+  uint32_t* q_out;            // slots whose next ray must be traced
+  uint32_t* q_out_count;
+  uint32_t* trace_next;       // dynamic-fetch cursor of k_trace
+  uint32_t slots;
+};
+
+// ============================================================ traversal
+// BVH4.Hit (bvh4.go:49-164) as a persistent dynamic-fetch kernel: each lane owns one
+// ray; every loop iteration visits one node per lane; finished lanes are refilled from
+// the queue in wave-sized batches (__ballot + popcount prefix) so SIMD lanes stay busy
+// while traversal lengths differ. Visit order, leaf re-test (A10), equal-t acceptance
+// (A11) and the float32 box test (A15) follow the reference exactly.
+template <int STACK>
+__global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WaveParams wp, unsigned long long* counters,
+                                               uint32_t* err) {
+  __shared__ int32_t lds_stack[STACK * 256];
+  int32_t* stk = lds_stack + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t n = *wp.q_in_count;
+  uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
+  bool busy = false, exhausted = false;
+  uint32_t slot = 0;
+  V3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+  double tmin = 0, tmax = 0, time = 0;
+  float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
+  int32_t cur = -1;
+  int sp = 0;
+  double bt = 0, bu = 0, bv = 0;
+  int32_t bprim = -1;
+  for (;;) {
+    const uint64_t idle = __ballot(!busy);
+    if (idle != 0) {
+      const uint32_t nidle = (uint32_t)__popcll(idle);
+      if (!exhausted && (nidle >= 16 || idle == ~0ull)) {
+        const uint32_t leader = (uint32_t)__ffsll((long long)idle) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(wp.trace_next, nidle);
+        base = __shfl(base, (int)leader);
+        if (base + nidle >= n) exhausted = true;
+        if (!busy) {
+          const uint32_t my = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
+          if (my < n) {
+            slot = wp.q_in[my];
+            const RayRec& r = wp.rays[slot];
+            o = mk(r.o[0], r.o[1], r.o[2]);
+            d = mk(r.d[0], r.d[1], r.d[2]);
+            tmin = r.tmin; tmax = r.tmax; time = r.time;
+            if (r.kind == RAY_MAIN) c_rays++;
+            ix = (float)(1.0 / d.x); iy = (float)(1.0 / d.y); iz = (float)(1.0 / d.z);
+            ox = (float)o.x; oy = (float)o.y; oz = (float)o.z;
+            cur = sc.root;
+            sp = 0;
+            bprim = -1;
+            busy = cur != -1;
+            if (!busy) { HitOut& h = wp.hits[slot]; h.prim = -1; }
+          }
+        }
+      } else if (exhausted && idle == ~0ull) {
+        break;
+      }
+    }
+    if (!busy) continue;
+    // ---- one node visit
+    c_nodes++;
+    const float tm = (float)tmax;
+    int32_t next = -1;
+    if (ref_is_leaf(cur)) {
+      const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_id(cur));
+      const float4 a = lp[0], b = lp[1];
+      if (slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
+        const int32_t start = __float_as_int(b.z), count = __float_as_int(b.w);
+        for (int32_t k = start; k < start + count; k++) {
+          const double2* pp = reinterpret_cast<const double2*>(sc.prims + k);
+          const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
+          const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
+          const uint32_t kind = (uint32_t)__double2loint(p4.y);
+          if (kind == IZPI_PRIM_TRIANGLE) {
+            c_tri++;
+            double t, u, v;
+            if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) { tmax = t; bt = t; bu = u; bv = v; bprim = k; }
+          } else {
+            c_sph++;
+            double t; int root;
+            if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) { tmax = t; bt = t; bu = (double)root; bv = 0; bprim = k; }
+          }
+        }
+      }
+    } else {
+      const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
+      const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
+      const int4 ch = *reinterpret_cast<const int4*>(np + 6);
+      const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
+                  amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
+                  amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+      const int32_t ach[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (ach[i] == -1) continue;
+        if (!slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) continue;
+        if (next == -1) {
+          next = ach[i];
+        } else if (sp < STACK) {
+          stk[sp * 256] = ach[i];
+          sp++;
+        } else {
+          atomicOr(err, 1u);  // unreachable: STACK >= host-computed bound
+        }
+      }
+    }
+    if (next != -1) {
+      cur = next;
+    } else if (sp > 0) {
+      sp--;
+      cur = stk[sp * 256];
+    } else {
+      HitOut h;
+      h.t = bt; h.u = bu; h.v = bv; h.prim = bprim; h.pad = 0;
+      wp.hits[slot] = h;
+      busy = false;
+    }
+  }
+  unsigned long long vals[4] = {c_rays, c_nodes, c_tri, c_sph};
+  const int idx[4] = {CNT_RAYS, CNT_NODES, CNT_TRI, CNT_SPH};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    unsigned long long s = vals[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+    if (lane == 0 && s) atomicAdd(counters + idx[i], s);
+  }
+}
+
+// Full hit record of the closest primitive (triangle.go:223-264, sphere.go:71-92).
+struct HitRec {
+  double t, u, v;
+  V3 p, n;
+  uint32_t mat;
+};
+IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, V3 o, V3 d, double time, bool want_uv, HitRec& h) {
+  const GPrim& pr = sc.prims[c.prim];
+  h.t = c.t;
+  h.p = add(o, smul(d, c.t));
+  if (pr.kind == IZPI_PRIM_TRIANGLE) {
+    const uint32_t ti = pr.index;
+    const double eps = 1e-8;
+    double u = c.u, v = c.v;
+    double w = 1.0 - u - v;
+    double sum = u + v + w;
+    if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
+    const double* uv = sc.tri_uv + 6 * (size_t)ti;  // u0,v0,u1,v1,u2,v2
+    h.u = w * uv[0] + u * uv[2] + v * uv[4];
+    h.v = w * uv[1] + u * uv[3] + v * uv[5];
+    h.mat = sc.tri_mat[ti];
+    V3 n = ld3(sc.tri_normal + 3 * (size_t)ti);
+    const izpi_material& m = sc.materials[h.mat];
+    if (m.kind == IZPI_MAT_PBR && m.normal_tex >= 0) {  // Material.NormalMap() != nil
+      V3 nts = tex_rgb(sc, m.normal_tex, h.u, h.v);
+      nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
+      V3 tg = ld3(sc.tri_tangent + 3 * (size_t)ti), bt = ld3(sc.tri_bitangent + 3 * (size_t)ti);
+      V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
+                 tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
+      n = sdiv(nn, length(nn));
+    }
+    h.n = n;
+  } else {
+    double pa[9];
+    for (int q = 0; q < 9; q++) pa[q] = pr.a[q];
+    V3 ctr = sph_center(pa, time);
+    V3 on = sdiv(sub(h.p, ctr), pa[6]);
+    V3 flipped = dot(d, on) >= 0 ? smul(on, -1) : on;
+    h.n = c.u == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
+    h.mat = sc.sph_mat[pr.index];
+    if (want_uv) {
+      double phi = gm::atan2(flipped.z, flipped.x);
+      double theta = gm::asin(flipped.y);
+      h.u = 1.0 - (phi + 3.141592653589793) / (2.0 * 3.141592653589793);
+      h.v = (theta + 3.141592653589793 / 2.0) / 3.141592653589793;
+    } else {
+      h.u = 0; h.v = 0;  // no texture of this material reads (u,v)
+    }
+  }
+}
+
+// ================================================================ lights
+// HitableSlice.PDFValue over Scene.Lights (hitable_slice.go:98-105) with
+// Triangle.PDFValue (triangle.go:271-280) / Sphere.PDFValue (sphere.go:129-137).
+IZPI_DEV double lights_pdf(const DevScene& sc, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
+  const double weight = 1.0 / (double)sc.num_lights;
+  double sum = 0;
+  for (uint32_t i = 0; i < sc.num_lights; i++) {
+    const GLight& L = sc.lights[i];
+    double pdf = 0;
+    if (L.kind == IZPI_PRIM_TRIANGLE) {
+      c_lt++;
+      const double a[9] = {L.v0[0], L.v0[1], L.v0[2], L.e1[0], L.e1[1], L.e1[2], L.e2[0], L.e2[1], L.e2[2]};
+      double t, u, w;
+      if (tri_intersect(a, o, v, 0.001, 1.7976931348623157e308, t, u, w)) {
+        double dist2 = t * t * sqlen(v);
+        double cosine = gm::abs(dot(v, sdiv(ld3(L.n), length(v))));
+        pdf = dist2 / (cosine * L.area);
+      }
+    } else {
+      c_ls++;
+      const double a[9] = {L.c0[0], L.c0[1], L.c0[2], L.c1[0], L.c1[1], L.c1[2], L.radius, L.t0, L.t1};
+      double t; int root;
+      if (sph_intersect(a, o, v, 0.0, 0.001, 1.7976931348623157e308, t, root)) {
+        double cosThetaMax = gm::sqrt(1 - L.radius * L.radius / sqlen(sub(ld3(L.c0), o)));
+        double solidAngle = 6.283185307179586 * (1 - cosThetaMax);
+        pdf = 1 / solidAngle;
+      }
+    }
+    sum += weight * pdf;
+  }
+  return sum;
+}
+// HitableSlice.Random (hitable_slice.go:107-110) + Triangle/Sphere.Random
+IZPI_DEV V3 lights_random(const DevScene& sc, V3 o, Lcg& rng) {
+  int64_t index = go_int(rng.next() * (double)sc.num_lights);
+  const GLight& L = sc.lights[index];
+  if (L.kind == IZPI_PRIM_TRIANGLE) {
+    double t1 = rng.next();
+    V3 p01 = lerp(ld3(L.v0), ld3(L.v1), t1);
+    double t2 = rng.next();
+    V3 p02 = lerp(ld3(L.v0), ld3(L.v2), t2);
+    double t3 = rng.next();
+    return sub(lerp(p01, p02, t3), o);
+  }
+  V3 dir = sub(ld3(L.c0), o);
+  double dist2 = sqlen(dir);
+  Onb uvw;
+  uvw.build(dir);
+  return uvw.local(random_to_sphere(L.radius, dist2, rng));
+}
+
+// ============================================================== materials
+IZPI_DEV V3 reflect(V3 v, V3 n) { return sub(v, smul(n, 2 * dot(v, n))); }
+IZPI_DEV bool refract(V3 v, V3 n, double ni, V3& out) {
+  V3 uv = unit(v);
+  double dt = dot(uv, n);
+  double disc = 1.0 - ni * ni * (1 - dt * dt);
+  if (disc > 0) {
+    out = sub(smul(sub(uv, smul(n, dt)), ni), smul(n, gm::sqrt(disc)));
+    return true;
+  }
+  return false;
+}
+IZPI_DEV double schlick(double cosine, double ri) {
+  double r0 = (1.0 - ri) / (1.0 + ri);
+  r0 = r0 * r0;
+  return r0 + (1.0 - r0) * gm::pow((1.0 - cosine), 5);
+}
+// Dielectric.scatterCommon (dielectric.go:66-102): returns the scattered direction.
+IZPI_DEV V3 dielectric_scatter(V3 d, V3 n, double ri, Lcg& rng, bool& reflected_out) {
+  V3 reflected = reflect(d, n);
+  V3 outward;
+  double ni, cosine, prob;
+  if (dot(d, n) > 0) {
+    outward = smul(n, -1.0);
+    ni = ri;
+    cosine = ri * dot(d, n) / length(d);
+  } else {
+    outward = n;
+    ni = 1.0 / ri;
+    cosine = -dot(d, n) / length(d);
+  }
+  V3 refracted = mk(0, 0, 0);
+  if (refract(d, outward, ni, refracted)) prob = schlick(cosine, ri);
+  else prob = 1.0;
+  if (rng.next() < prob) { reflected_out = true; return reflected; }
+  reflected_out = false;
+  return refracted;
+}
+
+// ============================================================ shading
+struct ShadeParams {
+  uint32_t width, height, max_depth;
+  uint32_t chunk_spp, s0, tile_w, tile_h, total_units;
+  uint32_t num_bg_spd, slots;
+  const uint32_t* tiles;
+  const double* bg_wl;
+  const double* bg_val;
+  double background[3];
+  uint64_t seed;
+  double* out;                 // [total_units][3] per-sample result
+  double* recs;                // [max_depth][6][slots] unwinding records
+  uint32_t* head;              // next work unit
+  unsigned long long* counters;
+  uint32_t* error;
+};
+
+template <int SAMPLER>
+IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t depth, bool spec, V3 att, double s, double p) {
+  double* r = sp.recs + (size_t)depth * 6 * sp.slots + slot;
+  const size_t L = sp.slots;
+  r[0] = spec ? 1.0 : 0.0;
+  r[L] = att.x;
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) { r[2 * L] = att.y; r[3 * L] = att.z; }
+  if (!spec) { r[4 * L] = s; r[5 * L] = p; }
+}
+
+// Write the finished path's radiance after unwinding the recursion of
+// colour.go:80-94 / sampler/spectral.go:161-174 from depth-1 down to 0.
+template <int SAMPLER>
+IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L) {
+  const size_t Ls = sp.slots;
+  for (int dd = (int)P.depth - 1; dd >= 0; dd--) {
+    const double* r = sp.recs + (size_t)dd * 6 * Ls + slot;
+    const bool spec = r[0] != 0.0;
+    if (SAMPLER == IZPI_SAMPLER_COLOUR) {
+      V3 att = mk(r[Ls], r[2 * Ls], r[3 * Ls]);
+      if (spec) {
+        L = mul(att, L);                                   // vec3.Mul(att, Sample(...))
+      } else {
+        const double s = r[4 * Ls], p = r[5 * Ls];
+        V3 v1 = smul(L, s);                                // ScalarMul(Sample(...), ScatteringPDF)
+        V3 v2 = mul(att, v1);
+        V3 v3 = sdiv(v2, p);
+        L = mk(0.0 + v3.x, 0.0 + v3.y, 0.0 + v3.z);        // Add(emitted == 0, v3)
+      }
+    } else {
+      const double att = r[Ls];
+      if (spec) {
+        L.x = att * L.x;
+      } else {
+        const double s = r[4 * Ls], p = r[5 * Ls];
+        double v1 = L.x * s;
+        double v2 = att * v1;
+        double v3 = v2 / p;
+        L.x = 0.0 + v3;
+      }
+    }
+  }
+  double* out = sp.out + (size_t)P.unit * 3;
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) {
+    V3 c = denan(L);  // rgb.go:36 DeNAN per sample
+    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+  } else {
+    double cx, cy, cz;  // render/spectral.go:162-166
+    cie_values(P.lambda, cx, cy, cz);
+    out[0] = (L.x * cx) / P.lpdf;
+    out[1] = (L.x * cy) / P.lpdf;
+    out[2] = (L.x * cz) / P.lpdf;
+  }
+}
+
+IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colour) {
+  // colour.go:34-36 returns blue; sampler/spectral.go:48-51 the background SPD.
+  return colour ? mk(0, 0, 1.0) : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
+}
+
+// Start the path of work unit `unit` in `slot`: per-sample LCG streams, wavelength
+// (spectral), jitter, Camera.GetRay (camera.go:61-89). Returns false when the sample
+// is already complete (spectral pdf == 0 or maxDepth == 0); its result is written.
+template <int SAMPLER>
+IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slot, uint32_t unit, PathSt& P, RayRec& R) {
+  const uint32_t pix_local = unit / sp.chunk_spp;
+  const uint32_t s = sp.s0 + unit % sp.chunk_spp;
+  const uint32_t tile_px = sp.tile_w * sp.tile_h;
+  const uint32_t tile = pix_local / tile_px, in_tile = pix_local % tile_px;
+  const uint32_t x = sp.tiles[4 * tile] + in_tile % sp.tile_w;
+  const uint32_t y = sp.tiles[4 * tile + 1] + in_tile / sp.tile_w;
+  const uint64_t key = ((uint64_t)s << 32) | (uint64_t)(y * sp.width + x);
+  Lcg rng;
+  rng.s = (uint32_t)splitmix64(sp.seed ^ key);
+  Lcg cam;
+  cam.s = (uint32_t)splitmix64(sp.seed ^ key ^ IZPI_CAMERA_STREAM_SALT);
+  P.unit = unit;
+  P.depth = 0;
+  P.lambda = 0;
+  P.lpdf = 1;
+  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) {
+    sample_wavelength(rng.next(), P.lambda, P.lpdf);
+    if (P.lpdf == 0) {  // render/spectral.go:78-80: skipped, still counted in 1/spp
+      double* out = sp.out + (size_t)unit * 3;
+      out[0] = 0; out[1] = 0; out[2] = 0;
+      return false;
+    }
+  }
+  const double u = ((double)x + rng.next()) / (double)sp.width;
+  const double v = ((double)y + rng.next()) / (double)sp.height;
+  double px, py;
+  for (;;) {  // randomInUnitDisc
+    double rx = cam.next(), ry = cam.next();
+    px = rx * 2.0 - 1.0;
+    py = ry * 2.0 - 1.0;
+    double pz = 0.0 * 2.0 - 0.0;
+    if ((px * px) + (py * py) + (pz * pz) < 1.0) break;
+  }
+  const izpi_camera& c = sc.cam;
+  const double rdx = px * c.lens_radius, rdy = py * c.lens_radius;
+  V3 offset = add(smul(ld3(c.u), rdx), smul(ld3(c.v), rdy));
+  const double time = c.time0 + cam.next() * (c.time1 - c.time0);
+  V3 origin = ld3(c.origin);
+  V3 ro = add(origin, offset);
+  V3 rd = sub(sub(add(add(ld3(c.lower_left), smul(ld3(c.horizontal), u)), smul(ld3(c.vertical), v)), origin), offset);
+  P.rng = rng.s;
+  if (sp.max_depth == 0) {
+    finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));
+    return false;
+  }
+  R.o[0] = ro.x; R.o[1] = ro.y; R.o[2] = ro.z;
+  R.d[0] = rd.x; R.d[1] = rd.y; R.d[2] = rd.z;
+  R.tmin = 0.001; R.tmax = 1.7976931348623157e308; R.time = time;
+  R.kind = RAY_MAIN; R.pad = 0;
+  return true;
+}
+
+// Append `push` lanes' slots to the output queue: one atomic per wave.
+IZPI_DEV void queue_push(const WaveParams& wp, bool push, uint32_t slot) {
+  const uint64_t m = __ballot(push);
+  if (m == 0) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(wp.q_out_count, (uint32_t)__popcll(m));
+  base = __shfl(base, (int)leader);
+  if (push) wp.q_out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = slot;
+}
+
+// Take units for the lanes that ask (one atomic per wave); returns UINT32_MAX when drained.
+IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
+  const uint64_t m = __ballot(want);
+  if (m == 0) return 0xFFFFFFFFu;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(sp.head, (uint32_t)__popcll(m));
+  base = __shfl(base, (int)leader);
+  const uint32_t my = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  return (want && my < sp.total_units) ? my : 0xFFFFFFFFu;
+}
+
+// Fill empty slots (first pass of a chunk): slot i takes new units until one needs tracing.
+template <int SAMPLER>
+__global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
+  bool want = slot < sp.slots;
+  bool push = false;
+  // a wave keeps grabbing while any of its lanes still lacks a traceable path
+  for (;;) {
+    const uint32_t unit = grab_unit(sp, want);
+    if (__ballot(want) == 0) break;
+    if (want) {
+      if (unit == 0xFFFFFFFFu) {
+        want = false;
+      } else {
+        PathSt P;
+        RayRec R;
+        if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
+          wp.paths[slot] = P;
+          wp.rays[slot] = R;
+          want = false;
+          push = true;
+        }
+      }
+    }
+  }
+  queue_push(wp, push, slot);
+}
+
+// One shading pass over the slots traced in the previous k_trace.
+template <int SAMPLER>
+__global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
+  const uint32_t n = *wp.q_in_count;
+  uint32_t c_lt = 0, c_ls = 0;
+  const uint32_t stride = gridDim.x * 256;
+  // Uniform trip count per wave so the wave-level queue/unit atomics stay convergent.
+  const uint32_t first = blockIdx.x * 256 + (threadIdx.x & ~63u);
+  for (uint32_t base = first; base < n; base += stride) {
+    const uint32_t i = base + (threadIdx.x & 63);
+    const bool valid = i < n;
+    uint32_t slot = valid ? wp.q_in[i] : 0;
+    bool push = false;      // slot has a ray to trace next
+    bool done = false;      // slot's sample finished: grab a new unit
+    if (valid) {
+      PathSt P = wp.paths[slot];
+      RayRec R = wp.rays[slot];
+      const HitOut H = wp.hits[slot];
+      Lcg rng;
+      rng.s = P.rng;
+      const V3 ro = mk(R.o[0], R.o[1], R.o[2]), rd = mk(R.d[0], R.d[1], R.d[2]);
+      V3 L = mk(0, 0, 0);
+      bool terminal = false;
+      bool spec = false, have_pdf = false;
+      V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
+      V3 hit_n = mk(0, 0, 0);
+      Onb cos_onb;
+      if (R.kind == RAY_PATHLEN) {
+        // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
+        const V3 hp = mk(P.pend[0], P.pend[1], P.pend[2]);
+        double len = 10.0;
+        if (H.prim >= 0) {
+          V3 exit_p = add(ro, smul(rd, H.t));
+          len = length(sub(exit_p, hp));
+          if (len < 0.1) len = 0.1;
+          if (len > 100.0) len = 100.0;
+        }
+        const uint32_t mat_id = (uint32_t)R.pad;  // dielectric material stashed by the glass bounce
+        const izpi_material& gm_ = sc.materials[mat_id];
+        if (COLOUR) att = mk(gm::exp(-gm_.rgb[0] * len), gm::exp(-gm_.rgb[1] * len), gm::exp(-gm_.rgb[2] * len));
+        else att.x = gm_.absorb_tex >= 0 ? gm::exp(-tex_spectral(sc, gm_.absorb_tex, P.lambda) * len) : 1.0;
+        spec = true;
+        next_o = hp;
+        next_d = rd;
+      } else if (H.prim < 0) {
+        L = COLOUR ? mk(sp.background[0], sp.background[1], sp.background[2])
+                   : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
+        terminal = true;
+      } else {
+        const GPrim& pr = sc.prims[H.prim];
+        const uint32_t mat_id = pr.kind == IZPI_PRIM_TRIANGLE ? sc.tri_mat[pr.index] : sc.sph_mat[pr.index];
+        HitRec h;
+        hit_record(sc, H, ro, rd, R.time, (sc.mat_flags[mat_id] & 1u) != 0, h);
+        hit_n = h.n;
+        next_o = h.p;
+        const izpi_material& m = sc.materials[h.mat];
+        switch (m.kind) {
+          case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
+            if (dot(h.n, rd) < 0.0) {
+              if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+              else L.x = tex_spectral(sc, m.spectral_tex, P.lambda);
+            }
+            terminal = true;
+            break;
+          }
+          case IZPI_MAT_LAMBERT: {  // lambertian.go:44-70: 2 draws for a ray the sampler discards (A6)
+            rng.next();
+            rng.next();
+            cos_onb.build(h.n);
+            if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+            else att.x = tex_spectral(sc, m.spectral_tex, P.lambda);
+            have_pdf = true;
+            break;
+          }
+          case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
+            const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
+            bool reflected;
+            next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
+            const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
+            if (!reflected && (!COLOUR || beer_rgb)) {
+              // the extra World.Hit of calculatePathLength: trace it, finish next pass
+              P.pend[0] = h.p.x; P.pend[1] = h.p.y; P.pend[2] = h.p.z;
+              P.rng = rng.s;
+              V3 start = add(h.p, smul(next_d, 0.001));
+              R.o[0] = start.x; R.o[1] = start.y; R.o[2] = start.z;
+              R.d[0] = next_d.x; R.d[1] = next_d.y; R.d[2] = next_d.z;
+              R.tmin = 0.0; R.tmax = 1000.0;
+              R.kind = RAY_PATHLEN; R.pad = h.mat;
+              wp.paths[slot] = P;
+              wp.rays[slot] = R;
+              push = true;
+              break;
+            }
+            att = mk(1.0, 1.0, 1.0);
+            spec = true;
+            break;
+          }
+          case IZPI_MAT_METAL: {  // metal.go:34-41 (RGB only: SpectralScatter is nonSpectral)
+            if (!COLOUR) { terminal = true; break; }
+            V3 reflected = reflect(unit(rd), h.n);
+            next_d = add(reflected, smul(random_in_unit_sphere(rng), m.fuzz));
+            att = mk(m.rgb[0], m.rgb[1], m.rgb[2]);
+            spec = true;
+            break;
+          }
+          case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
+            double alb_s = 0;
+            if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+            else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda);
+            else { V3 c = tex_rgb(sc, m.albedo_tex, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
+            V3 normal = h.n;
+            if (m.normal_tex >= 0) {
+              V3 nuv = tex_rgb(sc, m.normal_tex, h.u, h.v);
+              V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
+              V3 nn0 = h.n;
+              V3 t = cross(nn0, mk(0, 1, 0));
+              if (dot(t, t) < 0.001) t = cross(nn0, mk(1, 0, 0));
+              t = sdiv(t, length(t));
+              V3 b = cross(nn0, t);
+              b = sdiv(b, length(b));
+              V3 nn = mk(t.x * tn.x + b.x * tn.y + nn0.x * tn.z, t.y * tn.x + b.y * tn.y + nn0.y * tn.z,
+                         t.z * tn.x + b.z * tn.y + nn0.z * tn.z);
+              normal = sdiv(nn, length(nn));
+            }
+            V3 rough = m.roughness_tex >= 0 ? tex_rgb(sc, m.roughness_tex, h.u, h.v) : mk(0.5, 0.5, 0.5);
+            V3 metal = m.metalness_tex >= 0 ? tex_rgb(sc, m.metalness_tex, h.u, h.v) : mk(0.0, 0.0, 0.0);
+            double rv = (rough.x + rough.y + rough.z) / 3.0;
+            double mv = (metal.x + metal.y + metal.z) / 3.0;
+            Onb uvw;
+            uvw.build(normal);
+            V3 reflected = reflect(unit(rd), normal);
+            double cosTheta = gm::abs(dot(unit(rd), normal));
+            double fresnel = 0.04 + (1.0 - 0.04) * gm::pow(1.0 - cosTheta, 5.0);
+            fresnel = fresnel + (mv * 0.5);
+            double sprob = fresnel * (1.0 - rv);
+            if (rng.next() < sprob) {
+              double rf = gm::max(0.01, rv * 0.3);
+              V3 rdir = random_in_unit_sphere(rng);
+              next_d = unit(add(reflected, smul(rdir, rf)));
+              spec = true;
+            } else {
+              next_d = unit(uvw.local(random_cosine_direction(rng)));
+              spec = false;
+              have_pdf = true;  // the sampler ignores this ray and samples the mixture pdf
+            }
+            cos_onb.build(normal);
+            if (!COLOUR) att.x = spec ? alb_s * 1.5 : alb_s;
+            break;
+          }
+          default: {
+            atomicOr(sp.error, 2u);
+            terminal = true;
+          }
+        }
+      }
+      if (!push) {
+        if (terminal) {
+          finish<SAMPLER>(sp, slot, P, L);
+          done = true;
+        } else {
+          if (have_pdf) {
+            // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:85-90, mixture.go:17-33)
+            V3 dir;
+            if (rng.next() < 0.5) dir = lights_random(sc, next_o, rng);
+            else dir = cos_onb.local(random_cosine_direction(rng));
+            double cosv = dot(unit(dir), cos_onb.w);
+            double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
+            double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
+            double sc_cos = dot(hit_n, unit(dir));  // ScatteringPDF with the hit normal
+            if (sc_cos < 0) sc_cos = 0;
+            rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, pdf_val);
+            next_d = dir;
+          } else {
+            rec_store<SAMPLER>(sp, slot, P.depth, true, att, 0, 0);
+          }
+          P.depth++;
+          P.rng = rng.s;
+          if (P.depth >= sp.max_depth) {
+            finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
+            done = true;
+          } else {
+            R.o[0] = next_o.x; R.o[1] = next_o.y; R.o[2] = next_o.z;
+            R.d[0] = next_d.x; R.d[1] = next_d.y; R.d[2] = next_d.z;
+            R.tmin = 0.001; R.tmax = 1.7976931348623157e308;
+            R.kind = RAY_MAIN; R.pad = 0;
+            wp.paths[slot] = P;
+            wp.rays[slot] = R;
+            push = true;
+          }
+        }
+      }
+    }
+    // refill finished slots with new work units (wave-uniform loop)
+    bool want = done;
+    for (;;) {
+      if (__ballot(want) == 0) break;
+      const uint32_t unit = grab_unit(sp, want);
+      if (want) {
+        if (unit == 0xFFFFFFFFu) {
+          want = false;
+        } else {
+          PathSt P;
+          RayRec R;
+          if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
+            wp.paths[slot] = P;
+            wp.rays[slot] = R;
+            want = false;
+            push = true;
+          }
+        }
+      }
+    }
+    queue_push(wp, push, slot);
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long vals[2] = {c_lt, c_ls};
+  const int idx[2] = {CNT_LTRI, CNT_LSPH};
+  for (int k = 0; k < 2; k++) {
+    unsigned long long s = vals[k];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+    if (lane == 0 && s) atomicAdd(sp.counters + idx[k], s);
+  }
+}
+
+// Per-pixel sequential sum of the chunk's samples (render/rgb.go:36 col += ...,
+// render/spectral.go:164-166 sum += ...), in sample order; finalize on the last chunk.
+struct AccumParams {
+  uint32_t num_pixels, chunk_spp, spp, width, height, tile_w, tile_h, sampler, last, out_layout;
+  const uint32_t* tiles;
+  const double* samples;  // [num_pixels][chunk_spp][3]
+  double* running;        // [num_pixels][3]
+  double* out;
+};
+__global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= ap.num_pixels) return;
+  double c0 = ap.running[3 * (size_t)p], c1 = ap.running[3 * (size_t)p + 1], c2 = ap.running[3 * (size_t)p + 2];
+  const double* s = ap.samples + (size_t)p * ap.chunk_spp * 3;
+  for (uint32_t k = 0; k < ap.chunk_spp; k++) {
+    c0 = c0 + s[3 * k];
+    c1 = c1 + s[3 * k + 1];
+    c2 = c2 + s[3 * k + 2];
+  }
+  if (!ap.last) {
+    ap.running[3 * (size_t)p] = c0; ap.running[3 * (size_t)p + 1] = c1; ap.running[3 * (size_t)p + 2] = c2;
+    return;
+  }
+  double r0, r1, r2;
+  if (ap.sampler == IZPI_SAMPLER_COLOUR) {  // vec3.ScalarDiv(col, numSamples)
+    r0 = c0 / (double)ap.spp; r1 = c1 / (double)ap.spp; r2 = c2 / (double)ap.spp;
+  } else {  // sum * (1/numSamples)
+    const double inv = 1.0 / (double)ap.spp;
+    r0 = c0 * inv; r1 = c1 * inv; r2 = c2 * inv;
+  }
+  const uint32_t tile_px = ap.tile_w * ap.tile_h;
+  if (ap.out_layout == IZPI_OUT_PACKED) {
+    double* o = ap.out + (size_t)p * 4;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = 1.0;
+    return;
+  }
+  const uint32_t tile = p / tile_px, in_tile = p % tile_px;
+  const uint32_t x = ap.tiles[4 * tile] + in_tile % ap.tile_w;
+  const uint32_t y = ap.tiles[4 * tile + 1] + in_tile / ap.tile_w;
+  const uint32_t row = ap.height - y;  // canvas.Set(x, ny-y): row ny is dropped (A9)
+  if (row < ap.height) {
+    double* o = ap.out + ((size_t)row * ap.width + x) * 4;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = 1.0;
+  }
+}
+
+__global__ void k_unpack(const uint32_t* tiles, uint32_t num_pixels, uint32_t tile_w, uint32_t tile_h, uint32_t width,
+                         uint32_t height, const double* packed, double* canvas) {
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= num_pixels) return;
+  const uint32_t tile_px = tile_w * tile_h;
+  const uint32_t tile = p / tile_px, in_tile = p % tile_px;
+  const uint32_t x = tiles[4 * tile] + in_tile % tile_w;
+  const uint32_t y = tiles[4 * tile + 1] + in_tile / tile_w;
+  const uint32_t row = height - y;
+  if (row < height) {
+    const double* s = packed + (size_t)p * 4;
+    double* o = canvas + ((size_t)row * width + x) * 4;
+    o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+  }
+}
+
+// ------------------------------------------------------- component kernels
+// izpi_gpu_trace: rays [n][8] -> RayRec, queue = identity
+__global__ void k_trace_setup(const double* rays, uint32_t n, RayRec* rr, uint32_t* q, uint32_t* qn) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) *qn = n;
+  if (i >= n) return;
+  const double* r = rays + (size_t)i * 8;
+  RayRec R;
+  for (int k = 0; k < 3; k++) { R.o[k] = r[k]; R.d[k] = r[3 + k]; }
+  R.tmin = r[6]; R.tmax = r[7]; R.time = 0; R.kind = RAY_PATHLEN; R.pad = 0;
+  rr[i] = R;
+  q[i] = i;
+}
+__global__ void k_trace_records(const DevScene sc, const RayRec* rr, const HitOut* hits, uint32_t n, izpi_hit* out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  izpi_hit h;
+  memset(&h, 0, sizeof(h));
+  h.prim_ref = 0xFFFFFFFFu;
+  const HitOut c = hits[i];
+  if (c.prim >= 0) {
+    const RayRec R = rr[i];
+    HitRec hr;
+    hit_record(sc, c, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
+    const GPrim& p = sc.prims[c.prim];
+    h.hit = 1; h.t = hr.t; h.u = hr.u; h.v = hr.v;
+    h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
+    h.normal[0] = hr.n.x; h.normal[1] = hr.n.y; h.normal[2] = hr.n.z;
+    h.prim_ref = IZPI_PRIM_REF(p.kind, p.index);
+  }
+  out[i] = h;
+}
+
+__global__ void k_aabb4(const float* boxes, const float* rays, uint32_t n, uint8_t* masks) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float* b = boxes + (size_t)i * 24;
+  const float* r = rays + (size_t)i * 7;
+  uint8_t m = 0;
+  for (int k = 0; k < 4; k++)
+    if (slab(b[k], b[4 + k], b[8 + k], b[12 + k], b[16 + k], b[20 + k], r[0], r[1], r[2], r[3], r[4], r[5], r[6])) m |= (uint8_t)(1 << k);
+  masks[i] = m;
+}
+
+__global__ void k_gomath(int op, const double* x, const double* y, uint32_t n, double* out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double a = x[i], b = y ? y[i] : 0.0, r;
+  switch (op) {
+    case 0: r = gm::sin(a); break;
+    case 1: r = gm::cos(a); break;
+    case 2: r = gm::tan(a); break;
+    case 3: r = gm::exp(a); break;
+    case 4: r = gm::log(a); break;
+    case 5: r = gm::pow(a, b); break;
+    case 6: r = gm::atan2(a, b); break;
+    case 7: r = gm::asin(a); break;
+    case 8: r = gm::sqrt(a); break;
+    case 9: r = a / b; break;
+    case 10: r = gm::atan(a); break;
+    default: r = gm::nan();
+  }
+  out[i] = r;
+}
+
+// ================================================================ host side
+struct izpi_ctx {
+  int device = 0;
+  std::string err;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  int num_cus = 0;
+  // scene
+  bool have_scene = false;
+  DevScene sc{};
+  uint32_t stack_needed = 0;
+  std::vector<void*> scene_allocs;
+  // render workspace (grown on demand)
+  double* d_samples = nullptr; size_t samples_cap = 0;
+  double* d_recs = nullptr; size_t recs_cap = 0;
+  double* d_running = nullptr; size_t running_cap = 0;
+  double* d_out = nullptr; size_t out_cap = 0;
+  uint32_t* d_tiles = nullptr; size_t tiles_cap = 0;
+  double* d_bg = nullptr; size_t bg_cap = 0;
+  uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts
+  unsigned long long* d_counters = nullptr;
+  RayRec* d_rays = nullptr; size_t rays_cap = 0;
+  HitOut* d_hits = nullptr; size_t hits_cap = 0;
+  PathSt* d_paths = nullptr; size_t paths_cap = 0;
+  uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
+  uint32_t* h_count = nullptr;                        // pinned readback of the queue length
+  hipEvent_t ev3 = nullptr;
+  izpi_render_stats last{};
+  bool mat_ok_rgb = false, mat_ok_spectral = false;
+};
+
+namespace {
+
+template <typename T>
+int dev_upload(izpi_ctx* ctx, const T* host, size_t count, T** out) {
+  *out = nullptr;
+  if (count == 0) return IZPI_OK;
+  HIP_TRY(hipMalloc((void**)out, count * sizeof(T)));
+  ctx->scene_allocs.push_back(*out);
+  if (host) HIP_TRY(hipMemcpy(*out, host, count * sizeof(T), hipMemcpyHostToDevice));
+  return IZPI_OK;
+}
+#define UP(ptr, n, dst)                                   \
+  do {                                                    \
+    int rc_ = dev_upload(ctx, ptr, (size_t)(n), dst);     \
+    if (rc_) return rc_;                                  \
+  } while (0)
+
+int grow(izpi_ctx* ctx, void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return IZPI_OK;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, bytes));
+  *cap = bytes;
+  return IZPI_OK;
+}
+
+void free_scene(izpi_ctx* ctx) {
+  for (void* p : ctx->scene_allocs) (void)hipFree(p);
+  ctx->scene_allocs.clear();
+  ctx->have_scene = false;
+}
+
+template <typename K>
+int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
+  int per_cu = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0));
+  if (per_cu < 1) per_cu = 1;
+  *blocks = per_cu * ctx->num_cus;
+  return IZPI_OK;
+}
+
+uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint32_t n, uint32_t* tw, uint32_t* th) {
+  if (n == 0) return 0;
+  *tw = tiles[2] - tiles[0] + 1;
+  *th = tiles[3] - tiles[1] + 1;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t* t = tiles + 4 * i;
+    if (t[2] < t[0] || t[3] < t[1] || t[2] >= req->width || t[3] >= req->height) return 0;
+    if (t[2] - t[0] + 1 != *tw || t[3] - t[1] + 1 != *th) return 0;
+  }
+  return n;
+}
+
+// One chunk loop of the wavefront scheme: k_start fills the slots, then k_trace /
+// k_shade alternate until no slot has a ray left; k_accumulate folds the chunk's
+// per-sample radiance into the pixels in sample order.
+template <int SAMPLER, int STACK>
+int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveParams& wp, AccumParams& ap,
+               uint32_t num_pixels, uint32_t chunk, float* trace_ms, float* shade_ms, uint32_t* launches) {
+  hipStream_t st = ctx->stream;
+  int trace_res = 0, shade_res = 0;
+  int rc = resident_blocks(ctx, k_trace<STACK>, &trace_res);
+  if (rc) return rc;
+  if ((rc = resident_blocks(ctx, k_shade<SAMPLER>, &shade_res))) return rc;
+  uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
+  uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
+  for (uint32_t s0 = 0; s0 < req->spp; s0 += chunk) {
+    const uint32_t cs = std::min(chunk, req->spp - s0);
+    sp.chunk_spp = cs; sp.s0 = s0; sp.total_units = num_pixels * cs;
+    HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, sizeof(uint32_t), st));          // head
+    HIP_TRY(hipMemsetAsync(ctx->d_misc + 3, 0, 2 * sizeof(uint32_t), st));  // queue counts
+    wp.q_out = q[0]; wp.q_out_count = qn[0];
+    const uint32_t start_slots = std::min<uint32_t>(sp.slots, sp.total_units);
+    ShadeParams sp0 = sp;
+    sp0.slots = sp.slots;
+    hipLaunchKernelGGL(k_start<SAMPLER>, dim3((start_slots + 255) / 256), dim3(256), 0, st, ctx->sc, sp0, wp);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint32_t n = *ctx->h_count;
+    int cur = 0;
+    while (n > 0) {
+      wp.q_in = q[cur]; wp.q_in_count = qn[cur];
+      wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
+      HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
+      HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
+      const uint32_t tb = std::min<uint32_t>((uint32_t)trace_res, (n + 255) / 256 * 4);
+      HIP_TRY(hipEventRecord(ctx->ev1, st));
+      hipLaunchKernelGGL(k_trace<STACK>, dim3(std::max(1u, tb)), dim3(256), 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(ctx->ev2, st));
+      const uint32_t sb = std::min<uint32_t>((uint32_t)shade_res, (n + 255) / 256);
+      hipLaunchKernelGGL(k_shade<SAMPLER>, dim3(std::max(1u, sb)), dim3(256), 0, st, ctx->sc, sp, wp);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(ctx->ev3, st));
+      HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[1 - cur], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      float t_ms = 0, s_ms = 0;
+      HIP_TRY(hipEventElapsedTime(&t_ms, ctx->ev1, ctx->ev2));
+      HIP_TRY(hipEventElapsedTime(&s_ms, ctx->ev2, ctx->ev3));
+      *trace_ms += t_ms;
+      *shade_ms += s_ms;
+      (*launches)++;
+      n = *ctx->h_count;
+      cur = 1 - cur;
+    }
+    ap.chunk_spp = cs;
+    ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
+    hipLaunchKernelGGL(k_accumulate, dim3((num_pixels + 255) / 256), dim3(256), 0, st, ap);
+    HIP_TRY(hipGetLastError());
+  }
+  return IZPI_OK;
+}
+
+int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
+  if (!ctx->have_scene) { ctx->err = "render before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
+  if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
+  if (req->sampler != IZPI_SAMPLER_COLOUR && req->sampler != IZPI_SAMPLER_SPECTRAL) { ctx->err = "unsupported sampler"; return IZPI_ERR_UNSUPPORTED; }
+  if (req->sampler == IZPI_SAMPLER_COLOUR ? !ctx->mat_ok_rgb : !ctx->mat_ok_spectral) {
+    ctx->err = "a material lacks the textures this sampler reads";
+    return IZPI_ERR_INVALID;
+  }
+  if (ctx->sc.num_lights == 0) { ctx->err = "scene has no lights (HitableSlice.PDFValue divides by zero)"; return IZPI_ERR_INVALID; }
+  std::vector<uint32_t> tiles;
+  if (req->num_tiles) {
+    tiles.assign(req->tiles, req->tiles + 4 * (size_t)req->num_tiles);
+  } else {
+    tiles.resize(4 * ((size_t)req->width * req->height / 16 + 16));
+    uint32_t nt = izpi_host_tiles(req->width, req->height, tiles.data(), (uint32_t)(tiles.size() / 4));
+    if (nt == 0) { ctx->err = "image size not divisible by any common.Tiles step"; return IZPI_ERR_INVALID; }
+    tiles.resize(4 * (size_t)nt);
+  }
+  uint32_t tw = 0, th = 0;
+  const uint32_t ntiles = validate_tiles(req, tiles.data(), (uint32_t)(tiles.size() / 4), &tw, &th);
+  if (ntiles == 0) { ctx->err = "tiles must be non-empty, in bounds and equal-sized"; return IZPI_ERR_INVALID; }
+  const uint64_t num_pixels64 = (uint64_t)ntiles * tw * th;
+  if (num_pixels64 > (1ull << 30)) { ctx->err = "too many pixels in one request"; return IZPI_ERR_INVALID; }
+  const uint32_t num_pixels = (uint32_t)num_pixels64;
+  if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
+  const uint32_t stack = ctx->stack_needed <= 32 ? 32 : 64;
+  // chunking by spp keeps the per-sample buffer <= 64M samples (1.5 GiB)
+  const uint64_t max_units = 64ull << 20;
+  const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
+  const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, 1u << 21);
+  const uint32_t depth_cap = std::max(1u, req->max_depth);
+  int rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * 3 * sizeof(double)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_recs, &ctx->recs_cap, (size_t)depth_cap * 6 * slots * sizeof(double)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_rays, &ctx->rays_cap, (size_t)slots * sizeof(RayRec)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_hits, &ctx->hits_cap, (size_t)slots * sizeof(HitOut)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_paths, &ctx->paths_cap, (size_t)slots * sizeof(PathSt)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)2 * slots * sizeof(uint32_t)))) return rc;
+  const size_t nbg = req->num_bg_spd;
+  if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
+  hipStream_t st = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (nbg) {
+    HIP_TRY(hipMemcpyAsync(ctx->d_bg, req->bg_spd_wavelengths, nbg * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->d_bg + nbg, req->bg_spd_values, nbg * sizeof(double), hipMemcpyHostToDevice, st));
+  }
+  HIP_TRY(hipMemsetAsync(ctx->d_running, 0, (size_t)num_pixels * 3 * sizeof(double), st));
+  HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 5 * sizeof(uint32_t), st));
+
+  ShadeParams sp{};
+  sp.width = req->width; sp.height = req->height; sp.max_depth = req->max_depth;
+  sp.tile_w = tw; sp.tile_h = th; sp.num_bg_spd = (uint32_t)nbg; sp.slots = slots;
+  sp.tiles = ctx->d_tiles; sp.bg_wl = ctx->d_bg; sp.bg_val = ctx->d_bg + nbg;
+  sp.background[0] = req->background[0]; sp.background[1] = req->background[1]; sp.background[2] = req->background[2];
+  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.head = ctx->d_misc;
+  sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
+  WaveParams wp{};
+  wp.rays = ctx->d_rays; wp.hits = ctx->d_hits; wp.paths = ctx->d_paths; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  AccumParams ap{};
+  ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
+  ap.tile_w = tw; ap.tile_h = th; ap.sampler = req->sampler; ap.out_layout = req->out_layout;
+  ap.tiles = ctx->d_tiles; ap.samples = ctx->d_samples; ap.running = ctx->d_running; ap.out = out_dev;
+
+  float trace_ms = 0, shade_ms = 0;
+  uint32_t launches = 0;
+  HIP_TRY(hipEventRecord(ctx->ev0, st));
+  if (req->sampler == IZPI_SAMPLER_COLOUR)
+    rc = stack == 32 ? run_chunks<IZPI_SAMPLER_COLOUR, 32>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
+                     : run_chunks<IZPI_SAMPLER_COLOUR, 64>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches);
+  else
+    rc = stack == 32 ? run_chunks<IZPI_SAMPLER_SPECTRAL, 32>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
+                     : run_chunks<IZPI_SAMPLER_SPECTRAL, 64>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(ctx->ev1, st));
+  HIP_TRY(hipEventSynchronize(ctx->ev1));
+  float total_ms = 0;
+  HIP_TRY(hipEventElapsedTime(&total_ms, ctx->ev0, ctx->ev1));
+  unsigned long long cnt[CNT_N];
+  uint32_t misc[2];
+  HIP_TRY(hipMemcpy(cnt, ctx->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(misc, ctx->d_misc, sizeof(misc), hipMemcpyDeviceToHost));
+  izpi_render_stats& s = ctx->last;
+  memset(&s, 0, sizeof(s));
+  s.rays = cnt[CNT_RAYS]; s.node_visits = cnt[CNT_NODES]; s.tri_tests = cnt[CNT_TRI]; s.sph_tests = cnt[CNT_SPH];
+  s.light_tri_tests = cnt[CNT_LTRI]; s.light_sph_tests = cnt[CNT_LSPH];
+  s.samples = (uint64_t)num_pixels * req->spp;
+  s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches;
+  if (misc[1]) {
+    ctx->err = misc[1] & 1u ? "device guard: traversal stack overflow" : "device guard: unknown material kind";
+    return IZPI_ERR_DEVICE;
+  }
+  return IZPI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int izpi_gpu_open(int device, izpi_ctx** out) {
+  *out = nullptr;
+  izpi_ctx* ctx = new izpi_ctx();
+  ctx->device = device;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0 || device < 0 || device >= n) {
+    delete ctx;
+    return IZPI_ERR_HIP;
+  }
+  if (hipSetDevice(device) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
+  ctx->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+      hipEventCreate(&ctx->ev2) != hipSuccess || hipEventCreate(&ctx->ev3) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->h_count, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void**)&ctx->d_misc, 8 * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) != hipSuccess) {
+    delete ctx;
+    return IZPI_ERR_HIP;
+  }
+  *out = ctx;
+  return IZPI_OK;
+}
+
+int izpi_gpu_close(izpi_ctx* ctx) {
+  if (!ctx) return IZPI_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  free_scene(ctx);
+  void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
+                  ctx->d_counters, ctx->d_rays, ctx->d_hits, ctx->d_paths, ctx->d_queue};
+  for (void* p : bufs) if (p) (void)hipFree(p);
+  if (ctx->h_count) (void)hipHostFree(ctx->h_count);
+  if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return IZPI_OK;
+}
+
+const char* izpi_gpu_last_error(izpi_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
+  if (!ctx || !d) return IZPI_ERR_INVALID;
+  if (d->abi_version != IZPI_ABI_VERSION) { ctx->err = "ABI version mismatch"; return IZPI_ERR_INVALID; }
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  free_scene(ctx);
+  const uint32_t nt = d->num_tris, ns = d->num_spheres;
+  // ---- BVH4: split reference nodes into inner nodes and leaf records
+  std::vector<int32_t> ref(d->num_nodes);
+  uint32_t n_inner = 0, n_leaf = 0;
+  for (uint32_t k = 0; k < d->num_nodes; k++) {
+    const izpi_bvh4_node& n = d->nodes[k];
+    if (n.prim_count[0] > 0) {
+      for (int i = 1; i < 4; i++)
+        if (n.child[i] != -1) { ctx->err = "leaf node with more than one slot"; return IZPI_ERR_INVALID; }
+      ref[k] = -(int32_t)n_leaf - 2;
+      n_leaf++;
+    } else {
+      for (int i = 0; i < 4; i++)
+        if (n.prim_count[i] != 0) { ctx->err = "inner node with a primitive slot"; return IZPI_ERR_INVALID; }
+      ref[k] = (int32_t)n_inner++;
+    }
+  }
+  std::vector<GInner> inner(n_inner);
+  std::vector<GLeaf> leaves(n_leaf);
+  for (uint32_t k = 0; k < d->num_nodes; k++) {
+    const izpi_bvh4_node& n = d->nodes[k];
+    if (ref[k] <= -2) {
+      GLeaf& L = leaves[(size_t)leaf_id(ref[k])];
+      L.mn[0] = n.min_x[0]; L.mn[1] = n.min_y[0]; L.mn[2] = n.min_z[0];
+      L.mx[0] = n.max_x[0]; L.mx[1] = n.max_y[0]; L.mx[2] = n.max_z[0];
+      L.start = n.child[0]; L.count = n.prim_count[0];
+      if ((uint32_t)(L.start + L.count) > d->num_prims) { ctx->err = "leaf primitive range out of bounds"; return IZPI_ERR_INVALID; }
+    } else {
+      GInner& g = inner[(size_t)ref[k]];
+      memcpy(g.mnx, n.min_x, 16); memcpy(g.mny, n.min_y, 16); memcpy(g.mnz, n.min_z, 16);
+      memcpy(g.mxx, n.max_x, 16); memcpy(g.mxy, n.max_y, 16); memcpy(g.mxz, n.max_z, 16);
+      for (int i = 0; i < 4; i++) {
+        int32_t c = n.child[i];
+        if (c != -1 && (c < 0 || (uint32_t)c >= d->num_nodes)) { ctx->err = "child index out of bounds"; return IZPI_ERR_INVALID; }
+        g.child[i] = c == -1 ? -1 : ref[(size_t)c];
+        g.pad[i] = 0;
+      }
+    }
+  }
+  // ---- primitives in leaf order
+  std::vector<GPrim> prims(d->num_prims);
+  for (uint32_t k = 0; k < d->num_prims; k++) {
+    const uint32_t r = d->prim_ref[k], kind = IZPI_PRIM_KIND(r), idx = IZPI_PRIM_INDEX(r);
+    GPrim& g = prims[k];
+    g.kind = kind; g.index = idx;
+    if (kind == IZPI_PRIM_TRIANGLE) {
+      if (idx >= nt) { ctx->err = "triangle ref out of range"; return IZPI_ERR_INVALID; }
+      memcpy(g.a, d->tri_v0 + 3 * (size_t)idx, 24); memcpy(g.a + 3, d->tri_e1 + 3 * (size_t)idx, 24);
+      memcpy(g.a + 6, d->tri_e2 + 3 * (size_t)idx, 24);
+    } else {
+      if (idx >= ns) { ctx->err = "sphere ref out of range"; return IZPI_ERR_INVALID; }
+      memcpy(g.a, d->sph_center0 + 3 * (size_t)idx, 24); memcpy(g.a + 3, d->sph_center1 + 3 * (size_t)idx, 24);
+      g.a[6] = d->sph_radius[idx]; g.a[7] = d->sph_time[2 * (size_t)idx]; g.a[8] = d->sph_time[2 * (size_t)idx + 1];
+    }
+  }
+  // ---- lights
+  std::vector<GLight> lights(d->num_lights);
+  for (uint32_t i = 0; i < d->num_lights; i++) {
+    GLight& L = lights[i];
+    memset(&L, 0, sizeof(L));
+    const uint32_t r = d->light_ref[i], kind = IZPI_PRIM_KIND(r), idx = IZPI_PRIM_INDEX(r);
+    L.kind = kind; L.index = idx;
+    if (kind == IZPI_PRIM_TRIANGLE) {
+      if (idx >= nt) { ctx->err = "light triangle out of range"; return IZPI_ERR_INVALID; }
+      const izpi_material& m = d->materials[d->tri_mat[idx]];
+      if (m.kind == IZPI_MAT_PBR && m.normal_tex >= 0) { ctx->err = "normal-mapped light"; return IZPI_ERR_UNSUPPORTED; }
+      memcpy(L.v0, d->tri_v0 + 3 * (size_t)idx, 24); memcpy(L.v1, d->tri_v1 + 3 * (size_t)idx, 24);
+      memcpy(L.v2, d->tri_v2 + 3 * (size_t)idx, 24); memcpy(L.e1, d->tri_e1 + 3 * (size_t)idx, 24);
+      memcpy(L.e2, d->tri_e2 + 3 * (size_t)idx, 24); memcpy(L.n, d->tri_normal + 3 * (size_t)idx, 24);
+      L.area = d->tri_area[idx];
+    } else {
+      if (idx >= ns) { ctx->err = "light sphere out of range"; return IZPI_ERR_INVALID; }
+      memcpy(L.c0, d->sph_center0 + 3 * (size_t)idx, 24); memcpy(L.c1, d->sph_center1 + 3 * (size_t)idx, 24);
+      L.radius = d->sph_radius[idx]; L.t0 = d->sph_time[2 * (size_t)idx]; L.t1 = d->sph_time[2 * (size_t)idx + 1];
+    }
+  }
+  // ---- material flags: bit0 a texture of the material reads (u,v); bit1 usable by
+  // the Colour sampler; bit2 usable by the Spectral sampler (the reference would
+  // dereference a nil texture otherwise).
+  std::vector<uint32_t> mflags(d->num_materials, 0);
+  ctx->mat_ok_rgb = ctx->mat_ok_spectral = true;
+  for (uint32_t i = 0; i < d->num_materials; i++) {
+    const izpi_material& m = d->materials[i];
+    const int32_t ids[] = {m.albedo_tex, m.spectral_tex, m.normal_tex, m.roughness_tex, m.metalness_tex, m.absorb_tex};
+    for (int32_t t : ids) {
+      if (t < -1 || t >= (int32_t)d->num_textures) { ctx->err = "texture index out of range"; return IZPI_ERR_INVALID; }
+      if (t >= 0 && d->textures[t].kind == IZPI_TEX_IMAGE) mflags[i] |= 1u;
+    }
+    auto is_rgb = [&](int32_t t) { return t >= 0 && (d->textures[t].kind == IZPI_TEX_CONSTANT || d->textures[t].kind == IZPI_TEX_IMAGE); };
+    auto is_spec = [&](int32_t t) { return t >= 0 && (d->textures[t].kind == IZPI_TEX_SPECTRAL_GAUSSIAN || d->textures[t].kind == IZPI_TEX_SPECTRAL_TABULATED); };
+    auto opt_rgb = [&](int32_t t) { return t == -1 || is_rgb(t); };
+    bool rgb = false, spec = false;
+    switch (m.kind) {
+      case IZPI_MAT_LAMBERT: case IZPI_MAT_DIFFUSE_LIGHT: rgb = is_rgb(m.albedo_tex); spec = is_spec(m.spectral_tex); break;
+      case IZPI_MAT_DIELECTRIC: rgb = true; spec = is_spec(m.spectral_tex) && (m.absorb_tex == -1 || is_spec(m.absorb_tex)); break;
+      case IZPI_MAT_METAL: rgb = spec = true; break;
+      case IZPI_MAT_PBR: {
+        bool aux = opt_rgb(m.normal_tex) && opt_rgb(m.roughness_tex) && opt_rgb(m.metalness_tex);
+        rgb = aux && is_rgb(m.albedo_tex);
+        spec = aux && (is_spec(m.spectral_tex) || is_rgb(m.albedo_tex));
+        break;
+      }
+      default: ctx->err = "unknown material kind"; return IZPI_ERR_INVALID;
+    }
+    if (rgb) mflags[i] |= 2u; else ctx->mat_ok_rgb = false;
+    if (spec) mflags[i] |= 4u; else ctx->mat_ok_spectral = false;
+  }
+  // ---- upload
+  DevScene& sc = ctx->sc;
+  memset(&sc, 0, sizeof(sc));
+  GInner* di; GLeaf* dl; GPrim* dp; GLight* dlt;
+  double *dn, *duv, *dtg, *dbt, *dtex, *dswl, *dsv;
+  uint32_t *dtm, *dsm, *dmf;
+  izpi_material* dm; izpi_texture* dtx;
+  UP(inner.data(), inner.size(), &di);
+  UP(leaves.data(), leaves.size(), &dl);
+  UP(prims.data(), prims.size(), &dp);
+  UP(d->tri_normal, 3 * (size_t)nt, &dn);
+  UP(d->tri_uv, 6 * (size_t)nt, &duv);
+  UP(d->tri_tangent, 3 * (size_t)nt, &dtg);
+  UP(d->tri_bitangent, 3 * (size_t)nt, &dbt);
+  UP(d->tri_mat, nt, &dtm);
+  UP(d->sph_mat, ns, &dsm);
+  UP(lights.data(), lights.size(), &dlt);
+  UP(d->materials, d->num_materials, &dm);
+  UP(mflags.data(), mflags.size(), &dmf);
+  UP(d->textures, d->num_textures, &dtx);
+  UP(d->texels, d->num_texels, &dtex);
+  UP(d->spd_wavelengths, d->num_spd, &dswl);
+  UP(d->spd_values, d->num_spd, &dsv);
+  sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.tri_normal = dn; sc.tri_uv = duv; sc.tri_tangent = dtg;
+  sc.tri_bitangent = dbt; sc.tri_mat = dtm; sc.sph_mat = dsm; sc.lights = dlt; sc.materials = dm;
+  sc.mat_flags = dmf; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
+  sc.root = d->num_nodes ? ref[0] : -1;
+  sc.num_lights = d->num_lights;
+  sc.cam = d->camera;
+  // traversal stack bound (see host_scene.cpp stack_bound)
+  {
+    std::vector<uint32_t> best(d->num_nodes, 0);
+    for (size_t k = d->num_nodes; k-- > 0;) {
+      const izpi_bvh4_node& n = d->nodes[k];
+      if (n.prim_count[0] > 0) continue;
+      uint32_t valid = 0, deepest = 0;
+      for (int i = 0; i < 4; i++) {
+        if (n.child[i] < 0) continue;
+        valid++;
+        if ((uint32_t)n.child[i] <= k) { ctx->err = "BVH4 nodes not in pre-order"; return IZPI_ERR_INVALID; }
+        deepest = std::max(deepest, best[(size_t)n.child[i]]);
+      }
+      best[k] = (valid ? valid - 1 : 0) + deepest;
+    }
+    ctx->stack_needed = d->num_nodes ? best[0] : 0;
+  }
+  ctx->have_scene = true;
+  return IZPI_OK;
+}
+
+uint64_t izpi_gpu_output_bytes(const izpi_render_req* req) {
+  if (!req) return 0;
+  if (req->out_layout == IZPI_OUT_PACKED && req->num_tiles) {
+    uint64_t px = 0;
+    for (uint32_t i = 0; i < req->num_tiles; i++) {
+      const uint32_t* t = req->tiles + 4 * i;
+      px += (uint64_t)(t[2] - t[0] + 1) * (t[3] - t[1] + 1);
+    }
+    return px * 4 * sizeof(double);
+  }
+  return (uint64_t)req->width * req->height * 4 * sizeof(double);
+}
+
+int izpi_gpu_render_device(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  if (!out_dev) { ctx->err = "null output"; return IZPI_ERR_INVALID; }
+  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = render_impl(ctx, req, out_dev);
+  if (stats) *stats = ctx->last;
+  return rc;
+}
+
+int izpi_gpu_render(izpi_ctx* ctx, const izpi_render_req* req, double* out_host, izpi_render_stats* stats) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  if (!out_host || !req) { ctx->err = "null argument"; return IZPI_ERR_INVALID; }
+  HIP_TRY(hipSetDevice(ctx->device));
+  const size_t bytes = izpi_gpu_output_bytes(req);
+  int rc = grow(ctx, (void**)&ctx->d_out, &ctx->out_cap, bytes);
+  if (rc) return rc;
+  // start from the caller's buffer so untouched pixels keep their values
+  HIP_TRY(hipMemcpyAsync(ctx->d_out, out_host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  rc = render_impl(ctx, req, ctx->d_out);
+  if (stats) *stats = ctx->last;
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_host, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return IZPI_OK;
+}
+
+int izpi_gpu_unpack_tiles(izpi_ctx* ctx, const izpi_render_req* req, const double* packed_dev, double* canvas_dev) {
+  if (!ctx || !req || !packed_dev || !canvas_dev || !req->num_tiles) return IZPI_ERR_INVALID;
+  HIP_TRY(hipSetDevice(ctx->device));
+  uint32_t tw, th;
+  if (!validate_tiles(req, req->tiles, req->num_tiles, &tw, &th)) { ctx->err = "bad tiles"; return IZPI_ERR_INVALID; }
+  int rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, 4 * (size_t)req->num_tiles * sizeof(uint32_t));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->d_tiles, req->tiles, 4 * (size_t)req->num_tiles * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+  const uint32_t np = req->num_tiles * tw * th;
+  hipLaunchKernelGGL(k_unpack, dim3((np + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_tiles, np, tw, th, req->width,
+                     req->height, packed_dev, canvas_dev);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return IZPI_OK;
+}
+
+int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out) {
+  if (!ctx || !rays || !out) return IZPI_ERR_INVALID;
+  if (!ctx->have_scene) { ctx->err = "no scene"; return IZPI_ERR_NO_SCENE; }
+  if (n == 0) return IZPI_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  double* dr; izpi_hit* dh; RayRec* rr; HitOut* ho; uint32_t* q;
+  HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 8 * sizeof(double)));
+  HIP_TRY(hipMalloc((void**)&dh, (size_t)n * sizeof(izpi_hit)));
+  HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayRec)));
+  HIP_TRY(hipMalloc((void**)&ho, (size_t)n * sizeof(HitOut)));
+  HIP_TRY(hipMalloc((void**)&q, (size_t)n * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
+  HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
+  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, q, ctx->d_misc + 3);
+  WaveParams wp{};
+  wp.rays = rr; wp.hits = ho; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
+  const uint32_t blocks = std::max(1u, std::min<uint32_t>((n + 255) / 256, 4096));
+  if (ctx->stack_needed <= 32)
+    hipLaunchKernelGGL(k_trace<32>, dim3(blocks), dim3(256), 0, ctx->stream, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+  else
+    hipLaunchKernelGGL(k_trace<64>, dim3(blocks), dim3(256), 0, ctx->stream, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, ho, n, dh);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));
+  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(ho); (void)hipFree(q);
+  return IZPI_OK;
+}
+
+int izpi_gpu_ray_aabb4(izpi_ctx* ctx, const float* boxes, const float* rays, uint32_t n, uint8_t* masks) {
+  if (!ctx || !boxes || !rays || !masks) return IZPI_ERR_INVALID;
+  if (n == 0) return IZPI_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  float *db, *dr; uint8_t* dm;
+  HIP_TRY(hipMalloc((void**)&db, (size_t)n * 24 * sizeof(float)));
+  HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 7 * sizeof(float)));
+  HIP_TRY(hipMalloc((void**)&dm, n));
+  HIP_TRY(hipMemcpy(db, boxes, (size_t)n * 24 * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 7 * sizeof(float), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_aabb4, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, db, dr, n, dm);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipMemcpy(masks, dm, n, hipMemcpyDeviceToHost));
+  (void)hipFree(db); (void)hipFree(dr); (void)hipFree(dm);
+  return IZPI_OK;
+}
+
+int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uint32_t n, double* out) {
+  if (!ctx || !x || !out) return IZPI_ERR_INVALID;
+  if (n == 0) return IZPI_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  double *dx, *dy = nullptr, *dout;
+  HIP_TRY(hipMalloc((void**)&dx, (size_t)n * sizeof(double)));
+  HIP_TRY(hipMalloc((void**)&dout, (size_t)n * sizeof(double)));
+  HIP_TRY(hipMemcpy(dx, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+  if (y) {
+    HIP_TRY(hipMalloc((void**)&dy, (size_t)n * sizeof(double)));
+    HIP_TRY(hipMemcpy(dy, y, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+  }
+  hipLaunchKernelGGL(k_gomath, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, op, dx, dy, n, dout);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dx); (void)hipFree(dout);
+  if (dy) (void)hipFree(dy);
+  return IZPI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,156 @@
+"""GPURenderer — the drop-in for izpi's render.Renderer (internal/render/renderer.go:26-28).
+
+``GPURenderer(scene, W, H, spp, max_depth, ...)`` mirrors ``render.New`` (renderer.go:73-104)
+and ``.render()`` mirrors ``Render(ctx) image.Image`` (renderer.go:108-222): it returns the
+float64 NRGBA canvas (H, W, 4) the Go renderer fills — RGB for the Colour sampler, CIE XYZ
+before post-processing for the Spectral sampler (``.render_spectral_rgb()`` applies
+FireflyRejection + XYZToRGB like renderer.go:216-219).
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): tiles are dealt
+round-robin (tile_id % world == rank), each rank renders its tiles into a packed
+device buffer, and one ``gather`` moves them to rank 0, which scatters them into the
+canvas on its GPU (izpi_gpu_unpack_tiles). Per pixel-sample RNG streams make the image
+independent of the partition.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+from .scene import HostScene
+
+
+def _check(rc, ctx, what):
+    if rc != 0:
+        msg = N.lib().izpi_gpu_last_error(ctx).decode() if ctx else ""
+        raise RuntimeError("%s failed (status %d): %s" % (what, rc, msg))
+
+
+def common_tiles(width, height):
+    """common.Tiles + grid.WalkGrid spiral order, as an (n, 4) uint32 array."""
+    buf = (C.c_uint32 * (4 * (width * height // 16 + 16)))()
+    n = N.lib().izpi_host_tiles(width, height, buf, len(buf) // 4)
+    if n == 0:
+        raise ValueError("%dx%d is not divisible by any common.Tiles step" % (width, height))
+    return np.frombuffer(buf, np.uint32, count=4 * n).reshape(n, 4).copy()
+
+
+class GPURenderer:
+    def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
+                 spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None):
+        self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
+        self.sampler = int(sampler)
+        self.background = tuple(float(b) for b in background)
+        self.seed = int(seed)
+        self.device = int(device)
+        # leader mode: aspect = W/H overrides the scene camera (transport.go aspectOverride)
+        self.host = host_scene or HostScene(scene, aspect_override=float(width) / float(height), bvh_seed=bvh_seed)
+        if spectral_background is None:
+            self._bg_wl = np.zeros(0)
+            self._bg_val = np.zeros(0)
+        else:
+            wl, val = spectral_background
+            self._bg_wl = np.ascontiguousarray(wl, np.float64)
+            self._bg_val = np.ascontiguousarray(val, np.float64)
+        L = N.lib()
+        ctx = C.c_void_p()
+        rc = L.izpi_gpu_open(self.device, C.byref(ctx))
+        if rc != 0:
+            raise RuntimeError("izpi_gpu_open(%d) failed: no HIP device?" % self.device)
+        self.ctx = ctx
+        _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
+        self.stats = None
+
+    # -------------------------------------------------------------- request
+    def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None):
+        req = N.RenderReq()
+        req.width, req.height = self.width, self.height
+        req.spp = self.spp if spp is None else int(spp)
+        req.max_depth = self.max_depth
+        req.sampler = self.sampler
+        req.out_layout = layout
+        req.background[:] = self.background
+        req.seed = self.seed
+        keep = []
+        if tiles is not None:
+            t = np.ascontiguousarray(tiles, np.uint32).reshape(-1, 4)
+            keep.append(t)
+            req.num_tiles = len(t)
+            req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
+        if self._bg_wl.size:
+            req.num_bg_spd = self._bg_wl.size
+            req.bg_spd_wavelengths = self._bg_wl.ctypes.data_as(C.POINTER(C.c_double))
+            req.bg_spd_values = self._bg_val.ctypes.data_as(C.POINTER(C.c_double))
+        req._keep = keep
+        return req
+
+    # --------------------------------------------------------------- render
+    def render(self, tiles=None, canvas=None, spp=None):
+        """Render.Render(): returns the (H, W, 4) float64 canvas (host memory)."""
+        if canvas is None:
+            canvas = np.zeros((self.height, self.width, 4), np.float64)
+        req = self.request(tiles, N.OUT_CANVAS, spp)
+        st = N.RenderStats()
+        rc = N.lib().izpi_gpu_render(self.ctx, C.byref(req), canvas.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st))
+        _check(rc, self.ctx, "izpi_gpu_render")
+        self.stats = st.as_dict()
+        return canvas
+
+    def render_device(self, out_ptr, tiles=None, layout=N.OUT_CANVAS, spp=None):
+        """Render into device memory at `out_ptr` (e.g. torch tensor .data_ptr())."""
+        req = self.request(tiles, layout, spp)
+        st = N.RenderStats()
+        rc = N.lib().izpi_gpu_render_device(self.ctx, C.byref(req), C.c_void_p(out_ptr), C.byref(st))
+        _check(rc, self.ctx, "izpi_gpu_render_device")
+        self.stats = st.as_dict()
+        return self.stats
+
+    def output_doubles(self, tiles=None, layout=N.OUT_CANVAS):
+        req = self.request(tiles, layout)
+        return N.lib().izpi_gpu_output_bytes(C.byref(req)) // 8
+
+    def unpack(self, tiles, packed_ptr, canvas_ptr):
+        req = self.request(tiles, N.OUT_PACKED)
+        _check(N.lib().izpi_gpu_unpack_tiles(self.ctx, C.byref(req), C.c_void_p(packed_ptr), C.c_void_p(canvas_ptr)),
+               self.ctx, "izpi_gpu_unpack_tiles")
+
+    # ------------------------------------------------------------ multi-GPU
+    def render_distributed(self, rank, world, group=None, tiles=None):
+        """Tile-sharded render over `world` ranks; returns the canvas as a torch tensor
+        on rank 0 (None elsewhere) and this rank's stats. One RCCL gather."""
+        import torch
+        import torch.distributed as dist
+        all_tiles = common_tiles(self.width, self.height) if tiles is None else np.asarray(tiles, np.uint32)
+        mine = all_tiles[rank::world]
+        per_tile = int((all_tiles[0, 2] - all_tiles[0, 0] + 1) * (all_tiles[0, 3] - all_tiles[0, 1] + 1) * 4)
+        max_tiles = (len(all_tiles) + world - 1) // world
+        dev = torch.device("cuda", self.device)
+        packed = torch.zeros(max_tiles * per_tile, dtype=torch.float64, device=dev)
+        if len(mine):
+            self.render_device(packed.data_ptr(), tiles=mine, layout=N.OUT_PACKED)
+        torch.cuda.synchronize(dev)
+        if world == 1:
+            gathered = [packed]
+        else:
+            gathered = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+            dist.gather(packed, gather_list=gathered, dst=0, group=group)
+        if rank != 0:
+            return None, self.stats
+        canvas = torch.zeros((self.height, self.width, 4), dtype=torch.float64, device=dev)
+        for r in range(world):
+            rt = all_tiles[r::world]
+            if len(rt):
+                self.unpack(rt, gathered[r].data_ptr(), canvas.data_ptr())
+        torch.cuda.synchronize(dev)
+        return canvas, self.stats
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            N.lib().izpi_gpu_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
