@@ -75,6 +75,11 @@ uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint3
  * codes as izpi_gpu_gomath); used by the parity tests. */
 double izpi_host_gomath(int op, double x, double y);
 
+/* sizeof() of the boundary structs: 0 izpi_bvh4_node 1 izpi_texture 2 izpi_material
+ * 3 izpi_camera 4 izpi_scene_desc 5 izpi_render_req 6 izpi_render_stats 7 izpi_hit
+ * 8 izpi_tri_in 9 izpi_sphere_in 10 izpi_camera_in 11 izpi_scene_input (0 = unknown). */
+uint32_t izpi_abi_struct_size(int which);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,13 +120,16 @@ class SceneInput(C.Structure):
                 ("aspect_override", C.c_double), ("bvh_seed", C.c_uint64)]
 
 
+ABI_STRUCTS = [BVH4Node, Texture, Material, Camera, SceneDesc, RenderReq, RenderStats, Hit, TriIn, SphereIn, CameraIn,
+               SceneInput]
+
 # Symbols include/izpi_gpu.h and include/izpi_host.h declare (checked by tests).
 EXPORTS = [
     "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
     "izpi_gpu_render_device", "izpi_gpu_unpack_tiles", "izpi_gpu_output_bytes", "izpi_gpu_trace",
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
-    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath",
+    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
 ]
 
 _lib = None
@@ -170,5 +173,7 @@ def lib():
     L.izpi_host_tiles.restype = C.c_uint32
     L.izpi_host_gomath.argtypes = [C.c_int, C.c_double, C.c_double]
     L.izpi_host_gomath.restype = C.c_double
+    L.izpi_abi_struct_size.argtypes = [C.c_int]
+    L.izpi_abi_struct_size.restype = C.c_uint32
     _lib = L
     return L

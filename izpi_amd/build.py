@@ -2,13 +2,12 @@
 
 * ``izpi_amd/_lib/libizpi_gpu.so`` — the product: gfx950 HIP kernels + C ABI
   (include/izpi_gpu.h) + the C++ host scene producer (include/izpi_host.h).
-* ``oracle/_build/liboracle.so`` — TEST INFRASTRUCTURE only (CPU restatement).
+(The CPU oracle is test infrastructure and builds from oracle/Makefile.)
 
-Both are compiled with ``-ffp-contract=off`` and without fast-math so that every
+It is compiled with ``-ffp-contract=off`` and without fast-math so that every
 ``a*b+c`` rounds twice on host and device alike (Go on amd64 emits no FMA).
 """
 import os
-import shutil
 import subprocess
 import sys
 from pathlib import Path
@@ -17,8 +16,6 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "izpi_amd" / "csrc"
 LIBDIR = ROOT / "izpi_amd" / "_lib"
 LIB = LIBDIR / "libizpi_gpu.so"
-ORACLE_DIR = ROOT / "oracle"
-ORACLE_LIB = ORACLE_DIR / "_build" / "liboracle.so"
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -48,24 +45,10 @@ def build_gpu(force=False, verbose=True):
     return LIB
 
 
-def build_oracle(force=False, verbose=True):
-    deps = [ORACLE_DIR / "izpi_oracle.cpp", ORACLE_DIR / "go_math_ref.h", ORACLE_DIR / "cie_tables_ref.h",
-            ROOT / "include" / "izpi_host.h", ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_types.h"]
-    if not force and not _stale(ORACLE_LIB, deps):
-        return ORACLE_LIB
-    make = shutil.which("make")
-    cmd = [make, "-C", str(ORACLE_DIR)] + (["-B"] if force else [])
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True, stdout=None if verbose else subprocess.DEVNULL)
-    return ORACLE_LIB
-
-
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     force = "--force" in argv
     build_gpu(force=force)
-    build_oracle(force=force)
 
 
 if __name__ == "__main__":

@@ -506,6 +506,26 @@ uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint3
   return n < max_tiles ? n : max_tiles;
 }
 
+/* sizeof() of every boundary struct, in the order of IZPI_ABI_STRUCTS (tests compare
+ * them with the Python/ctypes and Go-side layouts). */
+uint32_t izpi_abi_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(izpi_bvh4_node);
+    case 1: return sizeof(izpi_texture);
+    case 2: return sizeof(izpi_material);
+    case 3: return sizeof(izpi_camera);
+    case 4: return sizeof(izpi_scene_desc);
+    case 5: return sizeof(izpi_render_req);
+    case 6: return sizeof(izpi_render_stats);
+    case 7: return sizeof(izpi_hit);
+    case 8: return sizeof(izpi_tri_in);
+    case 9: return sizeof(izpi_sphere_in);
+    case 10: return sizeof(izpi_camera_in);
+    case 11: return sizeof(izpi_scene_input);
+  }
+  return 0;
+}
+
 /* The product's Go-math header compiled for the host (parity hook for tests). */
 double izpi_host_gomath(int op, double x, double y) {
   switch (op) {

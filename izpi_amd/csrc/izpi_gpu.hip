@@ -20,6 +20,7 @@
 // render/rgb.go:36's sequential col += ...) and writes the canvas.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <algorithm>
 #include <string>
@@ -44,6 +45,8 @@ __constant__ double c_cie_wl[IZPI_CIE_N] = IZPI_CIE_WAVELENGTHS_INIT;
 __constant__ double c_cie_x[IZPI_CIE_N] = IZPI_CIE_X_INIT;
 __constant__ double c_cie_y[IZPI_CIE_N] = IZPI_CIE_Y_INIT;
 __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
+
+#define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_N };
 
@@ -623,7 +626,12 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
 }
 
 // One shading pass over the slots traced in the previous k_trace.
-template <int SAMPLER>
+// MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
+// DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
+// footprint small; MATSET_FULL adds Dielectric, Metal and PBR. The host picks the
+// variant from the scene's material kinds (results are identical).
+enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
+template <int SAMPLER, int MATSET>
 __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const uint32_t n = *wp.q_in_count;
@@ -650,7 +658,7 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
       V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
       V3 hit_n = mk(0, 0, 0);
       Onb cos_onb;
-      if (R.kind == RAY_PATHLEN) {
+      if (MATSET == MATSET_FULL && R.kind == RAY_PATHLEN) {
         // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
         const V3 hp = mk(P.pend[0], P.pend[1], P.pend[2]);
         double len = 10.0;
@@ -698,6 +706,7 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
             break;
           }
           case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
+            if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
             const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
             bool reflected;
             next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
@@ -721,6 +730,7 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
             break;
           }
           case IZPI_MAT_METAL: {  // metal.go:34-41 (RGB only: SpectralScatter is nonSpectral)
+            if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
             if (!COLOUR) { terminal = true; break; }
             V3 reflected = reflect(unit(rd), h.n);
             next_d = add(reflected, smul(random_in_unit_sphere(rng), m.fuzz));
@@ -729,6 +739,7 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
             break;
           }
           case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
+            if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
             double alb_s = 0;
             if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
             else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda);
@@ -1001,8 +1012,10 @@ struct izpi_ctx {
   uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
   uint32_t* h_count = nullptr;                        // pinned readback of the queue length
   hipEvent_t ev3 = nullptr;
+  hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
+  bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
 };
 
 namespace {
@@ -1062,14 +1075,14 @@ uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint3
 // One chunk loop of the wavefront scheme: k_start fills the slots, then k_trace /
 // k_shade alternate until no slot has a ray left; k_accumulate folds the chunk's
 // per-sample radiance into the pixels in sample order.
-template <int SAMPLER, int STACK>
+template <int SAMPLER, int STACK, int MATSET>
 int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveParams& wp, AccumParams& ap,
                uint32_t num_pixels, uint32_t chunk, float* trace_ms, float* shade_ms, uint32_t* launches) {
   hipStream_t st = ctx->stream;
   int trace_res = 0, shade_res = 0;
   int rc = resident_blocks(ctx, k_trace<STACK>, &trace_res);
   if (rc) return rc;
-  if ((rc = resident_blocks(ctx, k_shade<SAMPLER>, &shade_res))) return rc;
+  if ((rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res))) return rc;
   uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
   uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
   for (uint32_t s0 = 0; s0 < req->spp; s0 += chunk) {
@@ -1087,30 +1100,37 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     HIP_TRY(hipStreamSynchronize(st));
     uint32_t n = *ctx->h_count;
     int cur = 0;
+    // Launch passes in batches without a host round-trip per pass: both kernels read
+    // their queue length from device memory and exit at once when it is zero, so the
+    // host only polls the queue length once per batch (overshoot costs a few empty
+    // launches of ~5 us).
+    const int B = IZPI_PASS_BATCH;
     while (n > 0) {
-      wp.q_in = q[cur]; wp.q_in_count = qn[cur];
-      wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
-      HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
-      HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
-      const uint32_t tb = std::min<uint32_t>((uint32_t)trace_res, (n + 255) / 256 * 4);
-      HIP_TRY(hipEventRecord(ctx->ev1, st));
-      hipLaunchKernelGGL(k_trace<STACK>, dim3(std::max(1u, tb)), dim3(256), 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(ctx->ev2, st));
-      const uint32_t sb = std::min<uint32_t>((uint32_t)shade_res, (n + 255) / 256);
-      hipLaunchKernelGGL(k_shade<SAMPLER>, dim3(std::max(1u, sb)), dim3(256), 0, st, ctx->sc, sp, wp);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(ctx->ev3, st));
-      HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[1 - cur], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      for (int b = 0; b < B; b++) {
+        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
+        wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
+        HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
+        HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
+        HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
+        hipLaunchKernelGGL(k_trace<STACK>, dim3(trace_res), dim3(256), 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
+        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
+        cur = 1 - cur;
+      }
+      HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[cur], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      float t_ms = 0, s_ms = 0;
-      HIP_TRY(hipEventElapsedTime(&t_ms, ctx->ev1, ctx->ev2));
-      HIP_TRY(hipEventElapsedTime(&s_ms, ctx->ev2, ctx->ev3));
-      *trace_ms += t_ms;
-      *shade_ms += s_ms;
-      (*launches)++;
+      for (int b = 0; b < B; b++) {
+        float t_ms = 0, s_ms = 0;
+        HIP_TRY(hipEventElapsedTime(&t_ms, ctx->evb[3 * b], ctx->evb[3 * b + 1]));
+        HIP_TRY(hipEventElapsedTime(&s_ms, ctx->evb[3 * b + 1], ctx->evb[3 * b + 2]));
+        *trace_ms += t_ms;
+        *shade_ms += s_ms;
+        (*launches)++;
+      }
       n = *ctx->h_count;
-      cur = 1 - cur;
     }
     ap.chunk_spp = cs;
     ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
@@ -1147,9 +1167,23 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
   const uint32_t stack = ctx->stack_needed <= 32 ? 32 : 64;
   // chunking by spp keeps the per-sample buffer <= 64M samples (1.5 GiB)
-  const uint64_t max_units = 64ull << 20;
+  uint64_t max_units = 64ull << 20;
+  if (const char* e = getenv("IZPI_CHUNK_UNITS")) max_units = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
-  const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, 1u << 21);
+  // Paths in flight per wavefront pass. Larger = fewer k_trace/k_shade launches and
+  // a smaller share of launch tails; costs HBM for the per-slot state (~176 B +
+  // 48 B per depth level of unwinding records).
+  uint64_t slot_cap = 1ull << 23;
+  if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
+  {  // keep the wavefront state within a quarter of the free HBM
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+      const uint64_t per_slot = sizeof(RayRec) + sizeof(HitOut) + sizeof(PathSt) + 8 +
+                                (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
+      slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 4) / per_slot));
+    }
+  }
+  const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);
   const uint32_t depth_cap = std::max(1u, req->max_depth);
   int rc;
   if ((rc = grow(ctx, (void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * 3 * sizeof(double)))) return rc;
@@ -1189,12 +1223,16 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   float trace_ms = 0, shade_ms = 0;
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
-  if (req->sampler == IZPI_SAMPLER_COLOUR)
-    rc = stack == 32 ? run_chunks<IZPI_SAMPLER_COLOUR, 32>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
-                     : run_chunks<IZPI_SAMPLER_COLOUR, 64>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches);
-  else
-    rc = stack == 32 ? run_chunks<IZPI_SAMPLER_SPECTRAL, 32>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
-                     : run_chunks<IZPI_SAMPLER_SPECTRAL, 64>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches);
+#define IZPI_RUN(S, K, M) run_chunks<S, K, M>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
+  const bool basic = ctx->basic_materials;
+  if (req->sampler == IZPI_SAMPLER_COLOUR) {
+    if (stack == 32) rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, 32, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, 32, MATSET_FULL);
+    else rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, 64, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, 64, MATSET_FULL);
+  } else {
+    if (stack == 32) rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 32, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 32, MATSET_FULL);
+    else rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 64, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 64, MATSET_FULL);
+  }
+#undef IZPI_RUN
   if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, st));
   HIP_TRY(hipEventSynchronize(ctx->ev1));
@@ -1244,6 +1282,8 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
     delete ctx;
     return IZPI_ERR_HIP;
   }
+  for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++)
+    if (hipEventCreate(&ctx->evb[i]) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
   *out = ctx;
   return IZPI_OK;
 }
@@ -1258,6 +1298,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
+  for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb[i]) (void)hipEventDestroy(ctx->evb[i]);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
@@ -1355,6 +1396,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   // dereference a nil texture otherwise).
   std::vector<uint32_t> mflags(d->num_materials, 0);
   ctx->mat_ok_rgb = ctx->mat_ok_spectral = true;
+  ctx->basic_materials = true;
   for (uint32_t i = 0; i < d->num_materials; i++) {
     const izpi_material& m = d->materials[i];
     const int32_t ids[] = {m.albedo_tex, m.spectral_tex, m.normal_tex, m.roughness_tex, m.metalness_tex, m.absorb_tex};
@@ -1378,6 +1420,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       }
       default: ctx->err = "unknown material kind"; return IZPI_ERR_INVALID;
     }
+    if (m.kind != IZPI_MAT_LAMBERT && m.kind != IZPI_MAT_DIFFUSE_LIGHT) ctx->basic_materials = false;
     if (rgb) mflags[i] |= 2u; else ctx->mat_ok_rgb = false;
     if (spec) mflags[i] |= 4u; else ctx->mat_ok_spectral = false;
   }

@@ -119,26 +119,21 @@ class GPURenderer:
         """Tile-sharded render over `world` ranks; returns the canvas as a torch tensor
         on rank 0 (None elsewhere) and this rank's stats. One RCCL gather."""
         import torch
-        import torch.distributed as dist
+        from . import sharding
         all_tiles = common_tiles(self.width, self.height) if tiles is None else np.asarray(tiles, np.uint32)
-        mine = all_tiles[rank::world]
-        per_tile = int((all_tiles[0, 2] - all_tiles[0, 0] + 1) * (all_tiles[0, 3] - all_tiles[0, 1] + 1) * 4)
-        max_tiles = (len(all_tiles) + world - 1) // world
+        mine = sharding.shard_tiles(all_tiles, rank, world)
         dev = torch.device("cuda", self.device)
-        packed = torch.zeros(max_tiles * per_tile, dtype=torch.float64, device=dev)
+        packed = torch.zeros(sharding.packed_len(all_tiles, world), dtype=torch.float64, device=dev)
+        self.stats = None
         if len(mine):
             self.render_device(packed.data_ptr(), tiles=mine, layout=N.OUT_PACKED)
         torch.cuda.synchronize(dev)
-        if world == 1:
-            gathered = [packed]
-        else:
-            gathered = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
-            dist.gather(packed, gather_list=gathered, dst=0, group=group)
+        gathered = sharding.gather_packed(packed, rank, world, group)
         if rank != 0:
             return None, self.stats
         canvas = torch.zeros((self.height, self.width, 4), dtype=torch.float64, device=dev)
         for r in range(world):
-            rt = all_tiles[r::world]
+            rt = sharding.shard_tiles(all_tiles, r, world)
             if len(rt):
                 self.unpack(rt, gathered[r].data_ptr(), canvas.data_ptr())
         torch.cuda.synchronize(dev)

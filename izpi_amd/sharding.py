@@ -1,0 +1,70 @@
+"""Tile sharding across GPUs (one process per GPU) and the framebuffer gather.
+
+renderer.go:172-188 feeds tiles to workers dynamically; here the partition is static
+and interleaved — tile i goes to rank i % world — so centre tiles (dragon, glass) are
+spread over all ranks. Per pixel-sample RNG streams make every pixel independent of
+the partition, so the gathered canvas is bit-identical for any world size.
+
+Each rank packs its tiles contiguously (IZPI_OUT_PACKED: tile after tile, rows of
+sample y, 4 doubles per pixel). One collective moves them to rank 0: ``dist.gather``
+of equal-sized (padded) packed buffers — over RCCL/xGMI with the "nccl" backend, or
+gloo in the CPU tests. Rank 0 scatters them into the canvas (izpi_gpu_unpack_tiles on
+the GPU; :func:`unpack_into` is the same rule on the host).
+"""
+import numpy as np
+
+
+def shard_tiles(all_tiles, rank, world):
+    return np.ascontiguousarray(np.asarray(all_tiles, np.uint32)[rank::world])
+
+
+def tile_pixels(tiles):
+    t = np.asarray(tiles, np.int64)
+    return int(((t[:, 2] - t[:, 0] + 1) * (t[:, 3] - t[:, 1] + 1)).sum())
+
+
+def packed_len(all_tiles, world):
+    """Doubles per rank's (padded) packed buffer: max tiles per rank * tile pixels * 4."""
+    t = np.asarray(all_tiles, np.int64)
+    per_tile = int((t[0, 2] - t[0, 0] + 1) * (t[0, 3] - t[0, 1] + 1))
+    max_tiles = (len(t) + world - 1) // world
+    return max_tiles * per_tile * 4
+
+
+def gather_packed(packed, rank, world, group=None):
+    """Gather every rank's packed tensor to rank 0 (list of tensors there, None elsewhere)."""
+    import torch.distributed as dist
+    if world == 1:
+        return [packed]
+    out = [packed.new_empty(packed.shape) for _ in range(world)] if rank == 0 else None
+    dist.gather(packed, gather_list=out, dst=0, group=group)
+    return out
+
+
+def unpack_into(canvas, tiles, packed, width, height):
+    """Host twin of k_unpack: packed tile pixels -> canvas rows H - y (rgb.go:41)."""
+    p = 0
+    flat = np.asarray(packed).reshape(-1, 4)
+    for x0, y0, x1, y1 in np.asarray(tiles, np.int64):
+        for y in range(y0, y1 + 1):
+            n = x1 - x0 + 1
+            row = height - y
+            if row < height:
+                canvas[row, x0:x1 + 1] = flat[p:p + n]
+            p += n
+    return canvas
+
+
+def pack_from_canvas(canvas, tiles, height):
+    """Inverse of unpack_into for pixels that have a canvas row (y >= 1); rows dropped
+    by the reference (y == 0) are packed as zeros. Used by the CPU tests to turn oracle
+    canvases into the packed layout."""
+    out = []
+    for x0, y0, x1, y1 in np.asarray(tiles, np.int64):
+        for y in range(y0, y1 + 1):
+            row = height - y
+            if row < height:
+                out.append(canvas[row, x0:x1 + 1])
+            else:
+                out.append(np.zeros((x1 - x0 + 1, 4)))
+    return np.concatenate(out).reshape(-1)

@@ -26,12 +26,17 @@ class OracleStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
 
 
+def build(force=False):
+    """make -C oracle (test infrastructure build)."""
+    subprocess.run(["make", "-C", str(HERE)] + (["-B"] if force else []), check=True, stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
 def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        subprocess.run(["make", "-C", str(HERE)], check=True, stdout=subprocess.DEVNULL)
+    build()
     from izpi_amd import _native as N  # struct layouts of the boundary headers only
     L = C.CDLL(str(LIB_PATH))
     L.oracle_build.argtypes = [C.POINTER(N.SceneInput)]

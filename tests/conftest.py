@@ -17,8 +17,9 @@ def pytest_configure(config):
 def _built():
     """Build the product library and the oracle in-tree once per session."""
     from izpi_amd import build
+    from oracle import oracle
     build.build_gpu(verbose=False)
-    build.build_oracle(verbose=False)
+    oracle.build()
     yield
 
 
