@@ -297,6 +297,177 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
   }
 }
 
+// BVH4.Hit, step-scheduled variant. Each lane is in one of two modes: NODE (visit
+// the node `cur`: the 4-slot box test of an inner node, or the slot-0 re-test of a
+// leaf, A10) or PRIM (test primitive pk of the leaf being scanned, one per step).
+// Every loop iteration the wave runs ONE kind of step — the one most of its busy lanes
+// want (weighted by the relative cost of a node step and an f64 primitive test) — so
+// f32 node code and f64 triangle code no longer serialise inside one iteration. Each
+// ray still performs exactly the reference's sequence of node visits and primitive
+// tests (bvh4.go:76-160), only interleaved differently with other rays, so results and
+// counters are unchanged.
+// The traversal stack is a ring of S entries per lane in LDS; when a push finds the
+// ring full, the oldest entry is spilled to a per-thread global area (entry e at
+// spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
+// are kept per wave in SGPRs (popcounts of ballots).
+template <int S, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
+                                                uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w) {
+  static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
+  __shared__ int32_t lds_stack[S * 256];
+  int32_t* stk = lds_stack + threadIdx.x;
+  int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t n = *wp.q_in_count;
+  uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
+  bool busy = false, in_prim = false;
+  bool exhausted = false;
+  uint32_t slot = 0;
+  double tmax = 0;
+  float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
+  int32_t cur = -1, pk = 0, pend = 0;
+  int sp = 0, low = 0;
+  int32_t bprim = -1;
+  for (;;) {
+    const uint64_t idle = __ballot(!busy);
+    if (idle != 0) {
+      const uint32_t nidle = (uint32_t)__popcll(idle);
+      if (!exhausted && (nidle >= 16 || idle == ~0ull)) {
+        const uint32_t leader = (uint32_t)__ffsll((long long)idle) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(wp.trace_next, nidle);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, (int)leader));
+        if (base + nidle >= n) exhausted = true;
+        bool main_ray = false;
+        if (!busy) {
+          const uint32_t my = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
+          if (my < n) {
+            slot = wp.q_in[my];
+            const RayRec& r = wp.rays[slot];
+            tmax = r.tmax;
+            main_ray = r.kind == RAY_MAIN;
+            ix = (float)(1.0 / r.d[0]); iy = (float)(1.0 / r.d[1]); iz = (float)(1.0 / r.d[2]);
+            ox = (float)r.o[0]; oy = (float)r.o[1]; oz = (float)r.o[2];
+            cur = sc.root;
+            sp = 0; low = 0;
+            in_prim = false;
+            bprim = -1;
+            busy = cur != -1;
+            if (!busy) { HitOut& h = wp.hits[slot]; h.t = 0; h.u = 0; h.v = 0; h.prim = -1; h.pad = 0; }
+          }
+        }
+        c_rays += (uint64_t)__popcll(__ballot(main_ray));
+      } else if (exhausted && idle == ~0ull) {
+        break;
+      }
+    }
+    const uint64_t m_prim = __ballot(busy && in_prim);
+    const uint64_t m_node = __ballot(busy && !in_prim);
+    if ((m_prim | m_node) == 0) continue;
+    const uint32_t n_prim = (uint32_t)__popcll(m_prim), n_node = (uint32_t)__popcll(m_node);
+    bool advance = false;   // lane finished its current node / leaf: take next or pop
+    int32_t next = -1;
+    if (n_prim * prim_w >= n_node * 16u) {
+      // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134)
+      bool is_tri = false;
+      if (busy && in_prim) {
+        // the f64 ray is re-read here (L2) instead of living in 14 VGPRs across node steps
+        const double2* rp = reinterpret_cast<const double2*>(wp.rays + slot);
+        const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+        const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
+        const double tmin = r3.x;
+        const double2* pp = reinterpret_cast<const double2*>(sc.prims + pk);
+        const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
+        const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
+        const uint32_t kind = (uint32_t)__double2loint(p4.y);
+        is_tri = kind == IZPI_PRIM_TRIANGLE;
+        if (is_tri) {
+          double t, u, v;
+          if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
+            tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v;
+          }
+        } else {
+          const double time = wp.rays[slot].time;  // only spheres read the ray time
+          double t; int root;
+          if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
+            tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0;
+          }
+        }
+        pk++;
+        if (pk == pend) { in_prim = false; advance = true; }
+      }
+      const uint32_t n_tri = (uint32_t)__popcll(__ballot(is_tri));
+      c_tri += n_tri;
+      c_sph += n_prim - n_tri;
+    } else {
+      c_nodes += n_node;
+      // ---- node step: visit `cur` (bvh4.go:87-146)
+      if (busy && !in_prim) {
+        const float tm = (float)tmax;
+        if (ref_is_leaf(cur)) {
+          const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_id(cur));
+          const float4 a = lp[0], b = lp[1];
+          const int32_t start = __float_as_int(b.z), count = __float_as_int(b.w);
+          if (count > 0 && slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
+            in_prim = true; pk = start; pend = start + count;
+          } else {
+            advance = true;
+          }
+        } else {
+          const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
+          const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
+          const int4 ch = *reinterpret_cast<const int4*>(np + 6);
+          const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
+                      amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
+                      amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+          const int32_t ach[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            if (ach[i] == -1) continue;
+            if (!slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) continue;
+            if (next == -1) {
+              next = ach[i];
+            } else {  // push (bvh4.go:141-145)
+              if (sp >= 64) {
+                atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
+              } else {
+                if (sp - low >= S) {  // ring full: spill the oldest entry
+                  gsp[(size_t)low * spill_stride] = stk[(low & (S - 1)) * 256];
+                  low++;
+                }
+                stk[(sp & (S - 1)) * 256] = ach[i];
+                sp++;
+              }
+            }
+          }
+          advance = true;
+        }
+      }
+    }
+    if (advance) {
+      if (next != -1) {
+        cur = next;
+      } else if (sp > 0) {  // pop (bvh4.go:150-160)
+        sp--;
+        if (sp < low) { cur = gsp[(size_t)sp * spill_stride]; low = sp; }
+        else cur = stk[(sp & (S - 1)) * 256];
+      } else {
+        HitOut& h = wp.hits[slot];
+        h.t = bprim >= 0 ? tmax : 0.0;
+        h.prim = bprim;
+        if (bprim < 0) { h.u = 0; h.v = 0; }
+        busy = false;
+      }
+    }
+  }
+  if (lane == 0) {
+    if (c_rays) atomicAdd(counters + CNT_RAYS, (unsigned long long)c_rays);
+    if (c_nodes) atomicAdd(counters + CNT_NODES, (unsigned long long)c_nodes);
+    if (c_tri) atomicAdd(counters + CNT_TRI, (unsigned long long)c_tri);
+    if (c_sph) atomicAdd(counters + CNT_SPH, (unsigned long long)c_sph);
+  }
+}
+
 // Full hit record of the closest primitive (triangle.go:223-264, sphere.go:71-92).
 struct HitRec {
   double t, u, v;
@@ -1010,6 +1181,7 @@ struct izpi_ctx {
   HitOut* d_hits = nullptr; size_t hits_cap = 0;
   PathSt* d_paths = nullptr; size_t paths_cap = 0;
   uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
+  int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   uint32_t* h_count = nullptr;                        // pinned readback of the queue length
   hipEvent_t ev3 = nullptr;
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
@@ -1060,6 +1232,58 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
   return IZPI_OK;
 }
 
+// Traversal kernel selection. IZPI_TRACE=1 picks the one-visit-per-iteration kernel
+// (k_trace, LDS stack sized by the host bound); the default 2 picks the step-scheduled
+// k_trace2 with an LDS ring of IZPI_TRACE_RING entries (8/16/32, default 16) and global
+// spill; IZPI_PRIM_W (default 32) weighs primitive steps against node steps (x/16).
+// All variants give identical results and counters.
+struct Tracer {
+  int variant = 2, stack = 32, ring = 16, wpe = 5;
+  uint32_t prim_w = 32;
+  int blocks = 0;
+};
+
+// k_trace2 instances: ring entries x minimum waves per SIMD (register budget).
+#define IZPI_T2_LIST(X) X(8, 4) X(8, 6) X(8, 8) X(16, 4) X(16, 5) X(16, 6) X(16, 8) X(32, 4)
+
+int make_tracer(izpi_ctx* ctx, Tracer* t) {
+  *t = Tracer();
+  if (const char* e = getenv("IZPI_TRACE")) t->variant = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("IZPI_TRACE_RING")) t->ring = atoi(e);
+  if (const char* e = getenv("IZPI_TRACE_WPE")) t->wpe = atoi(e);
+  if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
+  t->stack = ctx->stack_needed <= 32 ? 32 : 64;
+  int rc = IZPI_ERR_INVALID;
+  if (t->variant == 1) {
+    rc = t->stack == 32 ? resident_blocks(ctx, k_trace<32>, &t->blocks) : resident_blocks(ctx, k_trace<64>, &t->blocks);
+    return rc;
+  }
+#define IZPI_T2_OCC(R, W) if (t->ring == R && t->wpe == W) rc = resident_blocks(ctx, k_trace2<R, W>, &t->blocks);
+  IZPI_T2_LIST(IZPI_T2_OCC)
+#undef IZPI_T2_OCC
+  if (rc == IZPI_ERR_INVALID) { ctx->err = "no k_trace2 instance for IZPI_TRACE_RING/IZPI_TRACE_WPE"; return rc; }
+  if (rc) return rc;
+  return grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, (size_t)t->blocks * 256 * 64 * sizeof(int32_t));
+}
+
+void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStream_t st) {
+  const dim3 g(t.blocks), b(256);
+  if (t.variant == 1) {
+    if (t.stack == 32) hipLaunchKernelGGL(k_trace<32>, g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+    else hipLaunchKernelGGL(k_trace<64>, g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+    return;
+  }
+  const uint32_t stride = (uint32_t)t.blocks * 256;
+#define IZPI_T2_LAUNCH(R, W)                                                                                  \
+  if (t.ring == R && t.wpe == W) {                                                                           \
+    hipLaunchKernelGGL((k_trace2<R, W>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
+                       stride, t.prim_w);                                                                    \
+    return;                                                                                                  \
+  }
+  IZPI_T2_LIST(IZPI_T2_LAUNCH)
+#undef IZPI_T2_LAUNCH
+}
+
 uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint32_t n, uint32_t* tw, uint32_t* th) {
   if (n == 0) return 0;
   *tw = tiles[2] - tiles[0] + 1;
@@ -1075,12 +1299,13 @@ uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint3
 // One chunk loop of the wavefront scheme: k_start fills the slots, then k_trace /
 // k_shade alternate until no slot has a ray left; k_accumulate folds the chunk's
 // per-sample radiance into the pixels in sample order.
-template <int SAMPLER, int STACK, int MATSET>
+template <int SAMPLER, int MATSET>
 int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveParams& wp, AccumParams& ap,
                uint32_t num_pixels, uint32_t chunk, float* trace_ms, float* shade_ms, uint32_t* launches) {
   hipStream_t st = ctx->stream;
-  int trace_res = 0, shade_res = 0;
-  int rc = resident_blocks(ctx, k_trace<STACK>, &trace_res);
+  int shade_res = 0;
+  Tracer tr;
+  int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
   if ((rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res))) return rc;
   uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
@@ -1112,7 +1337,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
         HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
-        hipLaunchKernelGGL(k_trace<STACK>, dim3(trace_res), dim3(256), 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+        launch_trace(ctx, tr, wp, st);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
         hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, ctx->sc, sp, wp);
@@ -1165,19 +1390,21 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (num_pixels64 > (1ull << 30)) { ctx->err = "too many pixels in one request"; return IZPI_ERR_INVALID; }
   const uint32_t num_pixels = (uint32_t)num_pixels64;
   if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
-  const uint32_t stack = ctx->stack_needed <= 32 ? 32 : 64;
-  // chunking by spp keeps the per-sample buffer <= 64M samples (1.5 GiB)
-  uint64_t max_units = 64ull << 20;
+  // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
+  // sample order. One chunk per request when it fits in 1/4 of the free HBM (C3: 12.9 GB
+  // of 288 GB), so the wavefront drains once per frame instead of once per chunk.
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  uint64_t max_units = std::max<uint64_t>(64ull << 20, (uint64_t)(free_b / 4) / (3 * sizeof(double)));
   if (const char* e = getenv("IZPI_CHUNK_UNITS")) max_units = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
   // Paths in flight per wavefront pass. Larger = fewer k_trace/k_shade launches and
   // a smaller share of launch tails; costs HBM for the per-slot state (~176 B +
   // 48 B per depth level of unwinding records).
-  uint64_t slot_cap = 1ull << 23;
+  uint64_t slot_cap = 1ull << 24;
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
   {  // keep the wavefront state within a quarter of the free HBM
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+    if (free_b > 0) {
       const uint64_t per_slot = sizeof(RayRec) + sizeof(HitOut) + sizeof(PathSt) + 8 +
                                 (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
       slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 4) / per_slot));
@@ -1223,15 +1450,12 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   float trace_ms = 0, shade_ms = 0;
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
-#define IZPI_RUN(S, K, M) run_chunks<S, K, M>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
+#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
   const bool basic = ctx->basic_materials;
-  if (req->sampler == IZPI_SAMPLER_COLOUR) {
-    if (stack == 32) rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, 32, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, 32, MATSET_FULL);
-    else rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, 64, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, 64, MATSET_FULL);
-  } else {
-    if (stack == 32) rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 32, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 32, MATSET_FULL);
-    else rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 64, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, 64, MATSET_FULL);
-  }
+  if (req->sampler == IZPI_SAMPLER_COLOUR)
+    rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
+  else
+    rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_FULL);
 #undef IZPI_RUN
   if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, st));
@@ -1294,7 +1518,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   free_scene(ctx);
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
-                  ctx->d_counters, ctx->d_rays, ctx->d_hits, ctx->d_paths, ctx->d_queue};
+                  ctx->d_counters, ctx->d_rays, ctx->d_hits, ctx->d_paths, ctx->d_queue, ctx->d_spill};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
@@ -1546,11 +1770,10 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, q, ctx->d_misc + 3);
   WaveParams wp{};
   wp.rays = rr; wp.hits = ho; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
-  const uint32_t blocks = std::max(1u, std::min<uint32_t>((n + 255) / 256, 4096));
-  if (ctx->stack_needed <= 32)
-    hipLaunchKernelGGL(k_trace<32>, dim3(blocks), dim3(256), 0, ctx->stream, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
-  else
-    hipLaunchKernelGGL(k_trace<64>, dim3(blocks), dim3(256), 0, ctx->stream, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
+  Tracer tr;
+  int rc = make_tracer(ctx, &tr);
+  if (rc) return rc;
+  launch_trace(ctx, tr, wp, ctx->stream);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, ho, n, dh);
   HIP_TRY(hipGetLastError());

@@ -32,6 +32,7 @@ def main():
         variants = [dict(d, **{name: x}) for d in variants for x in vals.split(",")]
     times = {i: [] for i in range(len(variants))}
     ref = None
+    ref_cnt = None
     r.render()  # warm
     for _ in range(a.rounds):
         for i, env in enumerate(variants):
@@ -41,10 +42,12 @@ def main():
             img = r.render()
             times[i].append((time.perf_counter() - t) * 1e3)
             st = r.stats
+            cnt = tuple(st[k] for k in ("rays", "node_visits", "tri_tests", "sph_tests", "light_tri_tests"))
             if ref is None:
                 ref = img.copy()
-            elif img.tobytes() != ref.tobytes():
-                print("RESULT MISMATCH for", env, flush=True)
+                ref_cnt = cnt
+            elif img.tobytes() != ref.tobytes() or cnt != ref_cnt:
+                print("RESULT MISMATCH for", env, cnt, ref_cnt, flush=True)
             for k in env:
                 del os.environ[k]
             print("round", env, "%.1f ms" % times[i][-1], "trace %.1f shade %.1f launches %d" %
