@@ -68,6 +68,7 @@ struct DevScene {
   const double* spd_val;
   int32_t root;                 // encoded ref of BVH4.Nodes[0]; -1 when empty
   uint32_t num_lights;
+  uint32_t nan_free_bounds;     // no NaN in any inner-node bound: slab4_fast allowed
   izpi_camera cam;
 };
 
@@ -191,6 +192,45 @@ IZPI_DEV bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float 
   float tn = max32(max32(t0x, t0y), t0z);
   float tf = min32(min32(t1x, t1y), t1z);
   return tn <= tf && tf >= 0 && tn <= tmax;
+}
+
+// RayAABB4 over the 4 slots of an inner node, NaN-free fast form. When the ray's f32
+// origin is finite and its f32 inverse direction is finite and non-zero on every axis,
+// and the node bounds hold no NaN (checked once at upload), no t value can be NaN, so
+// the scalar twin's swap / max32 / min32 reduce to IEEE min/max (they can differ only in
+// the sign of a zero, which no comparison below sees): the mask is bit-identical.
+// The subtract and multiply run as packed f32 pairs (children 0-1 and 2-3), min3/max3
+// fold the three axes.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+IZPI_DEV uint32_t slab4_fast(float4 mnx, float4 mny, float4 mnz, float4 mxx, float4 mxy, float4 mxz, float ox, float oy,
+                             float oz, float ix, float iy, float iz, float tmax) {
+  const f32x2 o_x = {ox, ox}, o_y = {oy, oy}, o_z = {oz, oz};
+  const f32x2 i_x = {ix, ix}, i_y = {iy, iy}, i_z = {iz, iz};
+  const f32x2 a0x = (f32x2{mnx.x, mnx.y} - o_x) * i_x, a1x = (f32x2{mnx.z, mnx.w} - o_x) * i_x;
+  const f32x2 b0x = (f32x2{mxx.x, mxx.y} - o_x) * i_x, b1x = (f32x2{mxx.z, mxx.w} - o_x) * i_x;
+  const f32x2 a0y = (f32x2{mny.x, mny.y} - o_y) * i_y, a1y = (f32x2{mny.z, mny.w} - o_y) * i_y;
+  const f32x2 b0y = (f32x2{mxy.x, mxy.y} - o_y) * i_y, b1y = (f32x2{mxy.z, mxy.w} - o_y) * i_y;
+  const f32x2 a0z = (f32x2{mnz.x, mnz.y} - o_z) * i_z, a1z = (f32x2{mnz.z, mnz.w} - o_z) * i_z;
+  const f32x2 b0z = (f32x2{mxz.x, mxz.y} - o_z) * i_z, b1z = (f32x2{mxz.z, mxz.w} - o_z) * i_z;
+  const float t0x[4] = {a0x.x, a0x.y, a1x.x, a1x.y}, t1x[4] = {b0x.x, b0x.y, b1x.x, b1x.y};
+  const float t0y[4] = {a0y.x, a0y.y, a1y.x, a1y.y}, t1y[4] = {b0y.x, b0y.y, b1y.x, b1y.y};
+  const float t0z[4] = {a0z.x, a0z.y, a1z.x, a1z.y}, t1z[4] = {b0z.x, b0z.y, b1z.x, b1z.y};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x[i], t1x[i]), __builtin_fminf(t0y[i], t1y[i])),
+                                     __builtin_fminf(t0z[i], t1z[i]));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x[i], t1x[i]), __builtin_fmaxf(t0y[i], t1y[i])),
+                                     __builtin_fmaxf(t0z[i], t1z[i]));
+    m |= (tn <= tf && tf >= 0.0f && tn <= tmax) ? (1u << i) : 0u;
+  }
+  return m;
+}
+IZPI_DEV bool ray_fast_ok(float ox, float oy, float oz, float ix, float iy, float iz) {
+  const float inf = __builtin_huge_valf();
+  return __builtin_fabsf(ox) < inf && __builtin_fabsf(oy) < inf && __builtin_fabsf(oz) < inf &&
+         __builtin_fabsf(ix) < inf && __builtin_fabsf(iy) < inf && __builtin_fabsf(iz) < inf &&
+         ix != 0.0f && iy != 0.0f && iz != 0.0f;
 }
 
 // ----------------------------------------------------- primitive tests

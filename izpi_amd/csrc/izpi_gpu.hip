@@ -328,6 +328,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t cur = -1, pk = 0, pend = 0;
   int sp = 0, low = 0;
   int32_t bprim = -1;
+  bool fast = false;      // slab4_fast is exact for this ray
   for (;;) {
     const uint64_t idle = __ballot(!busy);
     if (idle != 0) {
@@ -348,6 +349,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             main_ray = r.kind == RAY_MAIN;
             ix = (float)(1.0 / r.d[0]); iy = (float)(1.0 / r.d[1]); iz = (float)(1.0 / r.d[2]);
             ox = (float)r.o[0]; oy = (float)r.o[1]; oz = (float)r.o[2];
+            fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
             cur = sc.root;
             sp = 0; low = 0;
             in_prim = false;
@@ -401,6 +403,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       c_sph += n_prim - n_tri;
     } else {
       c_nodes += n_node;
+      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
       // ---- node step: visit `cur` (bvh4.go:87-146)
       if (busy && !in_prim) {
         const float tm = (float)tmax;
@@ -421,10 +424,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
                       amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
                       amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
           const int32_t ach[4] = {ch.x, ch.y, ch.z, ch.w};
+          uint32_t hm;
+          if (wave_fast) {
+            hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
+          } else {
+            hm = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) hm |= 1u << i;
+          }
 #pragma unroll
           for (int i = 0; i < 4; i++) {
             if (ach[i] == -1) continue;
-            if (!slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) continue;
+            if (!(hm & (1u << i))) continue;
             if (next == -1) {
               next = ach[i];
             } else {  // push (bvh4.go:141-145)
@@ -1676,6 +1688,12 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   sc.mat_flags = dmf; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
+  sc.nan_free_bounds = 1;
+  for (const GInner& g : inner) {
+    const float* f = g.mnx;  // the 24 bounds are contiguous
+    for (int i = 0; i < 24; i++) if (f[i] != f[i]) sc.nan_free_bounds = 0;
+  }
+  if (getenv("IZPI_NO_FAST_SLAB")) sc.nan_free_bounds = 0;
   sc.cam = d->camera;
   // traversal stack bound (see host_scene.cpp stack_bound)
   {

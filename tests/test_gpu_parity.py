@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 RMSE_TOL = 1e-6  # north_star: pixel RMSE < 1e-6 vs reference
 
 
-def oracle_canvas(scene, W, H, spp, sampler, max_depth=50, tiles=None, seed=12345, bg=None):
+def oracle_canvas(scene, W, H, spp, sampler, max_depth=50, tiles=None, seed=12345, bg=None, threads=16):
     o = O.OracleScene(scene, aspect_override=W / H)
     req = N.RenderReq(width=W, height=H, spp=spp, max_depth=max_depth, sampler=sampler, seed=seed)
     keep = []
@@ -36,7 +36,7 @@ def oracle_canvas(scene, W, H, spp, sampler, max_depth=50, tiles=None, seed=1234
         req.num_bg_spd = len(wl)
         req.bg_spd_wavelengths = wl.ctypes.data_as(C.POINTER(C.c_double))
         req.bg_spd_values = val.ctypes.data_as(C.POINTER(C.c_double))
-    canvas, stats = o.render(req, threads=8)
+    canvas, stats = o.render(req, threads=threads)
     return canvas.reshape(H, W, 4), stats
 
 
@@ -193,4 +193,88 @@ def test_tiles_packed_and_unpack(gpu):
     r.unpack(sub, packed.data_ptr(), canvas.data_ptr())
     torch.cuda.synchronize()
     assert_parity(canvas.cpu().numpy(), ref)
+    r.close()
+
+
+@pytest.mark.parametrize("env", [{"IZPI_TRACE": "1"}, {"IZPI_TRACE_RING": "8", "IZPI_TRACE_WPE": "4"},
+                                 {"IZPI_TRACE_RING": "32", "IZPI_TRACE_WPE": "4"}, {"IZPI_PRIM_W": "1"},
+                                 {"IZPI_PRIM_W": "100000"}, {"IZPI_SLOTS": "3000", "IZPI_CHUNK_UNITS": "5000"}])
+def test_kernel_variants_bitwise(gpu, env, monkeypatch):
+    """Traversal kernel variants, the LDS-ring spill path, step weights and tiny
+    slot/chunk counts are launch knobs only: results and counters must not move."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scene = configs.cornell_dragon(1.0, n=60)
+    r = GPURenderer(scene, 64, 64, 4)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
+
+
+def test_slow_slab_path_bitwise(gpu, monkeypatch):
+    """The NaN-free packed slab (slab4_fast) and the scalar twin give the same image."""
+    monkeypatch.setenv("IZPI_NO_FAST_SLAB", "1")
+    scene = configs.cornell_dragon(1.0, n=60)
+    r = GPURenderer(scene, 64, 64, 4)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
+
+
+def test_axis_aligned_rays_trace_bitwise(gpu):
+    """Rays with zero direction components (infinite f32 inverses) take the scalar-twin
+    slab path; origins on slab planes give 0*inf = NaN there (A14)."""
+    scene = configs.cornell_dragon(1.0, n=40)
+    o = O.OracleScene(scene, aspect_override=1.0)
+    r = GPURenderer(scene, 8, 8, 1)
+    rng = np.random.default_rng(7)
+    rays = []
+    for i in range(4096):
+        org = rng.uniform(-10, 110, 3)
+        if i % 3 == 0:
+            org = np.round(org)  # lands on box planes (x = 0, 100 ...) exactly
+        d = np.zeros(3)
+        d[i % 3] = 1.0 if (i // 3) % 2 else -1.0
+        if i % 5 == 0:
+            d[(i + 1) % 3] = rng.uniform(-1, 1)
+        rays.append(list(org) + list(d) + [0.001, 1e300])
+    rays = np.ascontiguousarray(rays, np.float64)
+    got = (N.Hit * len(rays))()
+    assert N.lib().izpi_gpu_trace(r.ctx, rays.ctypes.data_as(C.POINTER(C.c_double)), len(rays), got) == 0
+    want = o.trace(rays)
+    nhit = 0
+    for i in range(len(rays)):
+        g, w = got[i], want[i]
+        assert g.hit == w.hit, i
+        if w.hit:
+            nhit += 1
+            assert g.prim_ref == w.prim_ref, i
+            assert bytes(g)[:72] == bytes(w)[:72], i
+    assert nhit > 1000
+    r.close()
+
+
+def test_full_size_c3_frame_low_spp_bitwise(gpu):
+    """BASELINE.json's full C3 frame (1024x1024, 817k-triangle dragon) at 2 spp: every
+    pixel bit-identical to the oracle, counters equal."""
+    cfg = configs.configs()["C3"]
+    scene = cfg.build()
+    r = GPURenderer(scene, cfg.width, cfg.height, 2)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, 2, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
+
+
+def test_full_size_c3_tiles_full_spp_bitwise(gpu):
+    """Four centre tiles of the C3 frame at the metric's full 512 spp."""
+    cfg = configs.configs()["C3"]
+    scene = cfg.build()
+    tiles = common_tiles(cfg.width, cfg.height)[:4]  # spiral order starts at the centre
+    r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp)
+    img = r.render(tiles=tiles)
+    ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, cfg.spp, N.SAMPLER_COLOUR, tiles=tiles)
+    assert_parity(img, ref, r.stats, ostats)
     r.close()
