@@ -41,6 +41,13 @@ struct alignas(16) GPrim {
   uint32_t kind;    // IZPI_PRIM_*
   uint32_t index;   // transport-order index (shading data, lights)
 };
+// Shading record of a primitive, in BVH leaf order next to GPrim: everything the
+// deferred hit record needs for a constant-textured triangle in one 32-B line.
+struct alignas(32) GShade {
+  double n[3];      // triangle: unit(e1 x e2) (triangle.go:100); sphere: unused
+  uint32_t mat;     // material index
+  uint32_t ref;     // IZPI_PRIM_REF(kind, transport index)
+};
 // Light record (Scene.Lights entry, transport order): everything PDFValue/Random read.
 struct alignas(16) GLight {
   double v0[3], v1[3], v2[3], e1[3], e2[3], n[3];  // triangle
@@ -53,6 +60,7 @@ struct DevScene {
   const GInner* inner;
   const GLeaf* leaves;
   const GPrim* prims;
+  const GShade* shade;          // [num_prims], leaf order
   const double* tri_normal;     // [nt][3]
   const double* tri_uv;         // [nt][6]
   const double* tri_tangent;    // [nt][3]

@@ -312,7 +312,8 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
 // are kept per wave in SGPRs (popcounts of ballots).
 template <int S, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
-                                                uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w) {
+                                                uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
+                                                uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   __shared__ int32_t lds_stack[S * 256];
   int32_t* stk = lds_stack + threadIdx.x;
@@ -329,20 +330,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int sp = 0, low = 0;
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
+  uint32_t c_pos = 0, c_end = 0;  // wave-private range [c_pos, c_end) of the input queue
   for (;;) {
     const uint64_t idle = __ballot(!busy);
     if (idle != 0) {
       const uint32_t nidle = (uint32_t)__popcll(idle);
-      if (!exhausted && (nidle >= 16 || idle == ~0ull)) {
-        const uint32_t leader = (uint32_t)__ffsll((long long)idle) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(wp.trace_next, nidle);
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, (int)leader));
-        if (base + nidle >= n) exhausted = true;
+      if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos >= c_end) {
+        // the wave's private range of the queue is used up: take the next `tchunk`
+        // entries with one atomic (a single head word saturates near 88 dequeues/us)
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(wp.trace_next, tchunk);
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (b >= n) exhausted = true;
+        c_pos = b;
+        c_end = b + tchunk < n ? b + tchunk : n;
+      }
+      if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos < c_end) {
+        const uint32_t take = nidle < c_end - c_pos ? nidle : c_end - c_pos;
+        const uint32_t base = c_pos;
+        c_pos += take;
         bool main_ray = false;
         if (!busy) {
-          const uint32_t my = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
-          if (my < n) {
+          const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
+          const uint32_t my = base + rank;
+          if (rank < take) {
             slot = wp.q_in[my];
             const RayRec& r = wp.rays[slot];
             tmax = r.tmax;
@@ -486,40 +497,44 @@ struct HitRec {
   V3 p, n;
   uint32_t mat;
 };
-IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, V3 o, V3 d, double time, bool want_uv, HitRec& h) {
-  const GPrim& pr = sc.prims[c.prim];
+IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const GShade& gs, V3 o, V3 d, double time, bool want_uv,
+                         HitRec& h) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
-  if (pr.kind == IZPI_PRIM_TRIANGLE) {
-    const uint32_t ti = pr.index;
-    const double eps = 1e-8;
-    double u = c.u, v = c.v;
-    double w = 1.0 - u - v;
-    double sum = u + v + w;
-    if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
-    const double* uv = sc.tri_uv + 6 * (size_t)ti;  // u0,v0,u1,v1,u2,v2
-    h.u = w * uv[0] + u * uv[2] + v * uv[4];
-    h.v = w * uv[1] + u * uv[3] + v * uv[5];
-    h.mat = sc.tri_mat[ti];
-    V3 n = ld3(sc.tri_normal + 3 * (size_t)ti);
-    const izpi_material& m = sc.materials[h.mat];
-    if (m.kind == IZPI_MAT_PBR && m.normal_tex >= 0) {  // Material.NormalMap() != nil
-      V3 nts = tex_rgb(sc, m.normal_tex, h.u, h.v);
-      nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
-      V3 tg = ld3(sc.tri_tangent + 3 * (size_t)ti), bt = ld3(sc.tri_bitangent + 3 * (size_t)ti);
-      V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
-                 tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
-      n = sdiv(nn, length(nn));
+  h.mat = gs.mat;
+  if (IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
+    const uint32_t ti = IZPI_PRIM_INDEX(gs.ref);
+    V3 n = mk(gs.n[0], gs.n[1], gs.n[2]);
+    if (want_uv) {  // (u,v) are read only by image textures and normal maps
+      const double eps = 1e-8;
+      double u = c.u, v = c.v;
+      double w = 1.0 - u - v;
+      double sum = u + v + w;
+      if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
+      const double* uv = sc.tri_uv + 6 * (size_t)ti;  // u0,v0,u1,v1,u2,v2
+      h.u = w * uv[0] + u * uv[2] + v * uv[4];
+      h.v = w * uv[1] + u * uv[3] + v * uv[5];
+      const izpi_material& m = sc.materials[h.mat];
+      if (m.kind == IZPI_MAT_PBR && m.normal_tex >= 0) {  // Material.NormalMap() != nil
+        V3 nts = tex_rgb(sc, m.normal_tex, h.u, h.v);
+        nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
+        V3 tg = ld3(sc.tri_tangent + 3 * (size_t)ti), bt = ld3(sc.tri_bitangent + 3 * (size_t)ti);
+        V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
+                   tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
+        n = sdiv(nn, length(nn));
+      }
+    } else {
+      h.u = 0; h.v = 0;
     }
     h.n = n;
   } else {
+    const GPrim& pr = sc.prims[c.prim];
     double pa[9];
     for (int q = 0; q < 9; q++) pa[q] = pr.a[q];
     V3 ctr = sph_center(pa, time);
     V3 on = sdiv(sub(h.p, ctr), pa[6]);
     V3 flipped = dot(d, on) >= 0 ? smul(on, -1) : on;
     h.n = c.u == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
-    h.mat = sc.sph_mat[pr.index];
     if (want_uv) {
       double phi = gm::atan2(flipped.z, flipped.x);
       double theta = gm::asin(flipped.y);
@@ -756,15 +771,39 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slo
 }
 
 // Append `push` lanes' slots to the output queue: one atomic per wave.
-IZPI_DEV void queue_push(const WaveParams& wp, bool push, uint32_t slot) {
+IZPI_DEV void queue_push(uint32_t* q, uint32_t* count, bool push, uint32_t slot) {
   const uint64_t m = __ballot(push);
   if (m == 0) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
   uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(wp.q_out_count, (uint32_t)__popcll(m));
+  if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
   base = __shfl(base, (int)leader);
-  if (push) wp.q_out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = slot;
+  if (push) q[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = slot;
+}
+IZPI_DEV void queue_push(const WaveParams& wp, bool push, uint32_t slot) { queue_push(wp.q_out, wp.q_out_count, push, slot); }
+
+// Block-wide reservation: every lane with `want` gets a distinct index from `counter`,
+// with ONE atomic per 256-thread block (a single counter word saturates near 88
+// returning atomics/us chip-wide, MI355X_MICROARCH.md "dequeue"). All threads of the
+// block must call it (block-uniform control flow).
+IZPI_DEV uint32_t block_reserve(uint32_t* counter, bool want) {
+  __shared__ uint32_t s_w[4];
+  __shared__ uint32_t s_base;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t m = __ballot(want);
+  if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    s_base = tot ? atomicAdd(counter, tot) : 0u;
+  }
+  __syncthreads();
+  uint32_t off = s_base;
+  for (uint32_t i = 0; i < w; i++) off += s_w[i];
+  off += (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  __syncthreads();  // s_w / s_base are reused by the next call
+  return off;
 }
 
 // Take units for the lanes that ask (one atomic per wave); returns UINT32_MAX when drained.
@@ -808,22 +847,39 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
   queue_push(wp, push, slot);
 }
 
+// Partial stores of the per-slot records: only the fields a pass changes are written,
+// so k_shade does not keep the untouched ones (ray time, wavelength, ...) in registers.
+IZPI_DEV void store_ray(RayRec* rr, V3 o, V3 d, double tmin, double tmax, uint32_t kind, uint32_t pad) {
+  double2* p = reinterpret_cast<double2*>(rr);
+  p[0] = make_double2(o.x, o.y);
+  p[1] = make_double2(o.z, d.x);
+  p[2] = make_double2(d.y, d.z);
+  p[3] = make_double2(tmin, tmax);
+  *reinterpret_cast<uint2*>(&rr->kind) = make_uint2(kind, pad);  // rr->time is left as is
+}
+IZPI_DEV void store_path_rng_depth(PathSt* ps, uint32_t rng, uint32_t depth) {
+  *reinterpret_cast<uint2*>(&ps->rng) = make_uint2(rng, depth);
+}
+
 // One shading pass over the slots traced in the previous k_trace.
 // MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
 // DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
 // footprint small; MATSET_FULL adds Dielectric, Metal and PBR. The host picks the
 // variant from the scene's material kinds (results are identical).
 enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
+#ifndef IZPI_SHADE_WPE
+#define IZPI_SHADE_WPE 3  // MATSET_BASIC register budget: 3 waves/SIMD (no spill; 4 spills ~150 B/lane)
+#endif
 template <int SAMPLER, int MATSET>
-__global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET == MATSET_BASIC && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE : 1)))
+k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const uint32_t n = *wp.q_in_count;
   uint32_t c_lt = 0, c_ls = 0;
   const uint32_t stride = gridDim.x * 256;
-  // Uniform trip count per wave so the wave-level queue/unit atomics stay convergent.
-  const uint32_t first = blockIdx.x * 256 + (threadIdx.x & ~63u);
-  for (uint32_t base = first; base < n; base += stride) {
-    const uint32_t i = base + (threadIdx.x & 63);
+  // Block-uniform trip count: the queue and unit reservations are block-wide.
+  for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
+    const uint32_t i = base + threadIdx.x;
     const bool valid = i < n;
     uint32_t slot = valid ? wp.q_in[i] : 0;
     bool push = false;      // slot has a ray to trace next
@@ -863,10 +919,9 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
                    : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
         terminal = true;
       } else {
-        const GPrim& pr = sc.prims[H.prim];
-        const uint32_t mat_id = pr.kind == IZPI_PRIM_TRIANGLE ? sc.tri_mat[pr.index] : sc.sph_mat[pr.index];
+        const GShade gs = sc.shade[H.prim];
         HitRec h;
-        hit_record(sc, H, ro, rd, R.time, (sc.mat_flags[mat_id] & 1u) != 0, h);
+        hit_record(sc, H, gs, ro, rd, R.time, (sc.mat_flags[gs.mat] & 1u) != 0, h);
         hit_n = h.n;
         next_o = h.p;
         const izpi_material& m = sc.materials[h.mat];
@@ -896,15 +951,10 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
             const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
             if (!reflected && (!COLOUR || beer_rgb)) {
               // the extra World.Hit of calculatePathLength: trace it, finish next pass
-              P.pend[0] = h.p.x; P.pend[1] = h.p.y; P.pend[2] = h.p.z;
-              P.rng = rng.s;
-              V3 start = add(h.p, smul(next_d, 0.001));
-              R.o[0] = start.x; R.o[1] = start.y; R.o[2] = start.z;
-              R.d[0] = next_d.x; R.d[1] = next_d.y; R.d[2] = next_d.z;
-              R.tmin = 0.0; R.tmax = 1000.0;
-              R.kind = RAY_PATHLEN; R.pad = h.mat;
-              wp.paths[slot] = P;
-              wp.rays[slot] = R;
+              PathSt* ps = wp.paths + slot;
+              ps->pend[0] = h.p.x; ps->pend[1] = h.p.y; ps->pend[2] = h.p.z;
+              store_path_rng_depth(ps, rng.s, P.depth);
+              store_ray(wp.rays + slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
               push = true;
               break;
             }
@@ -982,12 +1032,16 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
             V3 dir;
             if (rng.next() < 0.5) dir = lights_random(sc, next_o, rng);
             else dir = cos_onb.local(random_cosine_direction(rng));
-            double cosv = dot(unit(dir), cos_onb.w);
-            double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
-            double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
-            double sc_cos = dot(hit_n, unit(dir));  // ScatteringPDF with the hit normal
+            // (evaluated in an order that frees the ONB, normal and attenuation before
+            // the light-pdf loop; every value is computed exactly as in the reference)
+            const V3 ud = unit(dir);
+            const double cosv = dot(ud, cos_onb.w);
+            const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
+            double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
             if (sc_cos < 0) sc_cos = 0;
-            rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, pdf_val);
+            rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, 0);
+            const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
+            sp.recs[((size_t)P.depth * 6 + 5) * sp.slots + slot] = pdf_val;
             next_d = dir;
           } else {
             rec_store<SAMPLER>(sp, slot, P.depth, true, att, 0, 0);
@@ -998,22 +1052,18 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
             finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
             done = true;
           } else {
-            R.o[0] = next_o.x; R.o[1] = next_o.y; R.o[2] = next_o.z;
-            R.d[0] = next_d.x; R.d[1] = next_d.y; R.d[2] = next_d.z;
-            R.tmin = 0.001; R.tmax = 1.7976931348623157e308;
-            R.kind = RAY_MAIN; R.pad = 0;
-            wp.paths[slot] = P;
-            wp.rays[slot] = R;
+            store_path_rng_depth(wp.paths + slot, P.rng, P.depth);
+            store_ray(wp.rays + slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0);
             push = true;
           }
         }
       }
     }
-    // refill finished slots with new work units (wave-uniform loop)
+    // refill finished slots with new work units (block-uniform loop)
     bool want = done;
-    for (;;) {
-      if (__ballot(want) == 0) break;
-      const uint32_t unit = grab_unit(sp, want);
+    while (__syncthreads_or(want)) {
+      const uint32_t u = block_reserve(sp.head, want);
+      const uint32_t unit = u < sp.total_units ? u : 0xFFFFFFFFu;
       if (want) {
         if (unit == 0xFFFFFFFFu) {
           want = false;
@@ -1029,7 +1079,8 @@ __global__ void __launch_bounds__(256) k_shade(const DevScene sc, const ShadePar
         }
       }
     }
-    queue_push(wp, push, slot);
+    const uint32_t pos = block_reserve(wp.q_out_count, push);
+    if (push) wp.q_out[pos] = slot;
   }
   const uint32_t lane = threadIdx.x & 63;
   unsigned long long vals[2] = {c_lt, c_ls};
@@ -1126,7 +1177,8 @@ __global__ void k_trace_records(const DevScene sc, const RayRec* rr, const HitOu
   if (c.prim >= 0) {
     const RayRec R = rr[i];
     HitRec hr;
-    hit_record(sc, c, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
+    const GShade gs = sc.shade[c.prim];
+    hit_record(sc, c, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
     const GPrim& p = sc.prims[c.prim];
     h.hit = 1; h.t = hr.t; h.u = hr.u; h.v = hr.v;
     h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
@@ -1187,7 +1239,7 @@ struct izpi_ctx {
   double* d_out = nullptr; size_t out_cap = 0;
   uint32_t* d_tiles = nullptr; size_t tiles_cap = 0;
   double* d_bg = nullptr; size_t bg_cap = 0;
-  uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts
+  uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts, [5] free count
   unsigned long long* d_counters = nullptr;
   RayRec* d_rays = nullptr; size_t rays_cap = 0;
   HitOut* d_hits = nullptr; size_t hits_cap = 0;
@@ -1251,7 +1303,7 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 // All variants give identical results and counters.
 struct Tracer {
   int variant = 2, stack = 32, ring = 16, wpe = 5;
-  uint32_t prim_w = 32;
+  uint32_t prim_w = 32, tchunk = 128, refill_min = 32;
   int blocks = 0;
 };
 
@@ -1264,6 +1316,8 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   if (const char* e = getenv("IZPI_TRACE_RING")) t->ring = atoi(e);
   if (const char* e = getenv("IZPI_TRACE_WPE")) t->wpe = atoi(e);
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
   t->stack = ctx->stack_needed <= 32 ? 32 : 64;
   int rc = IZPI_ERR_INVALID;
   if (t->variant == 1) {
@@ -1289,7 +1343,7 @@ void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStrea
 #define IZPI_T2_LAUNCH(R, W)                                                                                  \
   if (t.ring == R && t.wpe == W) {                                                                           \
     hipLaunchKernelGGL((k_trace2<R, W>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
-                       stride, t.prim_w);                                                                    \
+                       stride, t.prim_w, t.tchunk, t.refill_min);                                            \
     return;                                                                                                  \
   }
   IZPI_T2_LIST(IZPI_T2_LAUNCH)
@@ -1417,7 +1471,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
   {  // keep the wavefront state within a quarter of the free HBM
     if (free_b > 0) {
-      const uint64_t per_slot = sizeof(RayRec) + sizeof(HitOut) + sizeof(PathSt) + 8 +
+      const uint64_t per_slot = sizeof(RayRec) + sizeof(HitOut) + sizeof(PathSt) + 12 +
                                 (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
       slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 4) / per_slot));
     }
@@ -1432,7 +1486,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if ((rc = grow(ctx, (void**)&ctx->d_rays, &ctx->rays_cap, (size_t)slots * sizeof(RayRec)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_hits, &ctx->hits_cap, (size_t)slots * sizeof(HitOut)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_paths, &ctx->paths_cap, (size_t)slots * sizeof(PathSt)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)2 * slots * sizeof(uint32_t)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)3 * slots * sizeof(uint32_t)))) return rc;
   const size_t nbg = req->num_bg_spd;
   if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
   hipStream_t st = ctx->stream;
@@ -1443,7 +1497,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   }
   HIP_TRY(hipMemsetAsync(ctx->d_running, 0, (size_t)num_pixels * 3 * sizeof(double), st));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), st));
-  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 5 * sizeof(uint32_t), st));
+  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 6 * sizeof(uint32_t), st));
 
   ShadeParams sp{};
   sp.width = req->width; sp.height = req->height; sp.max_depth = req->max_depth;
@@ -1592,16 +1646,23 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   }
   // ---- primitives in leaf order
   std::vector<GPrim> prims(d->num_prims);
+  std::vector<GShade> shade(d->num_prims);
   for (uint32_t k = 0; k < d->num_prims; k++) {
     const uint32_t r = d->prim_ref[k], kind = IZPI_PRIM_KIND(r), idx = IZPI_PRIM_INDEX(r);
     GPrim& g = prims[k];
     g.kind = kind; g.index = idx;
+    GShade& gs = shade[k];
+    memset(&gs, 0, sizeof(gs));
+    gs.ref = r;
     if (kind == IZPI_PRIM_TRIANGLE) {
       if (idx >= nt) { ctx->err = "triangle ref out of range"; return IZPI_ERR_INVALID; }
+      memcpy(gs.n, d->tri_normal + 3 * (size_t)idx, 24);
+      gs.mat = d->tri_mat[idx];
       memcpy(g.a, d->tri_v0 + 3 * (size_t)idx, 24); memcpy(g.a + 3, d->tri_e1 + 3 * (size_t)idx, 24);
       memcpy(g.a + 6, d->tri_e2 + 3 * (size_t)idx, 24);
     } else {
       if (idx >= ns) { ctx->err = "sphere ref out of range"; return IZPI_ERR_INVALID; }
+      gs.mat = d->sph_mat[idx];
       memcpy(g.a, d->sph_center0 + 3 * (size_t)idx, 24); memcpy(g.a + 3, d->sph_center1 + 3 * (size_t)idx, 24);
       g.a[6] = d->sph_radius[idx]; g.a[7] = d->sph_time[2 * (size_t)idx]; g.a[8] = d->sph_time[2 * (size_t)idx + 1];
     }
@@ -1663,13 +1724,14 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   // ---- upload
   DevScene& sc = ctx->sc;
   memset(&sc, 0, sizeof(sc));
-  GInner* di; GLeaf* dl; GPrim* dp; GLight* dlt;
+  GInner* di; GLeaf* dl; GPrim* dp; GShade* dsh; GLight* dlt;
   double *dn, *duv, *dtg, *dbt, *dtex, *dswl, *dsv;
   uint32_t *dtm, *dsm, *dmf;
   izpi_material* dm; izpi_texture* dtx;
   UP(inner.data(), inner.size(), &di);
   UP(leaves.data(), leaves.size(), &dl);
   UP(prims.data(), prims.size(), &dp);
+  UP(shade.data(), shade.size(), &dsh);
   UP(d->tri_normal, 3 * (size_t)nt, &dn);
   UP(d->tri_uv, 6 * (size_t)nt, &duv);
   UP(d->tri_tangent, 3 * (size_t)nt, &dtg);
@@ -1683,7 +1745,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(d->texels, d->num_texels, &dtex);
   UP(d->spd_wavelengths, d->num_spd, &dswl);
   UP(d->spd_values, d->num_spd, &dsv);
-  sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.tri_normal = dn; sc.tri_uv = duv; sc.tri_tangent = dtg;
+  sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tri_normal = dn; sc.tri_uv = duv; sc.tri_tangent = dtg;
   sc.tri_bitangent = dbt; sc.tri_mat = dtm; sc.sph_mat = dsm; sc.lights = dlt; sc.materials = dm;
   sc.mat_flags = dmf; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
