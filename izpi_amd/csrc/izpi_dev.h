@@ -30,7 +30,7 @@ __host__ __device__ inline int32_t leaf_id(int32_t r) { return -r - 2; }
 struct alignas(16) GInner {
   float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
   int32_t child[4];
-  int32_t pad[4];
+  int32_t leaf[4];  // leaf child: (prim start << 3) | count when its box equals this slot's, else 0
 };
 struct alignas(16) GLeaf {
   float mn[3], mx[3];

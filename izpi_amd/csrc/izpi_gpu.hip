@@ -379,6 +379,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     if ((m_prim | m_node) == 0) continue;
     const uint32_t n_prim = (uint32_t)__popcll(m_prim), n_node = (uint32_t)__popcll(m_node);
     bool advance = false;   // lane finished its current node / leaf: take next or pop
+    bool leaf_next = false; // the node step went straight into its first child leaf
     int32_t next = -1;
     if (n_prim * prim_w >= n_node * 16u) {
       // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134)
@@ -420,9 +421,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const float tm = (float)tmax;
         if (ref_is_leaf(cur)) {
           const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_id(cur));
-          const float4 a = lp[0], b = lp[1];
+          const float4 a = lp[0], b = lp[1];  // both loads issued together
           const int32_t start = __float_as_int(b.z), count = __float_as_int(b.w);
-          if (count > 0 && slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
+          const bool hit = slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm);
+          if (hit & (count > 0)) {
             in_prim = true; pk = start; pend = start + count;
           } else {
             advance = true;
@@ -431,41 +433,54 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
           const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
           const int4 ch = *reinterpret_cast<const int4*>(np + 6);
-          const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
-                      amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
-                      amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
-          const int32_t ach[4] = {ch.x, ch.y, ch.z, ch.w};
+          const int4 lf = *reinterpret_cast<const int4*>(np + 7);  // leaf-child shortcuts (GInner::leaf)
           uint32_t hm;
           if (wave_fast) {
             hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
           } else {
+            const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
+                        amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
+                        amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
             hm = 0;
 #pragma unroll
             for (int i = 0; i < 4; i++)
               if (slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) hm |= 1u << i;
           }
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            if (ach[i] == -1) continue;
-            if (!(hm & (1u << i))) continue;
-            if (next == -1) {
-              next = ach[i];
-            } else {  // push (bvh4.go:141-145)
-              if (sp >= 64) {
-                atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
-              } else {
-                if (sp - low >= S) {  // ring full: spill the oldest entry
-                  gsp[(size_t)low * spill_stride] = stk[(low & (S - 1)) * 256];
-                  low++;
-                }
-                stk[(sp & (S - 1)) * 256] = ach[i];
-                sp++;
+          // slots 0..3 with ChildIndex != -1 whose box is hit (bvh4.go:119-146): the first
+          // is visited next, the others are pushed in slot order (popped LIFO).
+          const uint32_t m = hm & ((ch.x != -1 ? 1u : 0u) | (ch.y != -1 ? 2u : 0u) | (ch.z != -1 ? 4u : 0u) |
+                                   (ch.w != -1 ? 8u : 0u));
+          const uint32_t f = m & 1u ? 0u : (m & 2u ? 1u : (m & 4u ? 2u : 3u));
+          next = m == 0 ? -1 : (f == 0 ? ch.x : (f == 1 ? ch.y : (f == 2 ? ch.z : ch.w)));
+          // A leaf visited straight after its parent re-tests the same f32 box with the
+          // same tMax (A10): the result is known to be a hit, so skip its node load and
+          // start on its primitives (the visit is still counted).
+          const int32_t lfe = f == 0 ? lf.x : (f == 1 ? lf.y : (f == 2 ? lf.z : lf.w));
+          if (m != 0 && lfe != 0) {
+            in_prim = true; pk = lfe >> 3; pend = pk + (lfe & 7);
+            next = -1;
+            leaf_next = true;
+          }
+          const uint32_t rest = m & (m - 1u);  // bits 1..3 only
+          const int np_ = __builtin_popcount(rest);
+          if (np_ > 0) {
+            if (sp + np_ > 64) {
+              atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
+            } else {
+              while (sp + np_ - low > S) {  // ring full: spill the oldest entries (rare)
+                gsp[(size_t)low * spill_stride] = stk[(low & (S - 1)) * 256];
+                low++;
               }
+              if (rest & 2u) stk[(sp & (S - 1)) * 256] = ch.y;
+              if (rest & 4u) stk[((sp + ((rest & 2u) ? 1 : 0)) & (S - 1)) * 256] = ch.z;
+              if (rest & 8u) stk[((sp + np_ - 1) & (S - 1)) * 256] = ch.w;
+              sp += np_;
             }
           }
-          advance = true;
+          advance = !leaf_next;
         }
       }
+      c_nodes += (uint64_t)__popcll(__ballot(leaf_next));
     }
     if (advance) {
       if (next != -1) {
@@ -1299,11 +1314,11 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 // Traversal kernel selection. IZPI_TRACE=1 picks the one-visit-per-iteration kernel
 // (k_trace, LDS stack sized by the host bound); the default 2 picks the step-scheduled
 // k_trace2 with an LDS ring of IZPI_TRACE_RING entries (8/16/32, default 16) and global
-// spill; IZPI_PRIM_W (default 32) weighs primitive steps against node steps (x/16).
+// spill; IZPI_PRIM_W (default 16) weighs primitive steps against node steps (x/16).
 // All variants give identical results and counters.
 struct Tracer {
   int variant = 2, stack = 32, ring = 16, wpe = 5;
-  uint32_t prim_w = 32, tchunk = 128, refill_min = 32;
+  uint32_t prim_w = 16, tchunk = 128, refill_min = 32;
   int blocks = 0;
 };
 
@@ -1640,7 +1655,18 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
         int32_t c = n.child[i];
         if (c != -1 && (c < 0 || (uint32_t)c >= d->num_nodes)) { ctx->err = "child index out of bounds"; return IZPI_ERR_INVALID; }
         g.child[i] = c == -1 ? -1 : ref[(size_t)c];
-        g.pad[i] = 0;
+        g.leaf[i] = 0;
+        if (c >= 0 && ref[(size_t)c] <= -2) {
+          // leaf child: shortcut entry (start << 3 | count) when the leaf's slot-0 box is
+          // bit-identical to this slot's box (so its re-test straight after this visit
+          // is known to pass), else 0
+          const izpi_bvh4_node& lnode = d->nodes[(size_t)c];
+          const float pb[6] = {n.min_x[i], n.min_y[i], n.min_z[i], n.max_x[i], n.max_y[i], n.max_z[i]};
+          const float lb[6] = {lnode.min_x[0], lnode.min_y[0], lnode.min_z[0], lnode.max_x[0], lnode.max_y[0], lnode.max_z[0]};
+          const int32_t st = lnode.child[0], cnt = lnode.prim_count[0];
+          if (memcmp(pb, lb, sizeof(pb)) == 0 && st >= 0 && st < (1 << 27) && cnt >= 1 && cnt <= 7)
+            g.leaf[i] = (st << 3) | cnt;
+        }
       }
     }
   }
