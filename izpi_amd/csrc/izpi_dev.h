@@ -5,7 +5,8 @@
 //   GInner  128 B  inner BVH4 nodes: SoA f32 bounds of 4 children + encoded child refs.
 //                  (== hitable.BVH4Node, bvh4.go:23-39, with PrimitiveCount — always 0 in
 //                  inner nodes — replaced by nothing; leaf children become leaf refs).
-//   GLeaf   32 B   one per reference leaf node: its slot-0 bounds + primitive range.
+//   GLeaf   32 B   one per reference leaf node, indexed by its first primitive: its slot-0
+//                  bounds + primitive range.
 //                  A reference leaf node carries only slot 0 (bvh4.go:736-760), so the
 //                  re-test on visit (quirk A10) needs 32 B instead of a 128 B node load.
 //   GPrim   80 B   primitives in BVH leaf order: triangle v0,e1,e2 (the 72 B Hit reads,
@@ -23,14 +24,18 @@
 namespace izd {
 
 // child ref encoding inside GInner / the traversal stack
-//   r >= 0 : inner node index;   r == -1 : empty slot;   r <= -2 : leaf id (-r - 2)
+//   r >= 0 : inner node index;   r == -1 : empty slot;   r <= -2 : leaf (below)
+//   leaf refs carry the leaf's primitive range: r = -(1 + (start << 3 | count)), count 1..4
+//   (bvh4.go:638-642 makes leaves of <= 4 primitives)
 __host__ __device__ inline bool ref_is_leaf(int32_t r) { return r <= -2; }
-__host__ __device__ inline int32_t leaf_id(int32_t r) { return -r - 2; }
+__host__ __device__ inline int32_t leaf_start(int32_t r) { return (-r - 1) >> 3; }
+__host__ __device__ inline int32_t leaf_count(int32_t r) { return (-r - 1) & 7; }
+__host__ __device__ inline int32_t make_leaf_ref(int32_t start, int32_t count) { return -(1 + ((start << 3) | count)); }
 
 struct alignas(16) GInner {
   float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
   int32_t child[4];
-  int32_t leaf[4];  // leaf child: (prim start << 3) | count when its box equals this slot's, else 0
+  int32_t pad[4];
 };
 struct alignas(16) GLeaf {
   float mn[3], mx[3];
@@ -77,6 +82,7 @@ struct DevScene {
   int32_t root;                 // encoded ref of BVH4.Nodes[0]; -1 when empty
   uint32_t num_lights;
   uint32_t nan_free_bounds;     // no NaN in any inner-node bound: slab4_fast allowed
+  uint32_t leaf_shortcut;       // every leaf's slot-0 box equals its parent slot's box
   izpi_camera cam;
 };
 

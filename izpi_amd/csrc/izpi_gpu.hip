@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
     const float tm = (float)tmax;
     int32_t next = -1;
     if (ref_is_leaf(cur)) {
-      const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_id(cur));
+      const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_start(cur));
       const float4 a = lp[0], b = lp[1];
       if (slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
         const int32_t start = __float_as_int(b.z), count = __float_as_int(b.w);
@@ -328,6 +328,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
   int32_t cur = -1, pk = 0, pend = 0;
   int sp = 0, low = 0;
+  int clean_from = 0;     // stack entries at positions >= clean_from were pushed after the last accepted hit
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
   uint32_t c_pos = 0, c_end = 0;  // wave-private range [c_pos, c_end) of the input queue
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             ox = (float)r.o[0]; oy = (float)r.o[1]; oz = (float)r.o[2];
             fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
             cur = sc.root;
-            sp = 0; low = 0;
+            sp = 0; low = 0; clean_from = 0;
             in_prim = false;
             bprim = -1;
             busy = cur != -1;
@@ -379,7 +380,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     if ((m_prim | m_node) == 0) continue;
     const uint32_t n_prim = (uint32_t)__popcll(m_prim), n_node = (uint32_t)__popcll(m_node);
     bool advance = false;   // lane finished its current node / leaf: take next or pop
-    bool leaf_next = false; // the node step went straight into its first child leaf
+    bool leaf_next = false; // the step went straight into a leaf whose re-test is known to pass
     int32_t next = -1;
     if (n_prim * prim_w >= n_node * 16u) {
       // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134)
@@ -398,13 +399,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (is_tri) {
           double t, u, v;
           if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
-            tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v;
+            tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v; clean_from = sp;
           }
         } else {
           const double time = wp.rays[slot].time;  // only spheres read the ray time
           double t; int root;
           if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
-            tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0;
+            tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0; clean_from = sp;
           }
         }
         pk++;
@@ -420,12 +421,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       if (busy && !in_prim) {
         const float tm = (float)tmax;
         if (ref_is_leaf(cur)) {
-          const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_id(cur));
+          const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_start(cur));
           const float4 a = lp[0], b = lp[1];  // both loads issued together
-          const int32_t start = __float_as_int(b.z), count = __float_as_int(b.w);
-          const bool hit = slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm);
-          if (hit & (count > 0)) {
-            in_prim = true; pk = start; pend = start + count;
+          if (slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
+            in_prim = true; pk = leaf_start(cur); pend = pk + leaf_count(cur);
           } else {
             advance = true;
           }
@@ -433,7 +432,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
           const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
           const int4 ch = *reinterpret_cast<const int4*>(np + 6);
-          const int4 lf = *reinterpret_cast<const int4*>(np + 7);  // leaf-child shortcuts (GInner::leaf)
           uint32_t hm;
           if (wave_fast) {
             hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
@@ -455,9 +453,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           // A leaf visited straight after its parent re-tests the same f32 box with the
           // same tMax (A10): the result is known to be a hit, so skip its node load and
           // start on its primitives (the visit is still counted).
-          const int32_t lfe = f == 0 ? lf.x : (f == 1 ? lf.y : (f == 2 ? lf.z : lf.w));
-          if (m != 0 && lfe != 0) {
-            in_prim = true; pk = lfe >> 3; pend = pk + (lfe & 7);
+          if (ref_is_leaf(next) && sc.leaf_shortcut) {
+            in_prim = true; pk = leaf_start(next); pend = pk + leaf_count(next);
             next = -1;
             leaf_next = true;
           }
@@ -480,7 +477,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           advance = !leaf_next;
         }
       }
-      c_nodes += (uint64_t)__popcll(__ballot(leaf_next));
     }
     if (advance) {
       if (next != -1) {
@@ -489,6 +485,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         sp--;
         if (sp < low) { cur = gsp[(size_t)sp * spill_stride]; low = sp; }
         else cur = stk[(sp & (S - 1)) * 256];
+        // An entry pushed after the last accepted hit meets the same tMax it was pushed
+        // with, so a leaf's re-test against its (identical) box passes: skip the load.
+        if (ref_is_leaf(cur) && sp >= clean_from && sc.leaf_shortcut) {
+          in_prim = true; pk = leaf_start(cur); pend = pk + leaf_count(cur);
+          leaf_next = true;
+        }
+        if (sp < clean_from) clean_from = sp;
       } else {
         HitOut& h = wp.hits[slot];
         h.t = bprim >= 0 ? tmax : 0.0;
@@ -497,6 +500,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         busy = false;
       }
     }
+    c_nodes += (uint64_t)__popcll(__ballot(leaf_next));  // leaf visits taken by a shortcut
   }
   if (lane == 0) {
     if (c_rays) atomicAdd(counters + CNT_RAYS, (unsigned long long)c_rays);
@@ -1623,14 +1627,16 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   const uint32_t nt = d->num_tris, ns = d->num_spheres;
   // ---- BVH4: split reference nodes into inner nodes and leaf records
   std::vector<int32_t> ref(d->num_nodes);
-  uint32_t n_inner = 0, n_leaf = 0;
+  uint32_t n_inner = 0;
   for (uint32_t k = 0; k < d->num_nodes; k++) {
     const izpi_bvh4_node& n = d->nodes[k];
     if (n.prim_count[0] > 0) {
       for (int i = 1; i < 4; i++)
         if (n.child[i] != -1) { ctx->err = "leaf node with more than one slot"; return IZPI_ERR_INVALID; }
-      ref[k] = -(int32_t)n_leaf - 2;
-      n_leaf++;
+      const int32_t st = n.child[0], cnt = n.prim_count[0];
+      if (st < 0 || (uint64_t)st + (uint64_t)cnt > d->num_prims) { ctx->err = "leaf primitive range out of bounds"; return IZPI_ERR_INVALID; }
+      if (cnt > 7 || st >= (1 << 27)) { ctx->err = "leaf too large for the leaf-ref encoding"; return IZPI_ERR_UNSUPPORTED; }
+      ref[k] = make_leaf_ref(st, cnt);
     } else {
       for (int i = 0; i < 4; i++)
         if (n.prim_count[i] != 0) { ctx->err = "inner node with a primitive slot"; return IZPI_ERR_INVALID; }
@@ -1638,15 +1644,15 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     }
   }
   std::vector<GInner> inner(n_inner);
-  std::vector<GLeaf> leaves(n_leaf);
+  std::vector<GLeaf> leaves(std::max<uint32_t>(1, d->num_prims));  // indexed by first primitive
+  uint32_t leaf_shortcut = 1;
   for (uint32_t k = 0; k < d->num_nodes; k++) {
     const izpi_bvh4_node& n = d->nodes[k];
     if (ref[k] <= -2) {
-      GLeaf& L = leaves[(size_t)leaf_id(ref[k])];
+      GLeaf& L = leaves[(size_t)leaf_start(ref[k])];
       L.mn[0] = n.min_x[0]; L.mn[1] = n.min_y[0]; L.mn[2] = n.min_z[0];
       L.mx[0] = n.max_x[0]; L.mx[1] = n.max_y[0]; L.mx[2] = n.max_z[0];
       L.start = n.child[0]; L.count = n.prim_count[0];
-      if ((uint32_t)(L.start + L.count) > d->num_prims) { ctx->err = "leaf primitive range out of bounds"; return IZPI_ERR_INVALID; }
     } else {
       GInner& g = inner[(size_t)ref[k]];
       memcpy(g.mnx, n.min_x, 16); memcpy(g.mny, n.min_y, 16); memcpy(g.mnz, n.min_z, 16);
@@ -1655,17 +1661,14 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
         int32_t c = n.child[i];
         if (c != -1 && (c < 0 || (uint32_t)c >= d->num_nodes)) { ctx->err = "child index out of bounds"; return IZPI_ERR_INVALID; }
         g.child[i] = c == -1 ? -1 : ref[(size_t)c];
-        g.leaf[i] = 0;
+        g.pad[i] = 0;
         if (c >= 0 && ref[(size_t)c] <= -2) {
-          // leaf child: shortcut entry (start << 3 | count) when the leaf's slot-0 box is
-          // bit-identical to this slot's box (so its re-test straight after this visit
-          // is known to pass), else 0
+          // a leaf's re-test (A10) may be skipped only if its slot-0 box is bit-identical
+          // to this slot's box (flattenBVH4 converts the same node.box twice, bvh4.go:745-781)
           const izpi_bvh4_node& lnode = d->nodes[(size_t)c];
           const float pb[6] = {n.min_x[i], n.min_y[i], n.min_z[i], n.max_x[i], n.max_y[i], n.max_z[i]};
           const float lb[6] = {lnode.min_x[0], lnode.min_y[0], lnode.min_z[0], lnode.max_x[0], lnode.max_y[0], lnode.max_z[0]};
-          const int32_t st = lnode.child[0], cnt = lnode.prim_count[0];
-          if (memcmp(pb, lb, sizeof(pb)) == 0 && st >= 0 && st < (1 << 27) && cnt >= 1 && cnt <= 7)
-            g.leaf[i] = (st << 3) | cnt;
+          if (memcmp(pb, lb, sizeof(pb)) != 0) leaf_shortcut = 0;
         }
       }
     }
@@ -1776,6 +1779,8 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   sc.mat_flags = dmf; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
+  sc.leaf_shortcut = leaf_shortcut;
+  if (getenv("IZPI_NO_LEAF_SHORTCUT")) sc.leaf_shortcut = 0;
   sc.nan_free_bounds = 1;
   for (const GInner& g : inner) {
     const float* f = g.mnx;  // the 24 bounds are contiguous
