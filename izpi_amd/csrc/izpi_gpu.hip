@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
 // ring full, the oldest entry is spilled to a per-thread global area (entry e at
 // spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
 // are kept per wave in SGPRs (popcounts of ballots).
-template <int S, int WPE>
+template <int S, int WPE, bool P2>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
@@ -383,8 +383,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     bool leaf_next = false; // the step went straight into a leaf whose re-test is known to pass
     int32_t next = -1;
     if (n_prim * prim_w >= n_node * 16u) {
-      // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134)
-      bool is_tri = false;
+      // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134); with P2, two
+      // consecutive primitives of the leaf per step (their loads and arithmetic overlap;
+      // the second test still sees the tMax the first may have shrunk, as in the loop)
+      bool is_tri = false, second = false, is_tri2 = false;
       if (busy && in_prim) {
         // the f64 ray is re-read here (L2) instead of living in 14 VGPRs across node steps
         const double2* rp = reinterpret_cast<const double2*>(wp.rays + slot);
@@ -393,27 +395,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const double tmin = r3.x;
         const double2* pp = reinterpret_cast<const double2*>(sc.prims + pk);
         const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
-        const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
-        const uint32_t kind = (uint32_t)__double2loint(p4.y);
-        is_tri = kind == IZPI_PRIM_TRIANGLE;
-        if (is_tri) {
-          double t, u, v;
-          if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
-            tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v; clean_from = sp;
+        second = P2 && pk + 1 < pend;
+        double2 s0 = p0, s1 = p1, s2 = p2, s3 = p3, s4 = p4;
+        if (second) { s0 = pp[5]; s1 = pp[6]; s2 = pp[7]; s3 = pp[8]; s4 = pp[9]; }
+#pragma unroll
+        for (int j = 0; j < (P2 ? 2 : 1); j++) {
+          if (j == 1 && !second) break;
+          const double2 a0 = j ? s0 : p0, a1 = j ? s1 : p1, a2 = j ? s2 : p2, a3 = j ? s3 : p3, a4 = j ? s4 : p4;
+          const double pa[9] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, a4.x};
+          const bool tri = (uint32_t)__double2loint(a4.y) == IZPI_PRIM_TRIANGLE;
+          if (j == 0) is_tri = tri; else is_tri2 = tri;
+          if (tri) {
+            double t, u, v;
+            if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
+              tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v; clean_from = sp;
+            }
+          } else {
+            const double time = wp.rays[slot].time;  // only spheres read the ray time
+            double t; int root;
+            if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
+              tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0; clean_from = sp;
+            }
           }
-        } else {
-          const double time = wp.rays[slot].time;  // only spheres read the ray time
-          double t; int root;
-          if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
-            tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0; clean_from = sp;
-          }
+          pk++;
         }
-        pk++;
         if (pk == pend) { in_prim = false; advance = true; }
       }
-      const uint32_t n_tri = (uint32_t)__popcll(__ballot(is_tri));
+      const uint32_t n_tri = (uint32_t)__popcll(__ballot(is_tri)) + (uint32_t)__popcll(__ballot(is_tri2));
+      const uint32_t n_tests = n_prim + (uint32_t)__popcll(__ballot(second));
       c_tri += n_tri;
-      c_sph += n_prim - n_tri;
+      c_sph += n_tests - n_tri;
     } else {
       c_nodes += n_node;
       const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
@@ -1322,18 +1333,21 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 // All variants give identical results and counters.
 struct Tracer {
   int variant = 2, stack = 32, ring = 16, wpe = 5;
+  bool p2 = false;
   uint32_t prim_w = 16, tchunk = 128, refill_min = 32;
   int blocks = 0;
 };
 
 // k_trace2 instances: ring entries x minimum waves per SIMD (register budget).
-#define IZPI_T2_LIST(X) X(8, 4) X(8, 6) X(8, 8) X(16, 4) X(16, 5) X(16, 6) X(16, 8) X(32, 4)
+#define IZPI_T2_LIST(X) X(8, 4, false) X(8, 8, false) X(16, 4, false) X(16, 5, false) X(16, 6, false) X(16, 8, false) \
+  X(32, 4, false) X(16, 4, true) X(16, 5, true)
 
 int make_tracer(izpi_ctx* ctx, Tracer* t) {
   *t = Tracer();
   if (const char* e = getenv("IZPI_TRACE")) t->variant = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("IZPI_TRACE_RING")) t->ring = atoi(e);
   if (const char* e = getenv("IZPI_TRACE_WPE")) t->wpe = atoi(e);
+  if (const char* e = getenv("IZPI_TRACE_P2")) t->p2 = atoi(e) != 0;
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
@@ -1343,7 +1357,7 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
     rc = t->stack == 32 ? resident_blocks(ctx, k_trace<32>, &t->blocks) : resident_blocks(ctx, k_trace<64>, &t->blocks);
     return rc;
   }
-#define IZPI_T2_OCC(R, W) if (t->ring == R && t->wpe == W) rc = resident_blocks(ctx, k_trace2<R, W>, &t->blocks);
+#define IZPI_T2_OCC(R, W, P) if (t->ring == R && t->wpe == W && t->p2 == P) rc = resident_blocks(ctx, k_trace2<R, W, P>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
 #undef IZPI_T2_OCC
   if (rc == IZPI_ERR_INVALID) { ctx->err = "no k_trace2 instance for IZPI_TRACE_RING/IZPI_TRACE_WPE"; return rc; }
@@ -1359,9 +1373,9 @@ void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStrea
     return;
   }
   const uint32_t stride = (uint32_t)t.blocks * 256;
-#define IZPI_T2_LAUNCH(R, W)                                                                                  \
-  if (t.ring == R && t.wpe == W) {                                                                           \
-    hipLaunchKernelGGL((k_trace2<R, W>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
+#define IZPI_T2_LAUNCH(R, W, P)                                                                               \
+  if (t.ring == R && t.wpe == W && t.p2 == P) {                                                              \
+    hipLaunchKernelGGL((k_trace2<R, W, P>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
                        stride, t.prim_w, t.tchunk, t.refill_min);                                            \
     return;                                                                                                  \
   }
