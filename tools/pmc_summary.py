@@ -17,6 +17,7 @@ HBM bytes.
 """
 import collections
 import csv
+import re
 import json
 import shutil
 import sys
@@ -53,7 +54,7 @@ def main():
         per[k] = {"launches": launches, "fetch_bytes_per_launch": fb / launches,
                   "write_bytes_per_launch": wb / launches, "bytes_per_launch": (fb + wb) / launches}
     (dst / "pmc_traffic.json").write_text(json.dumps(per, indent=1))
-    trace = [v for k, v in per.items() if "k_trace<" in k]
+    trace = [v for k, v in per.items() if re.search(r"\bk_trace2?<", k)]
     if trace:
         t = trace[0]
         summ_f = ROOT / "profiles" / "pmc_summary.json"
