@@ -389,6 +389,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       bool is_tri = false, second = false, is_tri2 = false;
       if (busy && in_prim) {
         // the f64 ray is re-read here (L2) instead of living in 14 VGPRs across node steps
+        // (measured: keeping it in LDS instead makes k_shade's later read of the same
+        // record miss and costs more than it saves)
         const double2* rp = reinterpret_cast<const double2*>(wp.rays + slot);
         const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
         const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
@@ -1339,8 +1341,7 @@ struct Tracer {
 };
 
 // k_trace2 instances: ring entries x minimum waves per SIMD (register budget).
-#define IZPI_T2_LIST(X) X(8, 4, false) X(8, 8, false) X(16, 4, false) X(16, 5, false) X(16, 6, false) X(16, 8, false) \
-  X(32, 4, false) X(16, 4, true) X(16, 5, true)
+#define IZPI_T2_LIST(X) X(8, 4, false) X(8, 5, false) X(16, 4, false) X(16, 5, false) X(32, 4, false) X(16, 4, true)
 
 int make_tracer(izpi_ctx* ctx, Tracer* t) {
   *t = Tracer();
