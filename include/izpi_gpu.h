@@ -90,7 +90,15 @@ typedef struct izpi_render_req {
   const double* bg_spd_values;
   double background[3];       /* Colour background (leader.go:140: black) */
   uint64_t seed;              /* master seed of the per-sample LCG streams */
+  uint32_t post;              /* IZPI_POST_*: post-processing of a whole-frame IZPI_OUT_CANVAS render */
+  uint32_t pad_post;
+  double exposure;            /* XYZToRGB exposure (Scene.Exposure = camera exposure) */
 } izpi_render_req;
+
+/* Post-processing applied by Render for the Spectral sampler (renderer.go:215-219):
+ * spectral.FireflyRejection (firefly_rejection.go:12-113) then spectral.XYZToRGB
+ * (rgb_image.go:28-67, ACEScg matrix :13-17) with req->exposure. */
+enum { IZPI_POST_NONE = 0, IZPI_POST_SPECTRAL = 1 };
 
 /* Per-render counters. The traversal is bit-identical to the CPU restatement, so
  * these equal the oracle's counts exactly (used for algorithmic bytes, §8(d)). */
@@ -139,6 +147,12 @@ int izpi_gpu_render_device(izpi_ctx* ctx, const izpi_render_req* req, double* ou
 /* Scatter packed tiles (IZPI_OUT_PACKED, device memory) into a W*H*4 canvas
  * (device memory) applying the row = H - y rule of rgb.go:41 / spectral.go:36. */
 int izpi_gpu_unpack_tiles(izpi_ctx* ctx, const izpi_render_req* req, const double* packed_dev, double* canvas_dev);
+
+/* FireflyRejection + XYZToRGB of a W*H*4 float64 CIE-XYZ canvas (device memory) into
+ * `rgba_dev` (device memory, may not alias `xyz_dev`): the multi-GPU path runs it on
+ * rank 0 after the gather. */
+int izpi_gpu_spectral_post(izpi_ctx* ctx, const double* xyz_dev, double* rgba_dev, uint32_t width, uint32_t height,
+                           double exposure);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);

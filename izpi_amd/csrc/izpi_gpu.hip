@@ -1170,6 +1170,63 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
   }
 }
 
+// FireflyRejection (firefly_rejection.go:12-113) fused with XYZToRGB (rgb_image.go:28-67).
+// FireflyRejection reads only the ORIGINAL Y plane (it copies it first, :33-39) and
+// scales the pixel's own X, Y, Z, so pixels are independent: one thread per pixel, the
+// 18x18 Y halo of a 16x16 tile staged in LDS. The scaled XYZ then goes through the
+// exposure multiply and the ACEScg matrix in XYZToRGB's operation order.
+__global__ void __launch_bounds__(256) k_spectral_post(const double* in, double* out, uint32_t W, uint32_t H,
+                                                       double exposure) {
+  __shared__ double ys[18][18];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int x0 = blockIdx.x * 16, y0 = blockIdx.y * 16;
+  for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+    const int hx = x0 + (i % 18) - 1, hy = y0 + (i / 18) - 1;
+    ys[i / 18][i % 18] = (hx >= 0 && hx < (int)W && hy >= 0 && hy < (int)H) ? in[((size_t)hy * W + hx) * 4 + 1] : 0.0;
+  }
+  __syncthreads();
+  const int x = x0 + tx, y = y0 + ty;
+  if (x >= (int)W || y >= (int)H) return;
+  const size_t pi = ((size_t)y * W + x) * 4;
+  const double2 xy = *reinterpret_cast<const double2*>(in + pi), za = *reinterpret_cast<const double2*>(in + pi + 2);
+  double X = xy.x, Y = xy.y, Z = za.x;
+  const double cur = ys[ty + 1][tx + 1];
+  if (cur > 0) {  // `currentY <= 0` skips (NaN does not)
+    double nb[8];
+    int nn = 0;
+    for (int dy = -1; dy <= 1; dy++)
+      for (int dx = -1; dx <= 1; dx++) {
+        if (dx == 0 && dy == 0) continue;
+        const int nx = x + dx, ny = y + dy;
+        if (nx >= 0 && nx < (int)W && ny >= 0 && ny < (int)H) {
+          const double v = ys[ty + 1 + dy][tx + 1 + dx];
+          if (v > 0) nb[nn++] = v;
+        }
+      }
+    if (nn >= 3) {
+      double sum = 0.0;
+      for (int i = 0; i < nn; i++) sum += nb[i];
+      const double mean = sum / (double)nn;
+      double vs = 0.0;
+      for (int i = 0; i < nn; i++) { const double d = nb[i] - mean; vs += d * d; }
+      const double stddev = gm::sqrt(vs / (double)nn);
+      const double threshold = mean + 2.5 * stddev;
+      if (cur > threshold && threshold > 0) {
+        const double ratio = threshold / cur;
+        X *= ratio; Y *= ratio; Z *= ratio;
+      }
+    }
+  }
+  X *= exposure; Y *= exposure; Z *= exposure;
+  double2 rg, ba;
+  rg.x = 1.6410234 * X + -0.3248033 * Y + -0.2364247 * Z;
+  rg.y = -0.6636629 * X + 1.6153316 * Y + 0.0167563 * Z;
+  ba.x = 0.0117219 * X + -0.0082845 * Y + 0.9883949 * Z;
+  ba.y = za.y;  // alpha unchanged
+  *reinterpret_cast<double2*>(out + pi) = rg;
+  *reinterpret_cast<double2*>(out + pi + 2) = ba;
+}
+
 __global__ void k_unpack(const uint32_t* tiles, uint32_t num_pixels, uint32_t tile_w, uint32_t tile_h, uint32_t width,
                          uint32_t height, const double* packed, double* canvas) {
   const uint32_t p = blockIdx.x * 256 + threadIdx.x;
@@ -1278,6 +1335,7 @@ struct izpi_ctx {
   PathSt* d_paths = nullptr; size_t paths_cap = 0;
   uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
+  double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
   uint32_t* h_count = nullptr;                        // pinned readback of the queue length
   hipEvent_t ev3 = nullptr;
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
@@ -1469,6 +1527,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (!ctx->have_scene) { ctx->err = "render before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
   if (req->sampler != IZPI_SAMPLER_COLOUR && req->sampler != IZPI_SAMPLER_SPECTRAL) { ctx->err = "unsupported sampler"; return IZPI_ERR_UNSUPPORTED; }
+  if (req->post != IZPI_POST_NONE &&
+      (req->post != IZPI_POST_SPECTRAL || req->out_layout != IZPI_OUT_CANVAS || req->num_tiles != 0)) {
+    ctx->err = "post-processing needs a whole-frame IZPI_OUT_CANVAS request";
+    return IZPI_ERR_INVALID;
+  }
   if (req->sampler == IZPI_SAMPLER_COLOUR ? !ctx->mat_ok_rgb : !ctx->mat_ok_spectral) {
     ctx->err = "a material lacks the textures this sampler reads";
     return IZPI_ERR_INVALID;
@@ -1559,6 +1622,14 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
 #undef IZPI_RUN
   if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, st));
+  if (req->post == IZPI_POST_SPECTRAL) {  // renderer.go:215-219, outside the timed render like the reference
+    if ((rc = grow(ctx, (void**)&ctx->d_post, &ctx->post_cap, (size_t)req->width * req->height * 4 * sizeof(double)))) return rc;
+    dim3 g((req->width + 15) / 16, (req->height + 15) / 16);
+    hipLaunchKernelGGL(k_spectral_post, g, dim3(256), 0, st, out_dev, ctx->d_post, req->width, req->height, req->exposure);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out_dev, ctx->d_post, (size_t)req->width * req->height * 4 * sizeof(double),
+                           hipMemcpyDeviceToDevice, st));
+  }
   HIP_TRY(hipEventSynchronize(ctx->ev1));
   float total_ms = 0;
   HIP_TRY(hipEventElapsedTime(&total_ms, ctx->ev0, ctx->ev1));
@@ -1618,7 +1689,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   free_scene(ctx);
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
-                  ctx->d_counters, ctx->d_rays, ctx->d_hits, ctx->d_paths, ctx->d_queue, ctx->d_spill};
+                  ctx->d_counters, ctx->d_rays, ctx->d_hits, ctx->d_paths, ctx->d_queue, ctx->d_spill, ctx->d_post};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
@@ -1859,6 +1930,21 @@ int izpi_gpu_render(izpi_ctx* ctx, const izpi_render_req* req, double* out_host,
   if (stats) *stats = ctx->last;
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out_host, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return IZPI_OK;
+}
+
+int izpi_gpu_spectral_post(izpi_ctx* ctx, const double* xyz_dev, double* rgba_dev, uint32_t width, uint32_t height,
+                           double exposure) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  if (!xyz_dev || !rgba_dev || xyz_dev == rgba_dev || width == 0 || height == 0) {
+    ctx->err = "spectral_post: bad arguments (buffers must be distinct device canvases)";
+    return IZPI_ERR_INVALID;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  dim3 g((width + 15) / 16, (height + 15) / 16);
+  hipLaunchKernelGGL(k_spectral_post, g, dim3(256), 0, ctx->stream, xyz_dev, rgba_dev, width, height, exposure);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return IZPI_OK;
 }

@@ -4,7 +4,7 @@
 and ``.render()`` mirrors ``Render(ctx) image.Image`` (renderer.go:108-222): it returns the
 float64 NRGBA canvas (H, W, 4) the Go renderer fills — RGB for the Colour sampler, CIE XYZ
 before post-processing for the Spectral sampler (``.render_spectral_rgb()`` applies
-FireflyRejection + XYZToRGB like renderer.go:216-219).
+FireflyRejection + XYZToRGB on the GPU like renderer.go:216-219).
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL): tiles are dealt
 round-robin (tile_id % world == rank), each rank renders its tiles into a packed
@@ -62,8 +62,10 @@ class GPURenderer:
         self.stats = None
 
     # -------------------------------------------------------------- request
-    def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None):
+    def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None, post=N.POST_NONE):
         req = N.RenderReq()
+        req.post = post
+        req.exposure = self.exposure
         req.width, req.height = self.width, self.height
         req.spp = self.spp if spp is None else int(spp)
         req.max_depth = self.max_depth
@@ -85,16 +87,33 @@ class GPURenderer:
         return req
 
     # --------------------------------------------------------------- render
-    def render(self, tiles=None, canvas=None, spp=None):
-        """Render.Render(): returns the (H, W, 4) float64 canvas (host memory)."""
+    @property
+    def exposure(self):
+        return float(self.host.desc.camera.exposure)  # Scene.Exposure = camera exposure (scene.go:30)
+
+    def render(self, tiles=None, canvas=None, spp=None, post=N.POST_NONE):
+        """Render.Render(): returns the (H, W, 4) float64 canvas (host memory). With
+        post=POST_SPECTRAL (whole frame only) the XYZ canvas goes through
+        FireflyRejection + XYZToRGB on the GPU, as Render does for the Spectral sampler."""
         if canvas is None:
             canvas = np.zeros((self.height, self.width, 4), np.float64)
-        req = self.request(tiles, N.OUT_CANVAS, spp)
+        req = self.request(tiles, N.OUT_CANVAS, spp, post)
         st = N.RenderStats()
         rc = N.lib().izpi_gpu_render(self.ctx, C.byref(req), canvas.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st))
         _check(rc, self.ctx, "izpi_gpu_render")
         self.stats = st.as_dict()
         return canvas
+
+    def render_spectral_rgb(self):
+        """The full reference Render() for the Spectral sampler: XYZ render, then
+        FireflyRejection + XYZToRGB (renderer.go:215-219), all on the GPU."""
+        return self.render(post=N.POST_SPECTRAL)
+
+    def spectral_post(self, xyz_ptr, rgba_ptr):
+        """FireflyRejection + XYZToRGB of a device XYZ canvas into another device canvas."""
+        _check(N.lib().izpi_gpu_spectral_post(self.ctx, C.c_void_p(xyz_ptr), C.c_void_p(rgba_ptr), self.width,
+                                              self.height, C.c_double(self.exposure)), self.ctx,
+               "izpi_gpu_spectral_post")
 
     def render_device(self, out_ptr, tiles=None, layout=N.OUT_CANVAS, spp=None):
         """Render into device memory at `out_ptr` (e.g. torch tensor .data_ptr())."""
@@ -115,9 +134,10 @@ class GPURenderer:
                self.ctx, "izpi_gpu_unpack_tiles")
 
     # ------------------------------------------------------------ multi-GPU
-    def render_distributed(self, rank, world, group=None, tiles=None):
+    def render_distributed(self, rank, world, group=None, tiles=None, post=N.POST_NONE):
         """Tile-sharded render over `world` ranks; returns the canvas as a torch tensor
-        on rank 0 (None elsewhere) and this rank's stats. One RCCL gather."""
+        on rank 0 (None elsewhere) and this rank's stats. One RCCL gather. With
+        post=POST_SPECTRAL rank 0 applies FireflyRejection + XYZToRGB after the gather."""
         import torch
         from . import sharding
         all_tiles = common_tiles(self.width, self.height) if tiles is None else np.asarray(tiles, np.uint32)
@@ -136,6 +156,10 @@ class GPURenderer:
             rt = sharding.shard_tiles(all_tiles, r, world)
             if len(rt):
                 self.unpack(rt, gathered[r].data_ptr(), canvas.data_ptr())
+        if post == N.POST_SPECTRAL:
+            rgb = torch.empty_like(canvas)
+            self.spectral_post(canvas.data_ptr(), rgb.data_ptr())
+            canvas = rgb
         torch.cuda.synchronize(dev)
         return canvas, self.stats
 

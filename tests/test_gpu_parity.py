@@ -281,3 +281,39 @@ def test_full_size_c3_tiles_full_spp_bitwise(gpu):
     ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, cfg.spp, N.SAMPLER_COLOUR, tiles=tiles)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
+
+
+def test_spectral_post_kernel_bitwise(gpu):
+    """FireflyRejection + XYZToRGB (firefly_rejection.go, rgb_image.go) on a synthetic XYZ
+    canvas with fireflies, zeros, negative and NaN luminance, edges and corners."""
+    import torch
+    W, H = 67, 45
+    rng = np.random.default_rng(3)
+    xyz = rng.uniform(0.0, 1.0, (H, W, 4))
+    spikes = rng.random((H, W)) < 0.05
+    xyz[spikes, :3] *= 50.0
+    xyz[rng.random((H, W)) < 0.05, 1] = 0.0
+    xyz[rng.random((H, W)) < 0.02, 1] = -0.3
+    xyz[5, 7, 1] = np.nan
+    xyz[0, :, :] = 0.0  # the row the reference never writes (A9)
+    r = GPURenderer(configs.cornell_rgb(), W, H, 1)
+    for exposure in (1.0, 0.7):
+        want = O.xyz_to_rgb(O.firefly(xyz.reshape(-1), W, H), W, H, exposure).reshape(H, W, 4)
+        src = torch.from_numpy(xyz.copy()).cuda()
+        dst = torch.empty_like(src)
+        assert N.lib().izpi_gpu_spectral_post(r.ctx, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), W, H,
+                                              C.c_double(exposure)) == 0
+        got = dst.cpu().numpy()
+        assert got.tobytes() == want.tobytes()
+    r.close()
+
+
+def test_render_spectral_rgb_bitwise(gpu):
+    """Render() for the Spectral sampler: XYZ render + FireflyRejection + XYZToRGB."""
+    scene = configs.cornell_glass_spectral()
+    r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL)
+    img = r.render_spectral_rgb()
+    ref, _ = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_SPECTRAL)
+    want = O.xyz_to_rgb(O.firefly(ref.reshape(-1), 48, 48), 48, 48, r.exposure).reshape(48, 48, 4)
+    assert_parity(img, want)
+    r.close()
