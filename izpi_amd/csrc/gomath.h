@@ -96,18 +96,29 @@ IZPI_HD double ldexp(double frac, int ex) {
 }
 
 // modf.go (generic): integer and fractional parts with the sign of f.
-IZPI_HD double modf(double f, double* frac) {
-  if (f < 1) {
-    if (f < 0) { double fr; double ip = modf(-f, &fr); *frac = -fr; return -ip; }
-    if (f == 0) { *frac = f; return f; }
-    *frac = f; return 0;
-  }
+// (Go's `case f < 0: int, frac = Modf(-f); return -int, -frac` is written out without
+// recursion: a recursive call on the GPU forces a call stack and the full register file.)
+IZPI_HD double modf_ge1(double f, double* frac) {  // f >= 1, +Inf or NaN
   uint64_t x = bits(f);
   uint64_t e = ((x >> 52) & 0x7FF) - 1023;
   if (e < 64 - 12) x &= ~((1ull << (64 - 12 - e)) - 1);
   double ip = from_bits(x);
   *frac = f - ip;
   return ip;
+}
+IZPI_HD double modf(double f, double* frac) {
+  if (f < 1) {
+    if (f < 0) {
+      const double g = -f;  // > 0
+      double fr, ip;
+      if (g < 1) { fr = g; ip = 0; } else { ip = modf_ge1(g, &fr); }
+      *frac = -fr;
+      return -ip;
+    }
+    if (f == 0) { *frac = f; return f; }
+    *frac = f; return 0;
+  }
+  return modf_ge1(f, frac);
 }
 
 IZPI_HD bool is_odd_int(double x) {
@@ -230,19 +241,25 @@ IZPI_HD double log(double x) {
 }
 
 // pow.go
+// Pow(±0, y) for y != 0 and not NaN (pow.go "case x == 0").
+IZPI_HD double pow_zero(double x, double y) {
+  if (y < 0) return (signbit(x) && is_odd_int(y)) ? inf(-1) : inf(1);
+  return (signbit(x) && is_odd_int(y)) ? x : 0;
+}
 IZPI_HD double pow(double x, double y) {
   if (y == 0 || x == 1) return 1;
   if (y == 1) return x;
   if (is_nan(x) || is_nan(y)) return nan();
   if (x == 0) {
-    if (y < 0) return (signbit(x) && is_odd_int(y)) ? inf(-1) : inf(1);
-    if (y > 0) return (signbit(x) && is_odd_int(y)) ? x : 0;
+    return pow_zero(x, y);
   } else if (is_inf(y, 0)) {
     if (x == -1) return 1;
     if ((abs(x) < 1) == is_inf(y, 1)) return 0;
     return inf(1);
   } else if (is_inf(x, 0)) {
-    if (is_inf(x, -1)) return pow(1 / x, -y);
+    // Go: `return Pow(1/x, -y)`, i.e. Pow(-0, -y) (written out: no recursion on the GPU,
+    // where a recursive call forces a call stack and the full register file)
+    if (is_inf(x, -1)) return pow_zero(1 / x, -y);
     if (y < 0) return 0;
     if (y > 0) return inf(1);
   } else if (y == 0.5) {

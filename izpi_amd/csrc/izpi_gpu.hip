@@ -107,6 +107,7 @@ IZPI_DEV double spd_value(const double* wl, const double* vl, uint32_t n, double
 IZPI_DEV void sample_wavelength(double random, double& lambda, double& pdf) {
   double target = random * IZPI_CIE_Y_INTEGRAL;
   double current = 0.0;
+#pragma unroll 1
   for (int i = 0; i < IZPI_CIE_N; i++) {
     double y = c_cie_y[i];
     if (current + y >= target) {
@@ -132,6 +133,7 @@ IZPI_DEV void cie_values(double w, double& x, double& y, double& z) {
   if (w <= c_cie_wl[0]) { x = c_cie_x[0]; y = c_cie_y[0]; z = c_cie_z[0]; return; }
   if (w >= c_cie_wl[IZPI_CIE_N - 1]) { x = c_cie_x[IZPI_CIE_N - 1]; y = c_cie_y[IZPI_CIE_N - 1]; z = c_cie_z[IZPI_CIE_N - 1]; return; }
   int index = 0;
+#pragma unroll 1
   for (int i = 0; i < IZPI_CIE_N; i++) if (c_cie_wl[i] >= w) { index = i; break; }
   double w1 = c_cie_wl[index - 1], w2 = c_cie_wl[index];
   double t = (w - w1) / (w2 - w1);
@@ -902,8 +904,12 @@ enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
 #ifndef IZPI_SHADE_WPE
 #define IZPI_SHADE_WPE 3  // MATSET_BASIC register budget: 3 waves/SIMD (no spill; 4 spills ~150 B/lane)
 #endif
+#ifndef IZPI_SHADE_WPE_OTHER
+#define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
+#endif
 template <int SAMPLER, int MATSET>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET == MATSET_BASIC && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE : 1)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET == MATSET_BASIC && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
+                                                                                              : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const uint32_t n = *wp.q_in_count;

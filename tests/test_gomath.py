@@ -46,7 +46,11 @@ def inputs(op, n=4000, seed=1):
         x = np.concatenate([rng.uniform(0, 1, n // 2), rng.uniform(-3, 3, n // 2)])
         y = np.concatenate([np.full(n // 4, 5.0), np.full(n // 4, 2.0), rng.uniform(-3, 3, n // 2)])
         x = np.where(y != np.round(y), np.abs(x), x)
-        return x, y
+        # Go's special cases (pow.go): +-0, +-Inf, NaN, negative bases with integer exponents
+        sx = [float("-inf"), float("inf"), -0.0, 0.0, -2.0, -0.5, 0.5, 1.0, -1.0, float("nan")]
+        sy = [-3.0, -2.0, 2.0, 3.0, 0.5, -0.5, 2.5, float("inf"), float("-inf"), float("nan"), 1.0, 0.0]
+        gx, gy = np.meshgrid(sx, sy)
+        return np.concatenate([x, gx.ravel()]), np.concatenate([y, gy.ravel()])
     if op == "atan2":
         return rng.uniform(-1, 1, n), rng.uniform(-1, 1, n)
     if op in ("asin",):
@@ -84,6 +88,8 @@ def test_accuracy_against_libm(op):
     x, y = inputs(op, n=2000, seed=7)
     worst = 0
     for a, b in zip(x, y):
+        if not (math.isfinite(a) and math.isfinite(b)) or (op == "pow" and (a == 0.0 or (a < 0 and b != round(b)))):
+            continue  # special cases: checked against Go's table in test_pow_special_cases
         o = O.gomath(OPS[op], float(a), float(b))
         r = REF[op](float(a), float(b)) if op in ("pow", "atan2", "div") else REF[op](float(a))
         worst = max(worst, ulp_diff(o, r))
@@ -99,3 +105,21 @@ def test_special_values():
     assert O.gomath(OPS["atan2"], 0.0, -1.0) == math.pi
     # Payne-Hanek range (|x| >= 2^29) is outside the restatement: NaN by design
     assert math.isnan(O.gomath(OPS["sin"], 2.0 ** 30))
+
+
+def test_pow_special_cases():
+    """pow.go's special-case table (the branches the GPU build writes out without recursion)."""
+    inf, nan = float("inf"), float("nan")
+    P = lambda x, y: O.gomath(OPS["pow"], x, y)
+    H = lambda x, y: N.lib().izpi_host_gomath(OPS["pow"], x, y)
+    cases = [((-inf, -3.0), -0.0), ((-inf, -2.0), 0.0), ((-inf, 3.0), -inf), ((-inf, 2.0), inf),
+             ((-inf, 0.5), inf), ((-inf, -0.5), 0.0), ((-0.0, -3.0), -inf), ((-0.0, -2.0), inf), ((0.0, -1.0), inf),
+             ((-0.0, 3.0), -0.0), ((-0.0, 2.0), 0.0), ((inf, -1.0), 0.0), ((inf, 2.0), inf), ((-1.0, inf), 1.0),
+             ((0.5, inf), 0.0), ((2.0, -inf), 0.0), ((-2.0, 3.0), -8.0), ((-8.0, 1.0 / 3.0), nan), ((nan, 0.0), 1.0)]
+    for (x, y), want in cases:
+        for f in (P, H):
+            got = f(x, y)
+            if math.isnan(want):
+                assert math.isnan(got), (x, y, got)
+            else:
+                assert got == want and math.copysign(1, got) == math.copysign(1, want), (x, y, got, want)
