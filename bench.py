@@ -127,7 +127,8 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     agg = {k: 0.0 for k in ("node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests", "rays",
-                            "kernel_ms", "shade_ms", "total_ms", "launches", "samples")}
+                            "kernel_ms", "shade_ms", "total_ms", "launches", "samples", "node_steps", "prim_steps",
+                            "leaf_shortcuts")}
     for _ in range(args.steps):
         canvas, st = step()
         for k in agg:
@@ -186,6 +187,11 @@ def main():
             "rank0_render_ms_per_step": agg["total_ms"] / args.steps,
             "rank0_rays_per_step": agg["rays"] / args.steps,
             "rank0_node_visits_per_ray": agg["node_visits"] / max(agg["rays"], 1),
+            "rank0_tri_tests_per_ray": agg["tri_tests"] / max(agg["rays"], 1),
+            # k_trace2 SIMD efficiency: useful lane-steps / (64 x wave-level steps)
+            "rank0_node_step_lane_util": (agg["node_visits"] - agg["leaf_shortcuts"]) / max(64 * agg["node_steps"], 1),
+            "rank0_prim_step_lane_util": (agg["tri_tests"] + agg["sph_tests"]) / max(64 * agg["prim_steps"], 1),
+            "rank0_leaf_shortcut_frac": agg["leaf_shortcuts"] / max(agg["node_visits"], 1),
             "setup_s": round(setup_s, 2),
             "bvh_build_ms": r.host.build_ms,
             "image_mean_rgb": [float(x) for x in img[1:, :, :3].mean(axis=(0, 1))] if img is not None else None,

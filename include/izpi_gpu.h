@@ -115,6 +115,10 @@ typedef struct izpi_render_stats {
   double total_ms;        /* device time of the whole render call (kernels + accumulation) */
   uint32_t launches;      /* k_trace launches (wavefront iterations) in the call */
   uint32_t pad;
+  /* traversal-kernel work breakdown (diagnostics, not reference quantities): wave-level
+   * loop iterations that ran a node step / a primitive step, and leaf visits taken by a
+   * shortcut (no node load). */
+  uint64_t node_steps, prim_steps, leaf_shortcuts;
 } izpi_render_stats;
 
 /* Hit record returned by izpi_gpu_trace: BVH4.Hit (bvh4.go:49-164) followed by

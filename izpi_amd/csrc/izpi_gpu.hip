@@ -48,7 +48,7 @@ __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
 
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
 
-enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_N };
+enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT, CNT_N };
 
 
 // ======================================================= textures / spectra
@@ -323,6 +323,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = *wp.q_in_count;
   uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
+  uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
   bool busy = false, in_prim = false;
   bool exhausted = false;
   uint32_t slot = 0;
@@ -429,10 +430,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint32_t n_tests = n_prim + (uint32_t)__popcll(__ballot(second));
       c_tri += n_tri;
       c_sph += n_tests - n_tri;
+      c_pstep++;
     } else {
       c_nodes += n_node;
-      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
+      c_nstep++;
       // ---- node step: visit `cur` (bvh4.go:87-146)
+      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
       if (busy && !in_prim) {
         const float tm = (float)tmax;
         if (ref_is_leaf(cur)) {
@@ -515,13 +518,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         busy = false;
       }
     }
-    c_nodes += (uint64_t)__popcll(__ballot(leaf_next));  // leaf visits taken by a shortcut
+    const uint64_t n_short = (uint64_t)__popcll(__ballot(leaf_next));  // leaf visits taken by a shortcut
+    c_nodes += n_short;
+    c_short += n_short;
   }
   if (lane == 0) {
     if (c_rays) atomicAdd(counters + CNT_RAYS, (unsigned long long)c_rays);
     if (c_nodes) atomicAdd(counters + CNT_NODES, (unsigned long long)c_nodes);
     if (c_tri) atomicAdd(counters + CNT_TRI, (unsigned long long)c_tri);
     if (c_sph) atomicAdd(counters + CNT_SPH, (unsigned long long)c_sph);
+    atomicAdd(counters + CNT_NSTEP, (unsigned long long)c_nstep);
+    atomicAdd(counters + CNT_PSTEP, (unsigned long long)c_pstep);
+    atomicAdd(counters + CNT_SHORT, (unsigned long long)c_short);
   }
 }
 
@@ -1649,6 +1657,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.light_tri_tests = cnt[CNT_LTRI]; s.light_sph_tests = cnt[CNT_LSPH];
   s.samples = (uint64_t)num_pixels * req->spp;
   s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches;
+  s.node_steps = cnt[CNT_NSTEP]; s.prim_steps = cnt[CNT_PSTEP]; s.leaf_shortcuts = cnt[CNT_SHORT];
   if (misc[1]) {
     ctx->err = misc[1] & 1u ? "device guard: traversal stack overflow" : "device guard: unknown material kind";
     return IZPI_ERR_DEVICE;
