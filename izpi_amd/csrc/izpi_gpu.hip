@@ -171,6 +171,8 @@ struct WaveParams {
   uint32_t* q_out;            // slots whose next ray must be traced
   uint32_t* q_out_count;
   uint32_t* trace_next;       // dynamic-fetch cursor of k_trace
+  uint32_t* free_q;           // slots whose sample finished this pass (k_shade -> k_refill)
+  uint32_t* free_count;
   uint32_t slots;
 };
 
@@ -889,6 +891,50 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
   queue_push(wp, push, slot);
 }
 
+#ifndef IZPI_SPLIT_REFILL
+#define IZPI_SPLIT_REFILL 0  // 1: refill in its own kernel (k_refill; k_shade -35 VGPRs, but measured 2x slower shading)
+#endif
+// Give `slot` (when `want`) new work units until one yields a ray to trace (block-uniform
+// loop, block-wide unit reservations). Sets `push` when the slot has a ray.
+template <int SAMPLER>
+IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, bool want,
+                           bool& push) {
+  while (__syncthreads_or(want)) {
+    const uint32_t u = block_reserve(sp.head, want);
+    const uint32_t unit = u < sp.total_units ? u : 0xFFFFFFFFu;
+    if (want) {
+      if (unit == 0xFFFFFFFFu) {
+        want = false;
+      } else {
+        PathSt P;
+        RayRec R;
+        if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
+          wp.paths[slot] = P;
+          wp.rays[slot] = R;
+          want = false;
+          push = true;
+        }
+      }
+    }
+  }
+}
+
+// Refill the slots k_shade freed in this pass (its free list), then queue them.
+template <int SAMPLER>
+__global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  const uint32_t n = *wp.free_count;  // written by the previous kernel: the same value for every thread
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
+    const uint32_t i = base + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t slot = valid ? wp.free_q[i] : 0u;
+    bool push = false;
+    refill_block<SAMPLER>(sc, sp, wp, slot, valid, push);
+    const uint32_t pos = block_reserve(wp.q_out_count, push);
+    if (push) wp.q_out[pos] = slot;
+  }
+}
+
 // Partial stores of the per-slot records: only the fields a pass changes are written,
 // so k_shade does not keep the untouched ones (ray time, wavelength, ...) in registers.
 IZPI_DEV void store_ray(RayRec* rr, V3 o, V3 d, double tmin, double tmax, uint32_t kind, uint32_t pad) {
@@ -910,7 +956,7 @@ IZPI_DEV void store_path_rng_depth(PathSt* ps, uint32_t rng, uint32_t depth) {
 // variant from the scene's material kinds (results are identical).
 enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
 #ifndef IZPI_SHADE_WPE
-#define IZPI_SHADE_WPE 3  // MATSET_BASIC register budget: 3 waves/SIMD (no spill; 4 spills ~150 B/lane)
+#define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (no spill)
 #endif
 #ifndef IZPI_SHADE_WPE_OTHER
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
@@ -1105,26 +1151,14 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
         }
       }
     }
-    // refill finished slots with new work units (block-uniform loop)
-    bool want = done;
-    while (__syncthreads_or(want)) {
-      const uint32_t u = block_reserve(sp.head, want);
-      const uint32_t unit = u < sp.total_units ? u : 0xFFFFFFFFu;
-      if (want) {
-        if (unit == 0xFFFFFFFFu) {
-          want = false;
-        } else {
-          PathSt P;
-          RayRec R;
-          if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
-            wp.paths[slot] = P;
-            wp.rays[slot] = R;
-            want = false;
-            push = true;
-          }
-        }
-      }
+#if IZPI_SPLIT_REFILL
+    {  // finished slots go to the free list; k_refill gives them new units
+      const uint32_t fpos = block_reserve(wp.free_count, done);
+      if (done) wp.free_q[fpos] = slot;
     }
+#else
+    refill_block<SAMPLER>(sc, sp, wp, slot, done, push);
+#endif
     const uint32_t pos = block_reserve(wp.q_out_count, push);
     if (push) wp.q_out[pos] = slot;
   }
@@ -1342,7 +1376,7 @@ struct izpi_ctx {
   double* d_out = nullptr; size_t out_cap = 0;
   uint32_t* d_tiles = nullptr; size_t tiles_cap = 0;
   double* d_bg = nullptr; size_t bg_cap = 0;
-  uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts, [5] free count
+  uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts, [5] free count, [5] free count
   unsigned long long* d_counters = nullptr;
   RayRec* d_rays = nullptr; size_t rays_cap = 0;
   HitOut* d_hits = nullptr; size_t hits_cap = 0;
@@ -1480,7 +1514,11 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
   if ((rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res))) return rc;
+  int refill_res = 0;
+  if ((rc = resident_blocks(ctx, k_refill<SAMPLER>, &refill_res))) return rc;
   uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
+  wp.free_q = ctx->d_queue + 2 * (size_t)sp.slots;
+  wp.free_count = ctx->d_misc + 5;
   uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
   for (uint32_t s0 = 0; s0 < req->spp; s0 += chunk) {
     const uint32_t cs = std::min(chunk, req->spp - s0);
@@ -1508,12 +1546,17 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
         HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
         HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
+        if (IZPI_SPLIT_REFILL) HIP_TRY(hipMemsetAsync(wp.free_count, 0, sizeof(uint32_t), st));
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
         launch_trace(ctx, tr, wp, st);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
         hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, ctx->sc, sp, wp);
         HIP_TRY(hipGetLastError());
+        if (IZPI_SPLIT_REFILL) {
+          hipLaunchKernelGGL(k_refill<SAMPLER>, dim3(refill_res), dim3(256), 0, st, ctx->sc, sp, wp);
+          HIP_TRY(hipGetLastError());
+        }
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
       }
