@@ -117,8 +117,11 @@ def main():
     r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=local)
     setup_s = time.time() - t0
 
-    def step():
-        return r.render_distributed(rank, world)
+    from izpi_amd import _native as N
+    post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
+
+    def step():  # Render(): spectral configs include FireflyRejection + XYZToRGB (renderer.go:215-219)
+        return r.render_distributed(rank, world, post=post)
 
     for _ in range(args.warmup):
         step()
