@@ -83,6 +83,7 @@ struct DevScene {
   uint32_t num_lights;
   uint32_t nan_free_bounds;     // no NaN in any inner-node bound: slab4_fast allowed
   uint32_t leaf_shortcut;       // every leaf's slot-0 box equals its parent slot's box
+  uint32_t tri_only;            // no spheres: leaf tests may be spread over the wave
   izpi_camera cam;
 };
 
@@ -264,6 +265,26 @@ IZPI_DEV bool tri_intersect(const double* a, V3 o, V3 d, double tmin, double tma
   if (v < -eps || u + v > 1.0 + eps) return false;
   t = f * dot(e2, q);
   if (t < tmin || t > tmax) return false;
+  return true;
+}
+// The same test without the final `t > tMax` rejection: that last comparison is the
+// only one that depends on tMax, so tests of one leaf can run in parallel and be
+// accepted afterwards in primitive order against the running tMax (bit-identical).
+IZPI_DEV bool tri_intersect_no_tmax(const double* a, V3 o, V3 d, double tmin, double& t, double& u, double& v) {
+  const double eps = 1e-8;
+  V3 v0 = mk(a[0], a[1], a[2]), e1 = mk(a[3], a[4], a[5]), e2 = mk(a[6], a[7], a[8]);
+  V3 h = cross(d, e2);
+  double aa = dot(e1, h);
+  if (gm::abs(aa) < eps) return false;
+  double f = 1.0 / aa;
+  V3 s = sub(o, v0);
+  u = f * dot(s, h);
+  if (u < -eps || u > 1.0 + eps) return false;
+  V3 q = cross(s, e1);
+  v = f * dot(d, q);
+  if (v < -eps || u + v > 1.0 + eps) return false;
+  t = f * dot(e2, q);
+  if (t < tmin) return false;
   return true;
 }
 // Sphere.center (sphere.go:495-497)

@@ -314,12 +314,17 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
 // ring full, the oldest entry is spilled to a per-thread global area (entry e at
 // spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
 // are kept per wave in SGPRs (popcounts of ballots).
-template <int S, int WPE, bool P2>
+template <int S, int WPE, bool DIST>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   __shared__ int32_t lds_stack[S * 256];
+  // DIST: one wave-wide batch of leaf tests (primitive, owner lane, result)
+  __shared__ int32_t dist_prim[DIST ? 256 : 1];
+  __shared__ uint32_t dist_owner[DIST ? 256 : 1];
+  __shared__ double dist_t[DIST ? 256 : 1], dist_u[DIST ? 256 : 1], dist_v[DIST ? 256 : 1];
+  const uint32_t wbase = threadIdx.x & ~63u;
   int32_t* stk = lds_stack + threadIdx.x;
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
@@ -388,10 +393,54 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     bool leaf_next = false; // the step went straight into a leaf whose re-test is known to pass
     int32_t next = -1;
     if (n_prim * prim_w >= n_node * 16u) {
-      // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134); with P2, two
-      // consecutive primitives of the leaf per step (their loads and arithmetic overlap;
-      // the second test still sees the tMax the first may have shrunk, as in the loop)
-      bool is_tri = false, second = false, is_tri2 = false;
+      if constexpr (DIST) {  // the host picks DIST only for triangle-only scenes
+        // ---- distributed primitive step: every pending test of the PRIM lanes' leaves
+        // (up to 64) runs on its own lane, then each owner accepts its leaf's results in
+        // primitive order against its running tMax (bvh4.go:123-134, triangle.go:219)
+        const uint32_t cnt = (busy && in_prim) ? (uint32_t)(pend - pk) : 0u;  // 1..4
+        const uint64_t lt = (1ull << lane) - 1;
+        const uint32_t base = (uint32_t)__popcll(__ballot(cnt & 1u) & lt) + 2u * (uint32_t)__popcll(__ballot(cnt & 2u) & lt) +
+                              4u * (uint32_t)__popcll(__ballot(cnt & 4u) & lt);
+        const bool served = cnt > 0 && base + cnt <= 64;
+        const uint64_t ms = __ballot(served);
+        const int last = 63 - __clzll((long long)ms);
+        const uint32_t total = (uint32_t)__shfl((int)(base + cnt), last);
+        if (served)
+          for (uint32_t i = 0; i < cnt; i++) { dist_prim[wbase + base + i] = pk + (int32_t)i; dist_owner[wbase + base + i] = lane; }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t ow = lane < total ? dist_owner[wbase + lane] : lane;
+        const uint32_t oslot = (uint32_t)__shfl((int)slot, (int)ow);
+        if (lane < total) {
+          const int32_t pi = dist_prim[wbase + lane];
+          const double2* rp = reinterpret_cast<const double2*>(wp.rays + oslot);
+          const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+          const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
+          const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
+          const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
+          double t = 0, u = 0, v = 0;
+          const bool ok = tri_intersect_no_tmax(pa, mk(r0.x, r0.y, r1.x), mk(r1.y, r2.x, r2.y), r3.x, t, u, v);
+          dist_t[wbase + lane] = t; dist_u[wbase + lane] = u; dist_v[wbase + lane] = v;
+          dist_owner[wbase + lane] = ok ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (served) {
+          int32_t acc = -1;
+          for (uint32_t i = 0; i < cnt; i++) {
+            const uint32_t j = wbase + base + i;
+            const double t = dist_t[j];
+            if (dist_owner[j] && !(t > tmax)) { tmax = t; acc = (int32_t)j; bprim = pk + (int32_t)i; }
+          }
+          if (acc >= 0) { wp.hits[slot].u = dist_u[acc]; wp.hits[slot].v = dist_v[acc]; clean_from = sp; }
+          pk = pend;
+          in_prim = false;
+          advance = true;
+        }
+        __builtin_amdgcn_wave_barrier();
+        c_tri += total;
+        c_pstep++;
+      } else {
+      // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134)
+      bool is_tri = false;
       if (busy && in_prim) {
         // the f64 ray is re-read here (L2) instead of living in 14 VGPRs across node steps
         // (measured: keeping it in LDS instead makes k_shade's later read of the same
@@ -402,37 +451,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const double tmin = r3.x;
         const double2* pp = reinterpret_cast<const double2*>(sc.prims + pk);
         const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
-        second = P2 && pk + 1 < pend;
-        double2 s0 = p0, s1 = p1, s2 = p2, s3 = p3, s4 = p4;
-        if (second) { s0 = pp[5]; s1 = pp[6]; s2 = pp[7]; s3 = pp[8]; s4 = pp[9]; }
-#pragma unroll
-        for (int j = 0; j < (P2 ? 2 : 1); j++) {
-          if (j == 1 && !second) break;
-          const double2 a0 = j ? s0 : p0, a1 = j ? s1 : p1, a2 = j ? s2 : p2, a3 = j ? s3 : p3, a4 = j ? s4 : p4;
-          const double pa[9] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y, a4.x};
-          const bool tri = (uint32_t)__double2loint(a4.y) == IZPI_PRIM_TRIANGLE;
-          if (j == 0) is_tri = tri; else is_tri2 = tri;
-          if (tri) {
-            double t, u, v;
-            if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
-              tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v; clean_from = sp;
-            }
-          } else {
-            const double time = wp.rays[slot].time;  // only spheres read the ray time
-            double t; int root;
-            if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
-              tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0; clean_from = sp;
-            }
+        const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
+        is_tri = (uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE;
+        if (is_tri) {
+          double t, u, v;
+          if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
+            tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v; clean_from = sp;
           }
-          pk++;
+        } else {
+          const double time = wp.rays[slot].time;  // only spheres read the ray time
+          double t; int root;
+          if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
+            tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0; clean_from = sp;
+          }
         }
+        pk++;
         if (pk == pend) { in_prim = false; advance = true; }
       }
-      const uint32_t n_tri = (uint32_t)__popcll(__ballot(is_tri)) + (uint32_t)__popcll(__ballot(is_tri2));
-      const uint32_t n_tests = n_prim + (uint32_t)__popcll(__ballot(second));
+      const uint32_t n_tri = (uint32_t)__popcll(__ballot(is_tri));
       c_tri += n_tri;
-      c_sph += n_tests - n_tri;
+      c_sph += n_prim - n_tri;
       c_pstep++;
+      }
     } else {
       c_nodes += n_node;
       c_nstep++;
@@ -1437,24 +1477,26 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 // Traversal kernel selection. IZPI_TRACE=1 picks the one-visit-per-iteration kernel
 // (k_trace, LDS stack sized by the host bound); the default 2 picks the step-scheduled
 // k_trace2 with an LDS ring of IZPI_TRACE_RING entries (8/16/32, default 16) and global
-// spill; IZPI_PRIM_W (default 16) weighs primitive steps against node steps (x/16).
+// spill; IZPI_PRIM_W (default 32) weighs primitive steps against node steps (x/16).
 // All variants give identical results and counters.
 struct Tracer {
   int variant = 2, stack = 32, ring = 16, wpe = 5;
-  bool p2 = false;
-  uint32_t prim_w = 16, tchunk = 128, refill_min = 32;
+  bool p2 = true;  // DIST: spread leaf tests over the wave (triangle-only scenes)
+  uint32_t prim_w = 32, tchunk = 128, refill_min = 16;
   int blocks = 0;
 };
 
 // k_trace2 instances: ring entries x minimum waves per SIMD (register budget).
-#define IZPI_T2_LIST(X) X(8, 4, false) X(8, 5, false) X(16, 4, false) X(16, 5, false) X(32, 4, false) X(16, 4, true)
+#define IZPI_T2_LIST(X) X(8, 4, false) X(8, 5, false) X(16, 4, false) X(16, 5, false) X(32, 4, false) X(16, 4, true) \
+  X(16, 5, true) X(8, 5, true)
 
 int make_tracer(izpi_ctx* ctx, Tracer* t) {
   *t = Tracer();
   if (const char* e = getenv("IZPI_TRACE")) t->variant = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("IZPI_TRACE_RING")) t->ring = atoi(e);
   if (const char* e = getenv("IZPI_TRACE_WPE")) t->wpe = atoi(e);
-  if (const char* e = getenv("IZPI_TRACE_P2")) t->p2 = atoi(e) != 0;
+  if (const char* e = getenv("IZPI_TRACE_DIST")) t->p2 = atoi(e) != 0;
+  if (!ctx->sc.tri_only) t->p2 = false;  // sphere tests depend on tMax before the end (sphere.go:72-92)
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
@@ -1466,6 +1508,10 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   }
 #define IZPI_T2_OCC(R, W, P) if (t->ring == R && t->wpe == W && t->p2 == P) rc = resident_blocks(ctx, k_trace2<R, W, P>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
+  if (rc == IZPI_ERR_INVALID && t->p2) {  // no distributed instance for this ring/wpe: sequential leaf tests
+    t->p2 = false;
+    IZPI_T2_LIST(IZPI_T2_OCC)
+  }
 #undef IZPI_T2_OCC
   if (rc == IZPI_ERR_INVALID) { ctx->err = "no k_trace2 instance for IZPI_TRACE_RING/IZPI_TRACE_WPE"; return rc; }
   if (rc) return rc;
@@ -1923,6 +1969,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   sc.mat_flags = dmf; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
+  sc.tri_only = d->num_spheres == 0 ? 1u : 0u;
   sc.leaf_shortcut = leaf_shortcut;
   if (getenv("IZPI_NO_LEAF_SHORTCUT")) sc.leaf_shortcut = 0;
   sc.nan_free_bounds = 1;

@@ -201,7 +201,7 @@ def test_tiles_packed_and_unpack(gpu):
                                  {"IZPI_PRIM_W": "100000"}, {"IZPI_SLOTS": "3000", "IZPI_CHUNK_UNITS": "5000"},
                                  {"IZPI_NO_LEAF_SHORTCUT": "1"}, {"IZPI_TRACE_CHUNK": "1", "IZPI_REFILL_MIN": "1"},
                                  {"IZPI_TRACE_RING": "8", "IZPI_TRACE_WPE": "5"},
-                                 {"IZPI_TRACE_P2": "1", "IZPI_TRACE_WPE": "4"}])
+                                 {"IZPI_TRACE_DIST": "0"}, {"IZPI_TRACE_DIST": "1", "IZPI_TRACE_WPE": "4"}])
 def test_kernel_variants_bitwise(gpu, env, monkeypatch):
     """Traversal kernel variants, the LDS-ring spill path, step weights and tiny
     slot/chunk counts are launch knobs only: results and counters must not move."""
