@@ -871,22 +871,24 @@ IZPI_DEV void queue_push(const WaveParams& wp, bool push, uint32_t slot) { queue
 // with ONE atomic per 256-thread block (a single counter word saturates near 88
 // returning atomics/us chip-wide, MI355X_MICROARCH.md "dequeue"). All threads of the
 // block must call it (block-uniform control flow).
-IZPI_DEV uint32_t block_reserve(uint32_t* counter, bool want) {
-  __shared__ uint32_t s_w[4];
-  __shared__ uint32_t s_base;
+IZPI_DEV uint32_t block_reserve(uint32_t* counter, bool want, uint32_t& parity) {
+  // two LDS buffer sets used alternately, so no trailing barrier is needed before reuse
+  __shared__ uint32_t s_w[2][4];
+  __shared__ uint32_t s_base[2];
+  const uint32_t b = parity;
+  parity ^= 1u;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t m = __ballot(want);
-  if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+  if (lane == 0) s_w[b][w] = (uint32_t)__popcll(m);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    s_base = tot ? atomicAdd(counter, tot) : 0u;
+    const uint32_t tot = s_w[b][0] + s_w[b][1] + s_w[b][2] + s_w[b][3];
+    s_base[b] = tot ? atomicAdd(counter, tot) : 0u;
   }
   __syncthreads();
-  uint32_t off = s_base;
-  for (uint32_t i = 0; i < w; i++) off += s_w[i];
+  uint32_t off = s_base[b];
+  for (uint32_t i = 0; i < w; i++) off += s_w[b][i];
   off += (uint32_t)__popcll(m & ((1ull << lane) - 1));
-  __syncthreads();  // s_w / s_base are reused by the next call
   return off;
 }
 
@@ -938,9 +940,9 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
 // loop, block-wide unit reservations). Sets `push` when the slot has a ray.
 template <int SAMPLER>
 IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, bool want,
-                           bool& push) {
+                           bool& push, uint32_t& parity) {
   while (__syncthreads_or(want)) {
-    const uint32_t u = block_reserve(sp.head, want);
+    const uint32_t u = block_reserve(sp.head, want, parity);
     const uint32_t unit = u < sp.total_units ? u : 0xFFFFFFFFu;
     if (want) {
       if (unit == 0xFFFFFFFFu) {
@@ -962,6 +964,7 @@ IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const Wave
 // Refill the slots k_shade freed in this pass (its free list), then queue them.
 template <int SAMPLER>
 __global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  uint32_t parity = 0;  // block_reserve LDS buffer set
   const uint32_t n = *wp.free_count;  // written by the previous kernel: the same value for every thread
   const uint32_t stride = gridDim.x * 256;
   for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
@@ -969,8 +972,8 @@ __global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadePa
     const bool valid = i < n;
     const uint32_t slot = valid ? wp.free_q[i] : 0u;
     bool push = false;
-    refill_block<SAMPLER>(sc, sp, wp, slot, valid, push);
-    const uint32_t pos = block_reserve(wp.q_out_count, push);
+    refill_block<SAMPLER>(sc, sp, wp, slot, valid, push, parity);
+    const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
     if (push) wp.q_out[pos] = slot;
   }
 }
@@ -1005,6 +1008,7 @@ template <int SAMPLER, int MATSET>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET == MATSET_BASIC && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  uint32_t parity = 0;  // block_reserve LDS buffer set
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const uint32_t n = *wp.q_in_count;
   uint32_t c_lt = 0, c_ls = 0;
@@ -1193,13 +1197,13 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     }
 #if IZPI_SPLIT_REFILL
     {  // finished slots go to the free list; k_refill gives them new units
-      const uint32_t fpos = block_reserve(wp.free_count, done);
+      const uint32_t fpos = block_reserve(wp.free_count, done, parity);
       if (done) wp.free_q[fpos] = slot;
     }
 #else
-    refill_block<SAMPLER>(sc, sp, wp, slot, done, push);
+    refill_block<SAMPLER>(sc, sp, wp, slot, done, push, parity);
 #endif
-    const uint32_t pos = block_reserve(wp.q_out_count, push);
+    const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
     if (push) wp.q_out[pos] = slot;
   }
   const uint32_t lane = threadIdx.x & 63;
