@@ -150,22 +150,31 @@ struct alignas(16) RayRec {   // the ray a slot wants traced next
   uint32_t kind;              // RAY_MAIN (counts as a Sampler call) / RAY_PATHLEN
   uint32_t pad;
 };
-struct alignas(16) HitOut {   // closest hit of that ray (deferred record)
+// Closest hit of a slot's ray and its path state. In HBM each is split into a hot record
+// every pass reads and a cold one read only when needed (UV-textured / sphere hits;
+// spectral wavelength, dielectric point), so k_shade moves fewer 64-B sectors.
+struct HitOut {               // register form
   double t, u, v;             // triangle barycentrics, or u = sphere root
   int32_t prim;               // leaf-order primitive, -1 = miss
   uint32_t pad;
 };
-struct alignas(16) PathSt {   // sampler state of the pixel-sample in this slot
+struct alignas(16) HitHot { double t; int32_t prim; uint32_t pad; };
+struct alignas(16) HitUV { double u, v; };
+struct PathSt {               // register form
   double lambda, lpdf;        // wavelength and its pdf (spectral)
   double pend[3];             // dielectric hit point while its path-length ray is traced
   uint32_t rng, depth, unit, pad;
 };
+struct alignas(16) PathHot { uint32_t rng, depth, unit, pad; };
+struct alignas(16) PathCold { double lambda, lpdf; double pend[3]; double pad; };
 enum { RAY_MAIN = 0, RAY_PATHLEN = 1 };
 
 struct WaveParams {
   RayRec* rays;
-  HitOut* hits;
-  PathSt* paths;
+  HitHot* hhot;
+  HitUV* huv;
+  PathHot* phot;
+  PathCold* pcold;
   const uint32_t* q_in;       // slots to process this pass
   const uint32_t* q_in_count;
   uint32_t* q_out;            // slots whose next ray must be traced
@@ -224,7 +233,7 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
             sp = 0;
             bprim = -1;
             busy = cur != -1;
-            if (!busy) { HitOut& h = wp.hits[slot]; h.prim = -1; }
+            if (!busy) { wp.hhot[slot].prim = -1; }
           }
         }
       } else if (exhausted && idle == ~0ull) {
@@ -285,9 +294,10 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
       sp--;
       cur = stk[sp * 256];
     } else {
-      HitOut h;
-      h.t = bt; h.u = bu; h.v = bv; h.prim = bprim; h.pad = 0;
-      wp.hits[slot] = h;
+      HitHot h;
+      h.t = bt; h.prim = bprim; h.pad = 0;
+      wp.hhot[slot] = h;
+      wp.huv[slot] = HitUV{bu, bv};
       busy = false;
     }
   }
@@ -377,7 +387,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             in_prim = false;
             bprim = -1;
             busy = cur != -1;
-            if (!busy) { HitOut& h = wp.hits[slot]; h.t = 0; h.u = 0; h.v = 0; h.prim = -1; h.pad = 0; }
+            if (!busy) { wp.hhot[slot] = HitHot{0.0, -1, 0u}; wp.huv[slot] = HitUV{0.0, 0.0}; }
           }
         }
         c_rays += (uint64_t)__popcll(__ballot(main_ray));
@@ -430,7 +440,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             const double t = dist_t[j];
             if (dist_owner[j] && !(t > tmax)) { tmax = t; acc = (int32_t)j; bprim = pk + (int32_t)i; }
           }
-          if (acc >= 0) { wp.hits[slot].u = dist_u[acc]; wp.hits[slot].v = dist_v[acc]; clean_from = sp; }
+          if (acc >= 0) { wp.huv[slot] = HitUV{dist_u[acc], dist_v[acc]}; clean_from = sp; }
           pk = pend;
           in_prim = false;
           advance = true;
@@ -456,13 +466,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (is_tri) {
           double t, u, v;
           if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
-            tmax = t; bprim = pk; wp.hits[slot].u = u; wp.hits[slot].v = v; clean_from = sp;
+            tmax = t; bprim = pk; wp.huv[slot] = HitUV{u, v}; clean_from = sp;
           }
         } else {
           const double time = wp.rays[slot].time;  // only spheres read the ray time
           double t; int root;
           if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
-            tmax = t; bprim = pk; wp.hits[slot].u = (double)root; wp.hits[slot].v = 0; clean_from = sp;
+            tmax = t; bprim = pk; wp.huv[slot] = HitUV{(double)root, 0.0}; clean_from = sp;
           }
         }
         pk++;
@@ -553,10 +563,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
         if (sp < clean_from) clean_from = sp;
       } else {
-        HitOut& h = wp.hits[slot];
-        h.t = bprim >= 0 ? tmax : 0.0;
-        h.prim = bprim;
-        if (bprim < 0) { h.u = 0; h.v = 0; }
+        wp.hhot[slot] = HitHot{bprim >= 0 ? tmax : 0.0, bprim, 0u};
+        if (bprim < 0) wp.huv[slot] = HitUV{0.0, 0.0};
         busy = false;
       }
     }
@@ -581,8 +589,9 @@ struct HitRec {
   V3 p, n;
   uint32_t mat;
 };
-IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const GShade& gs, V3 o, V3 d, double time, bool want_uv,
-                         HitRec& h) {
+// `uvp` holds the hit's (u, v): read only for UV-textured triangles and for spheres.
+IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitUV* uvp, const GShade& gs, V3 o, V3 d, double time,
+                         bool want_uv, HitRec& h) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
   h.mat = gs.mat;
@@ -591,7 +600,8 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const GShade& gs, 
     V3 n = mk(gs.n[0], gs.n[1], gs.n[2]);
     if (want_uv) {  // (u,v) are read only by image textures and normal maps
       const double eps = 1e-8;
-      double u = c.u, v = c.v;
+      const HitUV huv = *uvp;
+      double u = huv.u, v = huv.v;
       double w = 1.0 - u - v;
       double sum = u + v + w;
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
@@ -618,7 +628,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const GShade& gs, 
     V3 ctr = sph_center(pa, time);
     V3 on = sdiv(sub(h.p, ctr), pa[6]);
     V3 flipped = dot(d, on) >= 0 ? smul(on, -1) : on;
-    h.n = c.u == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
+    h.n = uvp->u == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
     if (want_uv) {
       double phi = gm::atan2(flipped.z, flipped.x);
       double theta = gm::asin(flipped.y);
@@ -854,6 +864,12 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slo
   return true;
 }
 
+template <int SAMPLER>
+IZPI_DEV void store_path(const WaveParams& wp, uint32_t slot, const PathSt& P) {
+  wp.phot[slot] = PathHot{P.rng, P.depth, P.unit, 0u};
+  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { wp.pcold[slot].lambda = P.lambda; wp.pcold[slot].lpdf = P.lpdf; }
+}
+
 // Append `push` lanes' slots to the output queue: one atomic per wave.
 IZPI_DEV void queue_push(uint32_t* q, uint32_t* count, bool push, uint32_t slot) {
   const uint64_t m = __ballot(push);
@@ -922,7 +938,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
         PathSt P;
         RayRec R;
         if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
-          wp.paths[slot] = P;
+          store_path<SAMPLER>(wp, slot, P);
           wp.rays[slot] = R;
           want = false;
           push = true;
@@ -951,7 +967,7 @@ IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const Wave
         PathSt P;
         RayRec R;
         if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
-          wp.paths[slot] = P;
+          store_path<SAMPLER>(wp, slot, P);
           wp.rays[slot] = R;
           want = false;
           push = true;
@@ -988,7 +1004,7 @@ IZPI_DEV void store_ray(RayRec* rr, V3 o, V3 d, double tmin, double tmax, uint32
   p[3] = make_double2(tmin, tmax);
   *reinterpret_cast<uint2*>(&rr->kind) = make_uint2(kind, pad);  // rr->time is left as is
 }
-IZPI_DEV void store_path_rng_depth(PathSt* ps, uint32_t rng, uint32_t depth) {
+IZPI_DEV void store_path_rng_depth(PathHot* ps, uint32_t rng, uint32_t depth) {
   *reinterpret_cast<uint2*>(&ps->rng) = make_uint2(rng, depth);
 }
 
@@ -1021,9 +1037,19 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     bool push = false;      // slot has a ray to trace next
     bool done = false;      // slot's sample finished: grab a new unit
     if (valid) {
-      PathSt P = wp.paths[slot];
+      PathSt P;
+      {
+        const PathHot ph = wp.phot[slot];
+        P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.pad = 0;
+        P.lambda = 0; P.lpdf = 1;
+        if (!COLOUR) { const PathCold& pc = wp.pcold[slot]; P.lambda = pc.lambda; P.lpdf = pc.lpdf; }
+      }
       RayRec R = wp.rays[slot];
-      const HitOut H = wp.hits[slot];
+      HitOut H;
+      {
+        const HitHot hh = wp.hhot[slot];
+        H.t = hh.t; H.prim = hh.prim; H.pad = 0; H.u = 0; H.v = 0;
+      }
       Lcg rng;
       rng.s = P.rng;
       const V3 ro = mk(R.o[0], R.o[1], R.o[2]), rd = mk(R.d[0], R.d[1], R.d[2]);
@@ -1035,7 +1061,8 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       Onb cos_onb;
       if (MATSET == MATSET_FULL && R.kind == RAY_PATHLEN) {
         // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
-        const V3 hp = mk(P.pend[0], P.pend[1], P.pend[2]);
+        const PathCold& pc = wp.pcold[slot];
+        const V3 hp = mk(pc.pend[0], pc.pend[1], pc.pend[2]);
         double len = 10.0;
         if (H.prim >= 0) {
           V3 exit_p = add(ro, smul(rd, H.t));
@@ -1057,7 +1084,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       } else {
         const GShade gs = sc.shade[H.prim];
         HitRec h;
-        hit_record(sc, H, gs, ro, rd, R.time, (sc.mat_flags[gs.mat] & 1u) != 0, h);
+        hit_record(sc, H, wp.huv + slot, gs, ro, rd, R.time, (sc.mat_flags[gs.mat] & 1u) != 0, h);
         hit_n = h.n;
         next_o = h.p;
         const izpi_material& m = sc.materials[h.mat];
@@ -1087,9 +1114,9 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
             const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
             if (!reflected && (!COLOUR || beer_rgb)) {
               // the extra World.Hit of calculatePathLength: trace it, finish next pass
-              PathSt* ps = wp.paths + slot;
-              ps->pend[0] = h.p.x; ps->pend[1] = h.p.y; ps->pend[2] = h.p.z;
-              store_path_rng_depth(ps, rng.s, P.depth);
+              PathCold* pcw = wp.pcold + slot;
+              pcw->pend[0] = h.p.x; pcw->pend[1] = h.p.y; pcw->pend[2] = h.p.z;
+              store_path_rng_depth(wp.phot + slot, rng.s, P.depth);
               store_ray(wp.rays + slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
               push = true;
               break;
@@ -1188,7 +1215,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
             finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
             done = true;
           } else {
-            store_path_rng_depth(wp.paths + slot, P.rng, P.depth);
+            store_path_rng_depth(wp.phot + slot, P.rng, P.depth);
             store_ray(wp.rays + slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0);
             push = true;
           }
@@ -1348,18 +1375,20 @@ __global__ void k_trace_setup(const double* rays, uint32_t n, RayRec* rr, uint32
   rr[i] = R;
   q[i] = i;
 }
-__global__ void k_trace_records(const DevScene sc, const RayRec* rr, const HitOut* hits, uint32_t n, izpi_hit* out) {
+__global__ void k_trace_records(const DevScene sc, const RayRec* rr, const HitHot* hhot, const HitUV* huv, uint32_t n,
+                                izpi_hit* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   izpi_hit h;
   memset(&h, 0, sizeof(h));
   h.prim_ref = 0xFFFFFFFFu;
-  const HitOut c = hits[i];
+  HitOut c;
+  c.t = hhot[i].t; c.prim = hhot[i].prim; c.u = huv[i].u; c.v = huv[i].v; c.pad = 0;
   if (c.prim >= 0) {
     const RayRec R = rr[i];
     HitRec hr;
     const GShade gs = sc.shade[c.prim];
-    hit_record(sc, c, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
+    hit_record(sc, c, huv + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
     const GPrim& p = sc.prims[c.prim];
     h.hit = 1; h.t = hr.t; h.u = hr.u; h.v = hr.v;
     h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
@@ -1423,8 +1452,10 @@ struct izpi_ctx {
   uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts, [5] free count, [5] free count
   unsigned long long* d_counters = nullptr;
   RayRec* d_rays = nullptr; size_t rays_cap = 0;
-  HitOut* d_hits = nullptr; size_t hits_cap = 0;
-  PathSt* d_paths = nullptr; size_t paths_cap = 0;
+  HitHot* d_hhot = nullptr; size_t hhot_cap = 0;
+  HitUV* d_huv = nullptr; size_t huv_cap = 0;
+  PathHot* d_phot = nullptr; size_t phot_cap = 0;
+  PathCold* d_pcold = nullptr; size_t pcold_cap = 0;
   uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
@@ -1675,7 +1706,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
   {  // keep the wavefront state within a quarter of the free HBM
     if (free_b > 0) {
-      const uint64_t per_slot = sizeof(RayRec) + sizeof(HitOut) + sizeof(PathSt) + 12 +
+      const uint64_t per_slot = sizeof(RayRec) + sizeof(HitHot) + sizeof(HitUV) + sizeof(PathHot) + sizeof(PathCold) + 12 +
                                 (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
       slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 4) / per_slot));
     }
@@ -1688,8 +1719,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if ((rc = grow(ctx, (void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_rays, &ctx->rays_cap, (size_t)slots * sizeof(RayRec)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_hits, &ctx->hits_cap, (size_t)slots * sizeof(HitOut)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_paths, &ctx->paths_cap, (size_t)slots * sizeof(PathSt)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_hhot, &ctx->hhot_cap, (size_t)slots * sizeof(HitHot)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_huv, &ctx->huv_cap, (size_t)slots * sizeof(HitUV)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_phot, &ctx->phot_cap, (size_t)slots * sizeof(PathHot)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_pcold, &ctx->pcold_cap, (size_t)slots * sizeof(PathCold)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)3 * slots * sizeof(uint32_t)))) return rc;
   const size_t nbg = req->num_bg_spd;
   if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
@@ -1711,7 +1744,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.head = ctx->d_misc;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
   WaveParams wp{};
-  wp.rays = ctx->d_rays; wp.hits = ctx->d_hits; wp.paths = ctx->d_paths; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  wp.rays = ctx->d_rays; wp.hhot = ctx->d_hhot; wp.huv = ctx->d_huv; wp.phot = ctx->d_phot; wp.pcold = ctx->d_pcold; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
   ap.tile_w = tw; ap.tile_h = th; ap.sampler = req->sampler; ap.out_layout = req->out_layout;
@@ -1797,7 +1830,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   free_scene(ctx);
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
-                  ctx->d_counters, ctx->d_rays, ctx->d_hits, ctx->d_paths, ctx->d_queue, ctx->d_spill, ctx->d_post};
+                  ctx->d_counters, ctx->d_rays, ctx->d_hhot, ctx->d_huv, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
@@ -2079,28 +2112,29 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (!ctx->have_scene) { ctx->err = "no scene"; return IZPI_ERR_NO_SCENE; }
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
-  double* dr; izpi_hit* dh; RayRec* rr; HitOut* ho; uint32_t* q;
+  double* dr; izpi_hit* dh; RayRec* rr; HitHot* hh; HitUV* hu; uint32_t* q;
   HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 8 * sizeof(double)));
   HIP_TRY(hipMalloc((void**)&dh, (size_t)n * sizeof(izpi_hit)));
   HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayRec)));
-  HIP_TRY(hipMalloc((void**)&ho, (size_t)n * sizeof(HitOut)));
+  HIP_TRY(hipMalloc((void**)&hh, (size_t)n * sizeof(HitHot)));
+  HIP_TRY(hipMalloc((void**)&hu, (size_t)n * sizeof(HitUV)));
   HIP_TRY(hipMalloc((void**)&q, (size_t)n * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, q, ctx->d_misc + 3);
   WaveParams wp{};
-  wp.rays = rr; wp.hits = ho; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
+  wp.rays = rr; wp.hhot = hh; wp.huv = hu; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
   launch_trace(ctx, tr, wp, ctx->stream);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, ho, n, dh);
+  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, hu, n, dh);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));
-  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(ho); (void)hipFree(q);
+  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(hh); (void)hipFree(hu); (void)hipFree(q);
   return IZPI_OK;
 }
 
