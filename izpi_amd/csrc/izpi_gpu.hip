@@ -143,13 +143,17 @@ IZPI_DEV void cie_values(double w, double& x, double& y, double& z) {
 }
 
 // ============================================================ wavefront state
-// Per-slot records in HBM (AoS, 16-B aligned so each is a few dwordx4 accesses).
-struct alignas(16) RayRec {   // the ray a slot wants traced next
+// Per-slot records in HBM. The ray a slot wants traced next is kept as a 64-B-aligned
+// hot record (o, d, tmin, tmax: exactly one 64-B sector, read by every traversal refill
+// and primitive step) plus a 16-B aux record (time, kind, material of a path-length ray).
+struct RayRec {               // register form
   double o[3], d[3];
   double tmin, tmax, time;
   uint32_t kind;              // RAY_MAIN (counts as a Sampler call) / RAY_PATHLEN
   uint32_t pad;
 };
+struct alignas(64) RayHot { double o[3], d[3]; double tmin, tmax; };
+struct alignas(16) RayAux { double time; uint32_t kind, pad; };
 // Closest hit of a slot's ray and its path state. In HBM each is split into a hot record
 // every pass reads and a cold one read only when needed (UV-textured / sphere hits;
 // spectral wavelength, dielectric point), so k_shade moves fewer 64-B sectors.
@@ -170,7 +174,8 @@ struct alignas(16) PathCold { double lambda, lpdf; double pend[3]; double pad; }
 enum { RAY_MAIN = 0, RAY_PATHLEN = 1 };
 
 struct WaveParams {
-  RayRec* rays;
+  RayHot* rhot;
+  RayAux* raux;
   HitHot* hhot;
   HitUV* huv;
   PathHot* phot;
@@ -222,11 +227,12 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
           const uint32_t my = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
           if (my < n) {
             slot = wp.q_in[my];
-            const RayRec& r = wp.rays[slot];
+            const RayHot& r = wp.rhot[slot];
+            const RayAux& ra = wp.raux[slot];
             o = mk(r.o[0], r.o[1], r.o[2]);
             d = mk(r.d[0], r.d[1], r.d[2]);
-            tmin = r.tmin; tmax = r.tmax; time = r.time;
-            if (r.kind == RAY_MAIN) c_rays++;
+            tmin = r.tmin; tmax = r.tmax; time = ra.time;
+            if (ra.kind == RAY_MAIN) c_rays++;
             ix = (float)(1.0 / d.x); iy = (float)(1.0 / d.y); iz = (float)(1.0 / d.z);
             ox = (float)o.x; oy = (float)o.y; oz = (float)o.z;
             cur = sc.root;
@@ -376,9 +382,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const uint32_t my = base + rank;
           if (rank < take) {
             slot = wp.q_in[my];
-            const RayRec& r = wp.rays[slot];
+            const RayHot& r = wp.rhot[slot];
             tmax = r.tmax;
-            main_ray = r.kind == RAY_MAIN;
+            main_ray = wp.raux[slot].kind == RAY_MAIN;
             ix = (float)(1.0 / r.d[0]); iy = (float)(1.0 / r.d[1]); iz = (float)(1.0 / r.d[2]);
             ox = (float)r.o[0]; oy = (float)r.o[1]; oz = (float)r.o[2];
             fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
@@ -422,7 +428,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const uint32_t oslot = (uint32_t)__shfl((int)slot, (int)ow);
         if (lane < total) {
           const int32_t pi = dist_prim[wbase + lane];
-          const double2* rp = reinterpret_cast<const double2*>(wp.rays + oslot);
+          const double2* rp = reinterpret_cast<const double2*>(wp.rhot + oslot);
           const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
           const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
           const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
@@ -455,7 +461,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         // the f64 ray is re-read here (L2) instead of living in 14 VGPRs across node steps
         // (measured: keeping it in LDS instead makes k_shade's later read of the same
         // record miss and costs more than it saves)
-        const double2* rp = reinterpret_cast<const double2*>(wp.rays + slot);
+        const double2* rp = reinterpret_cast<const double2*>(wp.rhot + slot);
         const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
         const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
         const double tmin = r3.x;
@@ -469,7 +475,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             tmax = t; bprim = pk; wp.huv[slot] = HitUV{u, v}; clean_from = sp;
           }
         } else {
-          const double time = wp.rays[slot].time;  // only spheres read the ray time
+          const double time = wp.raux[slot].time;  // only spheres read the ray time
           double t; int root;
           if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
             tmax = t; bprim = pk; wp.huv[slot] = HitUV{(double)root, 0.0}; clean_from = sp;
@@ -870,6 +876,14 @@ IZPI_DEV void store_path(const WaveParams& wp, uint32_t slot, const PathSt& P) {
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { wp.pcold[slot].lambda = P.lambda; wp.pcold[slot].lpdf = P.lpdf; }
 }
 
+IZPI_DEV void store_ray_full(const WaveParams& wp, uint32_t slot, const RayRec& R) {
+  RayHot h;
+  for (int k = 0; k < 3; k++) { h.o[k] = R.o[k]; h.d[k] = R.d[k]; }
+  h.tmin = R.tmin; h.tmax = R.tmax;
+  wp.rhot[slot] = h;
+  wp.raux[slot] = RayAux{R.time, R.kind, R.pad};
+}
+
 // Append `push` lanes' slots to the output queue: one atomic per wave.
 IZPI_DEV void queue_push(uint32_t* q, uint32_t* count, bool push, uint32_t slot) {
   const uint64_t m = __ballot(push);
@@ -939,7 +953,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
         RayRec R;
         if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
           store_path<SAMPLER>(wp, slot, P);
-          wp.rays[slot] = R;
+          store_ray_full(wp, slot, R);
           want = false;
           push = true;
         }
@@ -968,7 +982,7 @@ IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const Wave
         RayRec R;
         if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
           store_path<SAMPLER>(wp, slot, P);
-          wp.rays[slot] = R;
+          store_ray_full(wp, slot, R);
           want = false;
           push = true;
         }
@@ -996,13 +1010,14 @@ __global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadePa
 
 // Partial stores of the per-slot records: only the fields a pass changes are written,
 // so k_shade does not keep the untouched ones (ray time, wavelength, ...) in registers.
-IZPI_DEV void store_ray(RayRec* rr, V3 o, V3 d, double tmin, double tmax, uint32_t kind, uint32_t pad) {
-  double2* p = reinterpret_cast<double2*>(rr);
+IZPI_DEV void store_ray(const WaveParams& wp, uint32_t slot, V3 o, V3 d, double tmin, double tmax, uint32_t kind,
+                        uint32_t pad) {
+  double2* p = reinterpret_cast<double2*>(wp.rhot + slot);
   p[0] = make_double2(o.x, o.y);
   p[1] = make_double2(o.z, d.x);
   p[2] = make_double2(d.y, d.z);
   p[3] = make_double2(tmin, tmax);
-  *reinterpret_cast<uint2*>(&rr->kind) = make_uint2(kind, pad);  // rr->time is left as is
+  *reinterpret_cast<uint2*>(&wp.raux[slot].kind) = make_uint2(kind, pad);  // the ray time is left as is
 }
 IZPI_DEV void store_path_rng_depth(PathHot* ps, uint32_t rng, uint32_t depth) {
   *reinterpret_cast<uint2*>(&ps->rng) = make_uint2(rng, depth);
@@ -1044,7 +1059,15 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
         P.lambda = 0; P.lpdf = 1;
         if (!COLOUR) { const PathCold& pc = wp.pcold[slot]; P.lambda = pc.lambda; P.lpdf = pc.lpdf; }
       }
-      RayRec R = wp.rays[slot];
+      RayRec R;
+      {
+        const RayHot rh = wp.rhot[slot];
+        for (int k = 0; k < 3; k++) { R.o[k] = rh.o[k]; R.d[k] = rh.d[k]; }
+        R.tmin = rh.tmin; R.tmax = rh.tmax;
+        const RayAux& ra = wp.raux[slot];
+        R.kind = ra.kind; R.pad = ra.pad;
+        R.time = 0;  // read below only for sphere hits
+      }
       HitOut H;
       {
         const HitHot hh = wp.hhot[slot];
@@ -1084,7 +1107,8 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       } else {
         const GShade gs = sc.shade[H.prim];
         HitRec h;
-        hit_record(sc, H, wp.huv + slot, gs, ro, rd, R.time, (sc.mat_flags[gs.mat] & 1u) != 0, h);
+        const double rtime = IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_SPHERE ? wp.raux[slot].time : 0.0;
+        hit_record(sc, H, wp.huv + slot, gs, ro, rd, rtime, (sc.mat_flags[gs.mat] & 1u) != 0, h);
         hit_n = h.n;
         next_o = h.p;
         const izpi_material& m = sc.materials[h.mat];
@@ -1117,7 +1141,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
               PathCold* pcw = wp.pcold + slot;
               pcw->pend[0] = h.p.x; pcw->pend[1] = h.p.y; pcw->pend[2] = h.p.z;
               store_path_rng_depth(wp.phot + slot, rng.s, P.depth);
-              store_ray(wp.rays + slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
+              store_ray(wp, slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
               push = true;
               break;
             }
@@ -1216,7 +1240,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
             done = true;
           } else {
             store_path_rng_depth(wp.phot + slot, P.rng, P.depth);
-            store_ray(wp.rays + slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0);
+            store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0);
             push = true;
           }
         }
@@ -1364,7 +1388,7 @@ __global__ void k_unpack(const uint32_t* tiles, uint32_t num_pixels, uint32_t ti
 
 // ------------------------------------------------------- component kernels
 // izpi_gpu_trace: rays [n][8] -> RayRec, queue = identity
-__global__ void k_trace_setup(const double* rays, uint32_t n, RayRec* rr, uint32_t* q, uint32_t* qn) {
+__global__ void k_trace_setup(const double* rays, uint32_t n, RayHot* rh, RayAux* ra, uint32_t* q, uint32_t* qn) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) *qn = n;
   if (i >= n) return;
@@ -1372,10 +1396,14 @@ __global__ void k_trace_setup(const double* rays, uint32_t n, RayRec* rr, uint32
   RayRec R;
   for (int k = 0; k < 3; k++) { R.o[k] = r[k]; R.d[k] = r[3 + k]; }
   R.tmin = r[6]; R.tmax = r[7]; R.time = 0; R.kind = RAY_PATHLEN; R.pad = 0;
-  rr[i] = R;
+  RayHot h;
+  for (int k = 0; k < 3; k++) { h.o[k] = R.o[k]; h.d[k] = R.d[k]; }
+  h.tmin = R.tmin; h.tmax = R.tmax;
+  rh[i] = h;
+  ra[i] = RayAux{R.time, R.kind, R.pad};
   q[i] = i;
 }
-__global__ void k_trace_records(const DevScene sc, const RayRec* rr, const HitHot* hhot, const HitUV* huv, uint32_t n,
+__global__ void k_trace_records(const DevScene sc, const RayHot* rr, const HitHot* hhot, const HitUV* huv, uint32_t n,
                                 izpi_hit* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
@@ -1385,7 +1413,7 @@ __global__ void k_trace_records(const DevScene sc, const RayRec* rr, const HitHo
   HitOut c;
   c.t = hhot[i].t; c.prim = hhot[i].prim; c.u = huv[i].u; c.v = huv[i].v; c.pad = 0;
   if (c.prim >= 0) {
-    const RayRec R = rr[i];
+    const RayHot R = rr[i];
     HitRec hr;
     const GShade gs = sc.shade[c.prim];
     hit_record(sc, c, huv + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
@@ -1451,7 +1479,8 @@ struct izpi_ctx {
   double* d_bg = nullptr; size_t bg_cap = 0;
   uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts, [5] free count, [5] free count
   unsigned long long* d_counters = nullptr;
-  RayRec* d_rays = nullptr; size_t rays_cap = 0;
+  RayHot* d_rhot = nullptr; size_t rhot_cap = 0;
+  RayAux* d_raux = nullptr; size_t raux_cap = 0;
   HitHot* d_hhot = nullptr; size_t hhot_cap = 0;
   HitUV* d_huv = nullptr; size_t huv_cap = 0;
   PathHot* d_phot = nullptr; size_t phot_cap = 0;
@@ -1706,7 +1735,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
   {  // keep the wavefront state within a quarter of the free HBM
     if (free_b > 0) {
-      const uint64_t per_slot = sizeof(RayRec) + sizeof(HitHot) + sizeof(HitUV) + sizeof(PathHot) + sizeof(PathCold) + 12 +
+      const uint64_t per_slot = sizeof(RayHot) + sizeof(RayAux) + sizeof(HitHot) + sizeof(HitUV) + sizeof(PathHot) + sizeof(PathCold) + 12 +
                                 (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
       slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 4) / per_slot));
     }
@@ -1718,7 +1747,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if ((rc = grow(ctx, (void**)&ctx->d_recs, &ctx->recs_cap, (size_t)depth_cap * 6 * slots * sizeof(double)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_rays, &ctx->rays_cap, (size_t)slots * sizeof(RayRec)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_rhot, &ctx->rhot_cap, (size_t)slots * sizeof(RayHot)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_raux, &ctx->raux_cap, (size_t)slots * sizeof(RayAux)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_hhot, &ctx->hhot_cap, (size_t)slots * sizeof(HitHot)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_huv, &ctx->huv_cap, (size_t)slots * sizeof(HitUV)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_phot, &ctx->phot_cap, (size_t)slots * sizeof(PathHot)))) return rc;
@@ -1744,7 +1774,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.head = ctx->d_misc;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
   WaveParams wp{};
-  wp.rays = ctx->d_rays; wp.hhot = ctx->d_hhot; wp.huv = ctx->d_huv; wp.phot = ctx->d_phot; wp.pcold = ctx->d_pcold; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  wp.rhot = ctx->d_rhot; wp.raux = ctx->d_raux; wp.hhot = ctx->d_hhot; wp.huv = ctx->d_huv; wp.phot = ctx->d_phot; wp.pcold = ctx->d_pcold; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
   ap.tile_w = tw; ap.tile_h = th; ap.sampler = req->sampler; ap.out_layout = req->out_layout;
@@ -1830,7 +1860,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   free_scene(ctx);
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
-                  ctx->d_counters, ctx->d_rays, ctx->d_hhot, ctx->d_huv, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post};
+                  ctx->d_counters, ctx->d_rhot, ctx->d_raux, ctx->d_hhot, ctx->d_huv, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
@@ -2112,19 +2142,20 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (!ctx->have_scene) { ctx->err = "no scene"; return IZPI_ERR_NO_SCENE; }
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
-  double* dr; izpi_hit* dh; RayRec* rr; HitHot* hh; HitUV* hu; uint32_t* q;
+  double* dr; izpi_hit* dh; RayHot* rr; RayAux* rx; HitHot* hh; HitUV* hu; uint32_t* q;
   HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 8 * sizeof(double)));
   HIP_TRY(hipMalloc((void**)&dh, (size_t)n * sizeof(izpi_hit)));
-  HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayRec)));
+  HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayHot)));
+  HIP_TRY(hipMalloc((void**)&rx, (size_t)n * sizeof(RayAux)));
   HIP_TRY(hipMalloc((void**)&hh, (size_t)n * sizeof(HitHot)));
   HIP_TRY(hipMalloc((void**)&hu, (size_t)n * sizeof(HitUV)));
   HIP_TRY(hipMalloc((void**)&q, (size_t)n * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
-  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, q, ctx->d_misc + 3);
+  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, rx, q, ctx->d_misc + 3);
   WaveParams wp{};
-  wp.rays = rr; wp.hhot = hh; wp.huv = hu; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
+  wp.rhot = rr; wp.raux = rx; wp.hhot = hh; wp.huv = hu; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
@@ -2134,7 +2165,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));
-  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(hh); (void)hipFree(hu); (void)hipFree(q);
+  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(rx); (void)hipFree(hh); (void)hipFree(hu); (void)hipFree(q);
   return IZPI_OK;
 }
 
