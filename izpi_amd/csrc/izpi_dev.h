@@ -58,6 +58,7 @@ struct alignas(16) GLight {
   double v0[3], v1[3], v2[3], e1[3], e2[3], n[3];  // triangle
   double area;
   double c0[3], c1[3], radius, t0, t1;             // sphere
+  double cz[3];                                    // sphere: center(0), the PDFValue ray's time
   uint32_t kind, index;
 };
 
@@ -293,11 +294,11 @@ IZPI_DEV V3 sph_center(const double* a, double time) {
   return add(c0, smul(sub(c1, c0), ((time - a[7]) / (a[8] - a[7]))));
 }
 // Sphere.Hit acceptance (sphere.go:63-95): root 0 or 1; strict bounds.
-IZPI_DEV bool sph_intersect(const double* a, V3 o, V3 d, double time, double tmin, double tmax, double& t, int& root) {
-  V3 oc = sub(o, sph_center(a, time));
+IZPI_DEV bool sph_intersect_at(V3 center, double radius, V3 o, V3 d, double tmin, double tmax, double& t, int& root) {
+  V3 oc = sub(o, center);
   double aa = dot(d, d);
   double b = dot(oc, d);
-  double c = dot(oc, oc) - (a[6] * a[6]);
+  double c = dot(oc, oc) - (radius * radius);
   double disc = (b * b) - (aa * c);
   if (disc > 0) {
     double temp = (-b - gm::sqrt(b * b - aa * c)) / aa;
@@ -306,6 +307,9 @@ IZPI_DEV bool sph_intersect(const double* a, V3 o, V3 d, double time, double tmi
     if (temp < tmax && temp > tmin) { t = temp; root = 1; return true; }
   }
   return false;
+}
+IZPI_DEV bool sph_intersect(const double* a, V3 o, V3 d, double time, double tmin, double tmax, double& t, int& root) {
+  return sph_intersect_at(sph_center(a, time), a[6], o, d, tmin, tmax, t, root);
 }
 
 }  // namespace izd
