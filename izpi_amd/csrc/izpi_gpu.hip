@@ -666,9 +666,8 @@ IZPI_DEV double lights_pdf(const DevScene& sc, V3 o, V3 v, uint32_t& c_lt, uint3
       }
     } else {
       c_ls++;
-      const double a[9] = {L.c0[0], L.c0[1], L.c0[2], L.c1[0], L.c1[1], L.c1[2], L.radius, L.t0, L.t1};
       double t; int root;
-      if (sph_intersect(a, o, v, 0.0, 0.001, 1.7976931348623157e308, t, root)) {
+      if (sph_intersect_at(ld3(L.cz), L.radius, o, v, 0.001, 1.7976931348623157e308, t, root)) {
         double cosThetaMax = gm::sqrt(1 - L.radius * L.radius / sqlen(sub(ld3(L.c0), o)));
         double solidAngle = 6.283185307179586 * (1 - cosThetaMax);
         pdf = 1 / solidAngle;
@@ -1972,6 +1971,10 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       if (idx >= ns) { ctx->err = "light sphere out of range"; return IZPI_ERR_INVALID; }
       memcpy(L.c0, d->sph_center0 + 3 * (size_t)idx, 24); memcpy(L.c1, d->sph_center1 + 3 * (size_t)idx, 24);
       L.radius = d->sph_radius[idx]; L.t0 = d->sph_time[2 * (size_t)idx]; L.t1 = d->sph_time[2 * (size_t)idx + 1];
+      // Sphere.center(0) (sphere.go:125-127) with the device's operation order:
+      // c0 + (c1 - c0) * ((0 - t0) / (t1 - t0)), computed once here
+      const double k = (0.0 - L.t0) / (L.t1 - L.t0);
+      for (int q = 0; q < 3; q++) L.cz[q] = L.c0[q] + (L.c1[q] - L.c0[q]) * k;
     }
   }
   // ---- material flags: bit0 a texture of the material reads (u,v); bit1 usable by
