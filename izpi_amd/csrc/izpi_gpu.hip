@@ -764,9 +764,17 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t depth, bo
 
 // Write the finished path's radiance after unwinding the recursion of
 // colour.go:80-94 / sampler/spectral.go:161-174 from depth-1 down to 0.
-template <int SAMPLER>
+template <int SAMPLER, bool NO_SPEC = false>
 IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L) {
   const size_t Ls = sp.slots;
+  if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
+    // +0 radiance through only non-specular records: every level computes
+    // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
+    // so the result is +0 without reading the records
+    double* out = sp.out + (size_t)P.unit * 3;
+    out[0] = 0.0; out[1] = 0.0; out[2] = 0.0;
+    return;
+  }
   for (int dd = (int)P.depth - 1; dd >= 0; dd--) {
     const double* r = sp.recs + (size_t)dd * 6 * Ls + slot;
     const bool spec = r[0] != 0.0;
@@ -1210,7 +1218,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       }
       if (!push) {
         if (terminal) {
-          finish<SAMPLER>(sp, slot, P, L);
+          finish<SAMPLER, MATSET == MATSET_BASIC>(sp, slot, P, L);
           done = true;
         } else {
           if (have_pdf) {

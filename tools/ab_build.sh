@@ -1,0 +1,11 @@
+#!/bin/bash
+# Build A/B variants of libizpi_gpu.so into izpi_amd/_lib/variants/:
+#   A = HEAD (git stash of the working tree), B = working tree. Leaves the tree as it was.
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p izpi_amd/_lib/variants
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -shared"
+$H -o izpi_amd/_lib/variants/B.so izpi_amd/csrc/izpi_gpu.hip izpi_amd/csrc/host_scene.cpp
+git stash -q
+trap 'git stash pop -q' EXIT
+$H -o izpi_amd/_lib/variants/A.so izpi_amd/csrc/izpi_gpu.hip izpi_amd/csrc/host_scene.cpp
