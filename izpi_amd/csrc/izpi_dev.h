@@ -308,6 +308,19 @@ IZPI_DEV bool sph_intersect_at(V3 center, double radius, V3 o, V3 d, double tmin
   }
   return false;
 }
+// The two candidate roots of sph_intersect_at, computed without tMax/tMin (the acceptance
+// `temp < tMax && temp > tMin`, root 0 first, is applied by the caller).
+IZPI_DEV bool sph_roots(V3 center, double radius, V3 o, V3 d, double& t0, double& t1) {
+  V3 oc = sub(o, center);
+  double aa = dot(d, d);
+  double b = dot(oc, d);
+  double c = dot(oc, oc) - (radius * radius);
+  double disc = (b * b) - (aa * c);
+  if (!(disc > 0)) return false;
+  t0 = (-b - gm::sqrt(b * b - aa * c)) / aa;
+  t1 = (-b + gm::sqrt(b * b - aa * c)) / aa;
+  return true;
+}
 IZPI_DEV bool sph_intersect(const double* a, V3 o, V3 d, double time, double tmin, double tmax, double& t, int& root) {
   return sph_intersect_at(sph_center(a, time), a[6], o, d, tmin, tmax, t, root);
 }

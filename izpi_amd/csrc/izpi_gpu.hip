@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     bool leaf_next = false; // the step went straight into a leaf whose re-test is known to pass
     int32_t next = -1;
     if (n_prim * prim_w >= n_node * 16u) {
-      if constexpr (DIST) {  // the host picks DIST only for triangle-only scenes
+      if constexpr (DIST) {
         // ---- distributed primitive step: every pending test of the PRIM lanes' leaves
         // (up to 64) runs on its own lane, then each owner accepts its leaf's results in
         // primitive order against its running tMax (bvh4.go:123-134, triangle.go:219)
@@ -434,25 +434,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
           const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
           double t = 0, u = 0, v = 0;
-          const bool ok = tri_intersect_no_tmax(pa, mk(r0.x, r0.y, r1.x), mk(r1.y, r2.x, r2.y), r3.x, t, u, v);
+          const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
+          uint32_t flags;
+          if ((uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE) {
+            flags = tri_intersect_no_tmax(pa, o, d, r3.x, t, u, v) ? 1u : 0u;
+          } else {
+            // sphere: both roots now, their tMin tests as flags; tMax is applied in order
+            // by the owner (sphere.go:72-92: root 0 if tMin < t0 < tMax, else root 1)
+            const double time = wp.raux[oslot].time;
+            flags = 2u;
+            if (sph_roots(sph_center(pa, time), pa[6], o, d, t, u))
+              flags |= 1u | (t > r3.x ? 4u : 0u) | (u > r3.x ? 8u : 0u);
+          }
           dist_t[wbase + lane] = t; dist_u[wbase + lane] = u; dist_v[wbase + lane] = v;
-          dist_owner[wbase + lane] = ok ? 1u : 0u;
+          dist_owner[wbase + lane] = flags;
         }
+        const uint32_t n_sph_tests = (uint32_t)__popcll(__ballot(lane < total && (dist_owner[wbase + lane] & 2u)));
         __builtin_amdgcn_wave_barrier();
         if (served) {
           int32_t acc = -1;
+          double acc_u = 0, acc_v = 0;
           for (uint32_t i = 0; i < cnt; i++) {
             const uint32_t j = wbase + base + i;
-            const double t = dist_t[j];
-            if (dist_owner[j] && !(t > tmax)) { tmax = t; acc = (int32_t)j; bprim = pk + (int32_t)i; }
+            const uint32_t f = dist_owner[j];
+            if (!(f & 1u)) continue;
+            if (!(f & 2u)) {  // triangle: reject only `t > tMax` (triangle.go:219)
+              const double t = dist_t[j];
+              if (!(t > tmax)) { tmax = t; acc = (int32_t)j; acc_u = dist_u[j]; acc_v = dist_v[j]; bprim = pk + (int32_t)i; }
+            } else {  // sphere: strict bounds, root 0 first
+              const double ta = dist_t[j], tb = dist_u[j];
+              if (ta < tmax && (f & 4u)) { tmax = ta; acc = (int32_t)j; acc_u = 0.0; acc_v = 0.0; bprim = pk + (int32_t)i; }
+              else if (tb < tmax && (f & 8u)) { tmax = tb; acc = (int32_t)j; acc_u = 1.0; acc_v = 0.0; bprim = pk + (int32_t)i; }
+            }
           }
-          if (acc >= 0) { wp.huv[slot] = HitUV{dist_u[acc], dist_v[acc]}; clean_from = sp; }
+          if (acc >= 0) { wp.huv[slot] = HitUV{acc_u, acc_v}; clean_from = sp; }
           pk = pend;
           in_prim = false;
           advance = true;
         }
         __builtin_amdgcn_wave_barrier();
-        c_tri += total;
+        c_tri += total - n_sph_tests;
+        c_sph += n_sph_tests;
         c_pstep++;
       } else {
       // ---- primitive step: one Hit() per PRIM lane (bvh4.go:123-134)
@@ -1567,7 +1589,6 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   if (const char* e = getenv("IZPI_TRACE_RING")) t->ring = atoi(e);
   if (const char* e = getenv("IZPI_TRACE_WPE")) t->wpe = atoi(e);
   if (const char* e = getenv("IZPI_TRACE_DIST")) t->p2 = atoi(e) != 0;
-  if (!ctx->sc.tri_only) t->p2 = false;  // sphere tests depend on tMax before the end (sphere.go:72-92)
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
