@@ -762,6 +762,7 @@ struct ShadeParams {
   uint32_t width, height, max_depth;
   uint32_t chunk_spp, s0, tile_w, tile_h, total_units;
   uint32_t num_bg_spd, slots;
+  uint32_t rec_depth;          // records per slot (max(1, max_depth))
   const uint32_t* tiles;
   const double* bg_wl;
   const double* bg_val;
@@ -774,21 +775,31 @@ struct ShadeParams {
   uint32_t* error;
 };
 
+// Unwinding records, one per bounce, laid out [slot][depth] so that a finishing path
+// reads its records as one contiguous run (48 B per level for Colour: flag, att xyz, s, p;
+// 32 B for Spectral: flag, att, s, p). A [depth][field][slot] layout made every field
+// of every level a separate scattered 64-B sector read (measured: 44% of C5 shading).
+template <int SAMPLER>
+struct RecLayout {
+  static constexpr uint32_t D = SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 4;  // doubles per record
+  static constexpr uint32_t S = D - 2;                                   // index of s (p follows)
+};
+template <int SAMPLER>
+IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t slot, uint32_t depth) {
+  return sp.recs + ((size_t)slot * sp.rec_depth + depth) * RecLayout<SAMPLER>::D;
+}
 template <int SAMPLER>
 IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t depth, bool spec, V3 att, double s, double p) {
-  double* r = sp.recs + (size_t)depth * 6 * sp.slots + slot;
-  const size_t L = sp.slots;
-  r[0] = spec ? 1.0 : 0.0;
-  r[L] = att.x;
-  if (SAMPLER == IZPI_SAMPLER_COLOUR) { r[2 * L] = att.y; r[3 * L] = att.z; }
-  if (!spec) { r[4 * L] = s; r[5 * L] = p; }
+  double2* r = reinterpret_cast<double2*>(rec_ptr<SAMPLER>(sp, slot, depth));
+  r[0] = make_double2(spec ? 1.0 : 0.0, att.x);
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) r[1] = make_double2(att.y, att.z);
+  if (!spec) r[RecLayout<SAMPLER>::S / 2] = make_double2(s, p);
 }
 
 // Write the finished path's radiance after unwinding the recursion of
 // colour.go:80-94 / sampler/spectral.go:161-174 from depth-1 down to 0.
 template <int SAMPLER, bool NO_SPEC = false>
 IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L) {
-  const size_t Ls = sp.slots;
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
     // +0 radiance through only non-specular records: every level computes
     // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
@@ -798,25 +809,25 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
     return;
   }
   for (int dd = (int)P.depth - 1; dd >= 0; dd--) {
-    const double* r = sp.recs + (size_t)dd * 6 * Ls + slot;
+    const double* r = rec_ptr<SAMPLER>(sp, slot, (uint32_t)dd);
     const bool spec = r[0] != 0.0;
     if (SAMPLER == IZPI_SAMPLER_COLOUR) {
-      V3 att = mk(r[Ls], r[2 * Ls], r[3 * Ls]);
+      V3 att = mk(r[1], r[2], r[3]);
       if (spec) {
         L = mul(att, L);                                   // vec3.Mul(att, Sample(...))
       } else {
-        const double s = r[4 * Ls], p = r[5 * Ls];
+        const double s = r[4], p = r[5];
         V3 v1 = smul(L, s);                                // ScalarMul(Sample(...), ScatteringPDF)
         V3 v2 = mul(att, v1);
         V3 v3 = sdiv(v2, p);
         L = mk(0.0 + v3.x, 0.0 + v3.y, 0.0 + v3.z);        // Add(emitted == 0, v3)
       }
     } else {
-      const double att = r[Ls];
+      const double att = r[1];
       if (spec) {
         L.x = att * L.x;
       } else {
-        const double s = r[4 * Ls], p = r[5 * Ls];
+        const double s = r[2], p = r[3];
         double v1 = L.x * s;
         double v2 = att * v1;
         double v3 = v2 / p;
@@ -1257,7 +1268,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
             if (sc_cos < 0) sc_cos = 0;
             rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, 0);
             const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
-            sp.recs[((size_t)P.depth * 6 + 5) * sp.slots + slot] = pdf_val;
+            rec_ptr<SAMPLER>(sp, slot, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
             next_d = dir;
           } else {
             rec_store<SAMPLER>(sp, slot, P.depth, true, att, 0, 0);
@@ -1799,6 +1810,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.tile_w = tw; sp.tile_h = th; sp.num_bg_spd = (uint32_t)nbg; sp.slots = slots;
   sp.tiles = ctx->d_tiles; sp.bg_wl = ctx->d_bg; sp.bg_val = ctx->d_bg + nbg;
   sp.background[0] = req->background[0]; sp.background[1] = req->background[1]; sp.background[2] = req->background[2];
+  sp.rec_depth = depth_cap;
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.head = ctx->d_misc;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
   WaveParams wp{};

@@ -4,7 +4,7 @@
 CFG=${1:-C3}; SPP=${2:-256}; R=${3:-2}
 cp izpi_amd/_lib/libizpi_gpu.so /tmp/keep.so
 for r in $(seq 1 $R); do
-  for v in A B; do
+  for v in ${VARIANTS:-A B}; do
     cp izpi_amd/_lib/variants/$v.so izpi_amd/_lib/libizpi_gpu.so
     timeout -k 10 300 python tools/tune.py --config $CFG --spp $SPP --rounds 1 2>&1 | grep round | sed "s/^/$v /" || exit 1
   done
