@@ -1050,14 +1050,16 @@ __global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadePa
 
 // Partial stores of the per-slot records: only the fields a pass changes are written,
 // so k_shade does not keep the untouched ones (ray time, wavelength, ...) in registers.
+// `aux`: also store kind/pad. Only MATSET_FULL turns a slot's ray into a path-length ray
+// and back, so the other variants leave the aux record as the path start wrote it.
 IZPI_DEV void store_ray(const WaveParams& wp, uint32_t slot, V3 o, V3 d, double tmin, double tmax, uint32_t kind,
-                        uint32_t pad) {
+                        uint32_t pad, bool aux = true) {
   double2* p = reinterpret_cast<double2*>(wp.rhot + slot);
   p[0] = make_double2(o.x, o.y);
   p[1] = make_double2(o.z, d.x);
   p[2] = make_double2(d.y, d.z);
   p[3] = make_double2(tmin, tmax);
-  *reinterpret_cast<uint2*>(&wp.raux[slot].kind) = make_uint2(kind, pad);  // the ray time is left as is
+  if (aux) *reinterpret_cast<uint2*>(&wp.raux[slot].kind) = make_uint2(kind, pad);  // the ray time is left as is
 }
 IZPI_DEV void store_path_rng_depth(PathHot* ps, uint32_t rng, uint32_t depth) {
   *reinterpret_cast<uint2*>(&ps->rng) = make_uint2(rng, depth);
@@ -1280,7 +1282,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
             done = true;
           } else {
             store_path_rng_depth(wp.phot + slot, P.rng, P.depth);
-            store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0);
+            store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0, MATSET == MATSET_FULL);
             push = true;
           }
         }
