@@ -317,3 +317,26 @@ def test_render_spectral_rgb_bitwise(gpu):
     want = O.xyz_to_rgb(O.firefly(ref.reshape(-1), 48, 48), 48, 48, r.exposure).reshape(48, 48, 4)
     assert_parity(img, want)
     r.close()
+
+
+@pytest.mark.parametrize("name", ["C2", "C4", "C5"])
+def test_full_size_frames_one_spp_bitwise(gpu, name):
+    """BASELINE.json's other configurations at their full image sizes (1 spp): the
+    Cornell box (C2), the PBR box with image textures and normal maps (C4) and the
+    spectral glass scene with dielectric spheres and path-length rays (C5, including
+    FireflyRejection + XYZToRGB). Every pixel bit-identical, counters equal."""
+    cfg = configs.configs()[name]
+    scene = cfg.build()
+    r = GPURenderer(scene, cfg.width, cfg.height, 1, sampler=cfg.sampler)
+    if cfg.sampler == N.SAMPLER_SPECTRAL:
+        img = r.render_spectral_rgb()
+        stats = r.stats
+        ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, 1, cfg.sampler)
+        ref = O.xyz_to_rgb(O.firefly(ref.reshape(-1), cfg.width, cfg.height), cfg.width, cfg.height,
+                           r.exposure).reshape(cfg.height, cfg.width, 4)
+    else:
+        img = r.render()
+        stats = r.stats
+        ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, 1, cfg.sampler)
+    assert_parity(img, ref, stats, ostats)
+    r.close()
