@@ -48,7 +48,8 @@ __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
 
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
 
-enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT, CNT_N };
+enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
+       CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_N };  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 
 // ======================================================= textures / spectra
@@ -337,9 +338,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   __shared__ int32_t lds_stack[S * 256];
   // DIST: one wave-wide batch of leaf tests (primitive, owner lane, result)
-  __shared__ int32_t dist_prim[DIST ? 256 : 1];
-  __shared__ uint32_t dist_owner[DIST ? 256 : 1];
-  __shared__ double dist_t[DIST ? 256 : 1], dist_u[DIST ? 256 : 1], dist_v[DIST ? 256 : 1];
+  // (+4: an owner reads its four entries unconditionally, past the wave's last batch entry)
+  __shared__ int32_t dist_prim[DIST ? 260 : 1];
+  __shared__ uint32_t dist_owner[DIST ? 260 : 1];
+  __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST ? 260 : 1], dist_v[DIST ? 260 : 1];
   const uint32_t wbase = threadIdx.x & ~63u;
   int32_t* stk = lds_stack + threadIdx.x;
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
@@ -358,7 +360,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
   uint32_t c_pos = 0, c_end = 0;  // wave-private range [c_pos, c_end) of the input queue
+#ifdef IZPI_TRACE_CLOCKS
+  uint64_t k_refill = 0, k_node = 0, k_prim = 0, k_adv = 0, k0 = 0, k1 = 0;
+#define IZPI_CLK(v) (v) = __builtin_readcyclecounter()
+#else
+#define IZPI_CLK(v) (void)0
+#endif
   for (;;) {
+    IZPI_CLK(k0);
     const uint64_t idle = __ballot(!busy);
     if (idle != 0) {
       const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -408,6 +417,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     bool advance = false;   // lane finished its current node / leaf: take next or pop
     bool leaf_next = false; // the step went straight into a leaf whose re-test is known to pass
     int32_t next = -1;
+#ifdef IZPI_TRACE_CLOCKS
+    IZPI_CLK(k1); k_refill += k1 - k0; k0 = k1;
+    const bool clk_prim = n_prim * prim_w >= n_node * 16u;
+#endif
     if (n_prim * prim_w >= n_node * 16u) {
       if constexpr (DIST) {
         // ---- distributed primitive step: every pending test of the PRIM lanes' leaves
@@ -451,7 +464,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
         const uint32_t n_sph_tests = (uint32_t)__popcll(__ballot(lane < total && (dist_owner[wbase + lane] & 2u)));
         __builtin_amdgcn_wave_barrier();
-        if (served) {
+        if (served && n_sph_tests == 0) {
+          // triangles only: the leaf's flags and distances come in one LDS round trip, the
+          // ordered accept runs in registers, and only the accepted (u, v) is read back
+          const uint32_t j0 = wbase + base;
+          uint32_t f[4];
+          double tt[4];
+#pragma unroll
+          for (uint32_t i = 0; i < 4; i++) { f[i] = dist_owner[j0 + i]; tt[i] = dist_t[j0 + i]; }
+          int32_t acc = -1;
+#pragma unroll
+          for (uint32_t i = 0; i < 4; i++)  // reject only `t > tMax` (triangle.go:219), in primitive order
+            if (i < cnt && (f[i] & 1u) && !(tt[i] > tmax)) { tmax = tt[i]; acc = (int32_t)i; }
+          if (acc >= 0) {
+            wp.huv[slot] = HitUV{dist_u[j0 + acc], dist_v[j0 + acc]};
+            bprim = pk + acc;
+            clean_from = sp;
+          }
+          pk = pend;
+          in_prim = false;
+          advance = true;
+        } else if (served) {
           int32_t acc = -1;
           double acc_u = 0, acc_v = 0;
           for (uint32_t i = 0; i < cnt; i++) {
@@ -576,6 +609,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
     }
+#ifdef IZPI_TRACE_CLOCKS
+    IZPI_CLK(k1); if (clk_prim) k_prim += k1 - k0; else k_node += k1 - k0; k0 = k1;
+#endif
     if (advance) {
       if (next != -1) {
         cur = next;
@@ -599,7 +635,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     const uint64_t n_short = (uint64_t)__popcll(__ballot(leaf_next));  // leaf visits taken by a shortcut
     c_nodes += n_short;
     c_short += n_short;
+#ifdef IZPI_TRACE_CLOCKS
+    IZPI_CLK(k1); k_adv += k1 - k0;
+#endif
   }
+#ifdef IZPI_TRACE_CLOCKS
+  if (lane == 0) {
+    atomicAdd(counters + CNT_CLK_REFILL, (unsigned long long)k_refill);
+    atomicAdd(counters + CNT_CLK_NODE, (unsigned long long)k_node);
+    atomicAdd(counters + CNT_CLK_PRIM, (unsigned long long)k_prim);
+    atomicAdd(counters + CNT_CLK_ADV, (unsigned long long)k_adv);
+  }
+#endif
   if (lane == 0) {
     if (c_rays) atomicAdd(counters + CNT_RAYS, (unsigned long long)c_rays);
     if (c_nodes) atomicAdd(counters + CNT_NODES, (unsigned long long)c_nodes);
@@ -1856,6 +1903,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.samples = (uint64_t)num_pixels * req->spp;
   s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches;
   s.node_steps = cnt[CNT_NSTEP]; s.prim_steps = cnt[CNT_PSTEP]; s.leaf_shortcuts = cnt[CNT_SHORT];
+#ifdef IZPI_TRACE_CLOCKS
+  fprintf(stderr, "IZPI_TRACE_CLOCKS refill %llu node %llu prim %llu advance %llu (wave cycles)\n", cnt[CNT_CLK_REFILL],
+          cnt[CNT_CLK_NODE], cnt[CNT_CLK_PRIM], cnt[CNT_CLK_ADV]);
+#endif
   if (misc[1]) {
     ctx->err = misc[1] & 1u ? "device guard: traversal stack overflow" : "device guard: unknown material kind";
     return IZPI_ERR_DEVICE;
