@@ -406,6 +406,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
         }
         c_rays += (uint64_t)__popcll(__ballot(main_ray));
+        // drain the new rays' loads here: left pending they make the compiler wait for
+        // vmcnt(0) at the loop head, i.e. for every hit-record store, on every iteration
+        __builtin_amdgcn_s_waitcnt(0x0F70);
       } else if (exhausted && idle == ~0ull) {
         break;
       }
@@ -617,8 +620,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         cur = next;
       } else if (sp > 0) {  // pop (bvh4.go:150-160)
         sp--;
-        if (sp < low) { cur = gsp[(size_t)sp * spill_stride]; low = sp; }
-        else cur = stk[(sp & (S - 1)) * 256];
+        // the LDS read is unconditional so that the compiler keeps it a ds_read: a select
+        // of the two addresses becomes a flat load, whose wait also drains every store
+        int32_t top = *(volatile __attribute__((address_space(3))) int32_t*)&lds_stack[threadIdx.x + (sp & (S - 1)) * 256];
+        if (sp < low) {
+          top = gsp[(size_t)sp * spill_stride];
+          low = sp;
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, not at the join for every pop
+        }
+        cur = top;
         // An entry pushed after the last accepted hit meets the same tMax it was pushed
         // with, so a leaf's re-test against its (identical) box passes: skip the load.
         if (ref_is_leaf(cur) && sp >= clean_from && sc.leaf_shortcut) {
