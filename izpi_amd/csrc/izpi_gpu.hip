@@ -342,6 +342,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   __shared__ int32_t dist_prim[DIST ? 260 : 1];
   __shared__ uint32_t dist_owner[DIST ? 260 : 1];
   __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST ? 260 : 1], dist_v[DIST ? 260 : 1];
+  // (u, v) of the lane's accepted hit so far: HitUV is stored once, when the ray finishes
+  // (a global store per accepted hit would hold up the wave's next load wait, since
+  // vmcnt counts stores and loads in one queue)
+  __shared__ double2 lds_uv[256];
   const uint32_t wbase = threadIdx.x & ~63u;
   int32_t* stk = lds_stack + threadIdx.x;
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
@@ -480,7 +484,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           for (uint32_t i = 0; i < 4; i++)  // reject only `t > tMax` (triangle.go:219), in primitive order
             if (i < cnt && (f[i] & 1u) && !(tt[i] > tmax)) { tmax = tt[i]; acc = (int32_t)i; }
           if (acc >= 0) {
-            wp.huv[slot] = HitUV{dist_u[j0 + acc], dist_v[j0 + acc]};
+            lds_uv[threadIdx.x] = make_double2(dist_u[j0 + acc], dist_v[j0 + acc]);
             bprim = pk + acc;
             clean_from = sp;
           }
@@ -503,7 +507,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
               else if (tb < tmax && (f & 8u)) { tmax = tb; acc = (int32_t)j; acc_u = 1.0; acc_v = 0.0; bprim = pk + (int32_t)i; }
             }
           }
-          if (acc >= 0) { wp.huv[slot] = HitUV{acc_u, acc_v}; clean_from = sp; }
+          if (acc >= 0) { lds_uv[threadIdx.x] = make_double2(acc_u, acc_v); clean_from = sp; }
           pk = pend;
           in_prim = false;
           advance = true;
@@ -529,14 +533,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         is_tri = (uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE;
         if (is_tri) {
           double t, u, v;
-          if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics go straight to the hit record
-            tmax = t; bprim = pk; wp.huv[slot] = HitUV{u, v}; clean_from = sp;
+          if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics wait in LDS (lds_uv)
+            tmax = t; bprim = pk; lds_uv[threadIdx.x] = make_double2(u, v); clean_from = sp;
           }
         } else {
           const double time = wp.raux[slot].time;  // only spheres read the ray time
           double t; int root;
           if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
-            tmax = t; bprim = pk; wp.huv[slot] = HitUV{(double)root, 0.0}; clean_from = sp;
+            tmax = t; bprim = pk; lds_uv[threadIdx.x] = make_double2((double)root, 0.0); clean_from = sp;
           }
         }
         pk++;
@@ -638,7 +642,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (sp < clean_from) clean_from = sp;
       } else {
         wp.hhot[slot] = HitHot{bprim >= 0 ? tmax : 0.0, bprim, 0u};
-        if (bprim < 0) wp.huv[slot] = HitUV{0.0, 0.0};
+        const double2 uv = bprim >= 0 ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
+        wp.huv[slot] = HitUV{uv.x, uv.y};
         busy = false;
       }
     }
