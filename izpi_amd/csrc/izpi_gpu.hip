@@ -556,6 +556,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       c_nstep++;
       // ---- node step: visit `cur` (bvh4.go:87-146)
       const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
+      if (__ballot(busy && !in_prim && sp + 3 - low > S) != 0) {
+        // ring too full for this step's three writes: spill the oldest entries (rare)
+        if (busy && !in_prim) {
+          while (sp + 3 - low > S) {
+            gsp[(size_t)low * spill_stride] = stk[(low & (S - 1)) * 256];
+            low++;
+          }
+        }
+      }
       if (busy && !in_prim) {
         const float tm = (float)tmax;
         if (ref_is_leaf(cur)) {
@@ -583,35 +592,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
               if (slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) hm |= 1u << i;
           }
           // slots 0..3 with ChildIndex != -1 whose box is hit (bvh4.go:119-146): the first
-          // is visited next, the others are pushed in slot order (popped LIFO).
+          // is visited next, the others are pushed in slot order (popped LIFO). Selects
+          // instead of branches: each divergent branch costs exec-mask and lane-mask
+          // bookkeeping on the scalar unit, which is as busy as the vector unit here.
           const uint32_t m = hm & ((ch.x != -1 ? 1u : 0u) | (ch.y != -1 ? 2u : 0u) | (ch.z != -1 ? 4u : 0u) |
                                    (ch.w != -1 ? 8u : 0u));
-          const uint32_t f = m & 1u ? 0u : (m & 2u ? 1u : (m & 4u ? 2u : 3u));
-          next = m == 0 ? -1 : (f == 0 ? ch.x : (f == 1 ? ch.y : (f == 2 ? ch.z : ch.w)));
+          const int32_t c01 = (m & 1u) ? ch.x : ch.y, c23 = (m & 4u) ? ch.z : ch.w;
+          next = m == 0 ? -1 : ((m & 3u) ? c01 : c23);
           // A leaf visited straight after its parent re-tests the same f32 box with the
           // same tMax (A10): the result is known to be a hit, so skip its node load and
           // start on its primitives (the visit is still counted).
-          if (ref_is_leaf(next) && sc.leaf_shortcut) {
-            in_prim = true; pk = leaf_start(next); pend = pk + leaf_count(next);
-            next = -1;
-            leaf_next = true;
-          }
+          leaf_next = ref_is_leaf(next) && sc.leaf_shortcut;
+          in_prim = leaf_next;
+          pk = leaf_next ? leaf_start(next) : pk;
+          pend = leaf_next ? leaf_start(next) + leaf_count(next) : pend;
+          next = leaf_next ? -1 : next;
+          // the other hit children, compacted in slot order, are written unconditionally to
+          // ring positions sp..sp+2 (the ring keeps 3 free entries above sp); sp moves by
+          // their count
           const uint32_t rest = m & (m - 1u);  // bits 1..3 only
           const int np_ = __builtin_popcount(rest);
-          if (np_ > 0) {
-            if (sp + np_ > 64) {
-              atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
-            } else {
-              while (sp + np_ - low > S) {  // ring full: spill the oldest entries (rare)
-                gsp[(size_t)low * spill_stride] = stk[(low & (S - 1)) * 256];
-                low++;
-              }
-              if (rest & 2u) stk[(sp & (S - 1)) * 256] = ch.y;
-              if (rest & 4u) stk[((sp + ((rest & 2u) ? 1 : 0)) & (S - 1)) * 256] = ch.z;
-              if (rest & 8u) stk[((sp + np_ - 1) & (S - 1)) * 256] = ch.w;
-              sp += np_;
-            }
-          }
+          const int32_t e0 = (rest & 2u) ? ch.y : ((rest & 4u) ? ch.z : ch.w);
+          const int32_t e1 = ((rest & 6u) == 6u) ? ch.z : ch.w;
+          stk[(sp & (S - 1)) * 256] = e0;
+          stk[((sp + 1) & (S - 1)) * 256] = e1;
+          stk[((sp + 2) & (S - 1)) * 256] = ch.w;
+          if (sp + np_ > 64) atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
+          sp += np_;
           advance = !leaf_next;
         }
       }
@@ -619,28 +626,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #ifdef IZPI_TRACE_CLOCKS
     IZPI_CLK(k1); if (clk_prim) k_prim += k1 - k0; else k_node += k1 - k0; k0 = k1;
 #endif
-    if (advance) {
-      if (next != -1) {
-        cur = next;
-      } else if (sp > 0) {  // pop (bvh4.go:150-160)
-        sp--;
-        // the LDS read is unconditional so that the compiler keeps it a ds_read: a select
-        // of the two addresses becomes a flat load, whose wait also drains every store
-        int32_t top = *(volatile __attribute__((address_space(3))) int32_t*)&lds_stack[threadIdx.x + (sp & (S - 1)) * 256];
-        if (sp < low) {
-          top = gsp[(size_t)sp * spill_stride];
-          low = sp;
-          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, not at the join for every pop
+    // ---- advance: next child, else pop (bvh4.go:150-160), else the ray is done
+    {
+      const bool do_pop = advance && next == -1 && sp > 0;
+      const bool do_fin = advance && next == -1 && sp == 0;
+      // the LDS read is unconditional (and volatile, so that the compiler keeps it a ds_read:
+      // a select of the LDS and spill addresses becomes a flat load, whose wait also
+      // drains every store)
+      const int spn = sp - 1;
+      int32_t top = *(volatile __attribute__((address_space(3))) int32_t*)&lds_stack[threadIdx.x + (spn & (S - 1)) * 256];
+      if (__ballot(do_pop && spn < low) != 0) {
+        if (do_pop && spn < low) {
+          top = gsp[(size_t)spn * spill_stride];
+          low = spn;
         }
-        cur = top;
-        // An entry pushed after the last accepted hit meets the same tMax it was pushed
-        // with, so a leaf's re-test against its (identical) box passes: skip the load.
-        if (ref_is_leaf(cur) && sp >= clean_from && sc.leaf_shortcut) {
-          in_prim = true; pk = leaf_start(cur); pend = pk + leaf_count(cur);
-          leaf_next = true;
-        }
-        if (sp < clean_from) clean_from = sp;
-      } else {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, not for every pop
+      }
+      cur = (advance && next != -1) ? next : (do_pop ? top : cur);
+      sp = do_pop ? spn : sp;
+      // An entry pushed after the last accepted hit meets the same tMax it was pushed
+      // with, so a leaf's re-test against its (identical) box passes: skip the load.
+      const bool lf = do_pop && ref_is_leaf(top) && spn >= clean_from && sc.leaf_shortcut;
+      in_prim = in_prim || lf;
+      leaf_next = leaf_next || lf;
+      pk = lf ? leaf_start(top) : pk;
+      pend = lf ? leaf_start(top) + leaf_count(top) : pend;
+      clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
+      if (do_fin) {
         wp.hhot[slot] = HitHot{bprim >= 0 ? tmax : 0.0, bprim, 0u};
         const double2 uv = bprim >= 0 ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
         wp.huv[slot] = HitUV{uv.x, uv.y};
