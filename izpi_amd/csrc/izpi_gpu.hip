@@ -331,15 +331,16 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
 // ring full, the oldest entry is spilled to a per-thread global area (entry e at
 // spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
 // are kept per wave in SGPRs (popcounts of ballots).
-template <int S, int WPE, bool DIST>
+// TRI: the scene holds no spheres (DevScene::tri_only), so the sphere code is compiled out.
+template <int S, int WPE, bool DIST, bool TRI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   __shared__ int32_t lds_stack[S * 256];
-  // DIST: one wave-wide batch of leaf tests (primitive, owner lane, result)
+  // DIST: one wave-wide batch of leaf tests: (primitive << 6 | owner lane), then the
+  // test's result flags in the same word; distances and barycentrics
   // (+4: an owner reads its four entries unconditionally, past the wave's last batch entry)
-  __shared__ int32_t dist_prim[DIST ? 260 : 1];
   __shared__ uint32_t dist_owner[DIST ? 260 : 1];
   __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST ? 260 : 1], dist_v[DIST ? 260 : 1];
   // (u, v) of the lane's accepted hit so far: HitUV is stored once, when the ray finishes
@@ -441,13 +442,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const uint64_t ms = __ballot(served);
         const int last = 63 - __clzll((long long)ms);
         const uint32_t total = (uint32_t)__shfl((int)(base + cnt), last);
-        if (served)
-          for (uint32_t i = 0; i < cnt; i++) { dist_prim[wbase + base + i] = pk + (int32_t)i; dist_owner[wbase + base + i] = lane; }
+        {  // a leaf has 1..4 primitives (bvh4.go:638): four predicated writes, no loop
+          const uint32_t e = ((uint32_t)pk << 6) | lane;
+          uint32_t* dq = dist_owner + wbase + base;
+          if (served) dq[0] = e;
+          if (served && cnt > 1) dq[1] = e + 64u;
+          if (served && cnt > 2) dq[2] = e + 128u;
+          if (served && cnt > 3) dq[3] = e + 192u;
+        }
         __builtin_amdgcn_wave_barrier();
-        const uint32_t ow = lane < total ? dist_owner[wbase + lane] : lane;
+        const uint32_t ent = lane < total ? dist_owner[wbase + lane] : lane;
+        const uint32_t ow = ent & 63u;
         const uint32_t oslot = (uint32_t)__shfl((int)slot, (int)ow);
         if (lane < total) {
-          const int32_t pi = dist_prim[wbase + lane];
+          const int32_t pi = (int32_t)(ent >> 6);
           const double2* rp = reinterpret_cast<const double2*>(wp.rhot + oslot);
           const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
           const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
@@ -456,7 +464,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           double t = 0, u = 0, v = 0;
           const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
           uint32_t flags;
-          if ((uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE) {
+          if (TRI || (uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE) {
             flags = tri_intersect_no_tmax(pa, o, d, r3.x, t, u, v) ? 1u : 0u;
           } else {
             // sphere: both roots now, their tMin tests as flags; tMax is applied in order
@@ -469,9 +477,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           dist_t[wbase + lane] = t; dist_u[wbase + lane] = u; dist_v[wbase + lane] = v;
           dist_owner[wbase + lane] = flags;
         }
-        const uint32_t n_sph_tests = (uint32_t)__popcll(__ballot(lane < total && (dist_owner[wbase + lane] & 2u)));
+        const uint32_t n_sph_tests = TRI ? 0u : (uint32_t)__popcll(__ballot(lane < total && (dist_owner[wbase + lane] & 2u)));
         __builtin_amdgcn_wave_barrier();
-        if (served && n_sph_tests == 0) {
+        if (served && (TRI || n_sph_tests == 0)) {
           // triangles only: the leaf's flags and distances come in one LDS round trip, the
           // ordered accept runs in registers, and only the accepted (u, v) is read back
           const uint32_t j0 = wbase + base;
@@ -491,7 +499,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           pk = pend;
           in_prim = false;
           advance = true;
-        } else if (served) {
+        } else if (!TRI && served) {
           int32_t acc = -1;
           double acc_u = 0, acc_v = 0;
           for (uint32_t i = 0; i < cnt; i++) {
@@ -530,13 +538,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const double2* pp = reinterpret_cast<const double2*>(sc.prims + pk);
         const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
         const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
-        is_tri = (uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE;
+        is_tri = TRI || (uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE;
         if (is_tri) {
           double t, u, v;
           if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) {  // barycentrics wait in LDS (lds_uv)
             tmax = t; bprim = pk; lds_uv[threadIdx.x] = make_double2(u, v); clean_from = sp;
           }
-        } else {
+        } else if (!TRI) {
           const double time = wp.raux[slot].time;  // only spheres read the ray time
           double t; int root;
           if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
@@ -1585,6 +1593,7 @@ struct izpi_ctx {
   bool have_scene = false;
   DevScene sc{};
   uint32_t stack_needed = 0;
+  uint32_t num_prims = 0;
   std::vector<void*> scene_allocs;
   // render workspace (grown on demand)
   double* d_samples = nullptr; size_t samples_cap = 0;
@@ -1661,14 +1670,16 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 // All variants give identical results and counters.
 struct Tracer {
   int variant = 2, stack = 32, ring = 16, wpe = 5;
-  bool p2 = true;  // DIST: spread leaf tests over the wave (triangle-only scenes)
+  bool p2 = true;  // DIST: spread leaf tests over the wave
+  bool tri = false;  // sphere code compiled out (scene without spheres)
   uint32_t prim_w = 32, tchunk = 128, refill_min = 16;
   int blocks = 0;
 };
 
 // k_trace2 instances: ring entries x minimum waves per SIMD (register budget).
-#define IZPI_T2_LIST(X) X(8, 4, false) X(8, 5, false) X(16, 4, false) X(16, 5, false) X(32, 4, false) X(16, 4, true) \
-  X(16, 5, true) X(8, 5, true)
+#define IZPI_T2_LIST(X) X(8, 4, false, false) X(8, 5, false, false) X(16, 4, false, false) X(16, 5, false, false) \
+  X(32, 4, false, false) X(16, 4, true, false) X(16, 5, true, false) X(8, 5, true, false) X(16, 5, true, true)   \
+  X(8, 5, true, true) X(16, 5, false, true)
 
 int make_tracer(izpi_ctx* ctx, Tracer* t) {
   *t = Tracer();
@@ -1679,14 +1690,22 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
+  // DIST packs (primitive << 6 | lane) into one LDS word
+  if (ctx->num_prims >= (1u << 26)) t->p2 = false;
+  t->tri = ctx->sc.tri_only != 0 && !getenv("IZPI_TRACE_NO_TRI");
   t->stack = ctx->stack_needed <= 32 ? 32 : 64;
   int rc = IZPI_ERR_INVALID;
   if (t->variant == 1) {
     rc = t->stack == 32 ? resident_blocks(ctx, k_trace<32>, &t->blocks) : resident_blocks(ctx, k_trace<64>, &t->blocks);
     return rc;
   }
-#define IZPI_T2_OCC(R, W, P) if (t->ring == R && t->wpe == W && t->p2 == P) rc = resident_blocks(ctx, k_trace2<R, W, P>, &t->blocks);
+#define IZPI_T2_OCC(R, W, P, T) \
+  if (t->ring == R && t->wpe == W && t->p2 == P && t->tri == T) rc = resident_blocks(ctx, k_trace2<R, W, P, T>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
+  if (rc == IZPI_ERR_INVALID && t->tri) {  // no triangle-only instance for this ring/wpe
+    t->tri = false;
+    IZPI_T2_LIST(IZPI_T2_OCC)
+  }
   if (rc == IZPI_ERR_INVALID && t->p2) {  // no distributed instance for this ring/wpe: sequential leaf tests
     t->p2 = false;
     IZPI_T2_LIST(IZPI_T2_OCC)
@@ -1705,9 +1724,9 @@ void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStrea
     return;
   }
   const uint32_t stride = (uint32_t)t.blocks * 256;
-#define IZPI_T2_LAUNCH(R, W, P)                                                                               \
-  if (t.ring == R && t.wpe == W && t.p2 == P) {                                                              \
-    hipLaunchKernelGGL((k_trace2<R, W, P>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
+#define IZPI_T2_LAUNCH(R, W, P, T)                                                                            \
+  if (t.ring == R && t.wpe == W && t.p2 == P && t.tri == T) {                                                \
+    hipLaunchKernelGGL((k_trace2<R, W, P, T>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
                        stride, t.prim_w, t.tchunk, t.refill_min);                                            \
     return;                                                                                                  \
   }
@@ -2186,6 +2205,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       best[k] = (valid ? valid - 1 : 0) + deepest;
     }
     ctx->stack_needed = d->num_nodes ? best[0] : 0;
+    ctx->num_prims = d->num_prims;
   }
   ctx->have_scene = true;
   return IZPI_OK;
