@@ -352,6 +352,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = *wp.q_in_count;
+  // Small queues (the wavefront's tail passes): chunks shrink so the rays spread over
+  // more waves, and waves past the last chunk exit at once instead of each paying a
+  // dequeue atomic on the one counter word (~88/us chip-wide).
+  const uint32_t nwaves = gridDim.x * 4u;
+  const uint32_t chunk = min(tchunk, max(16u, (n + nwaves - 1u) / nwaves));
+  if ((uint64_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk >= n) return;
   uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
   uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
   bool busy = false, in_prim = false;
@@ -377,14 +383,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     if (idle != 0) {
       const uint32_t nidle = (uint32_t)__popcll(idle);
       if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos >= c_end) {
-        // the wave's private range of the queue is used up: take the next `tchunk`
+        // the wave's private range of the queue is used up: take the next `chunk`
         // entries with one atomic (a single head word saturates near 88 dequeues/us)
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(wp.trace_next, tchunk);
+        if (lane == 0) b = atomicAdd(wp.trace_next, chunk);
         b = __builtin_amdgcn_readfirstlane(b);
         if (b >= n) exhausted = true;
         c_pos = b;
-        c_end = b + tchunk < n ? b + tchunk : n;
+        c_end = b + chunk < n ? b + chunk : n;
       }
       if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos < c_end) {
         const uint32_t take = nidle < c_end - c_pos ? nidle : c_end - c_pos;
@@ -575,60 +581,71 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
       if (busy && !in_prim) {
         const float tm = (float)tmax;
-        if (ref_is_leaf(cur)) {
-          const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_start(cur));
-          const float4 a = lp[0], b = lp[1];  // both loads issued together
-          if (slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
-            in_prim = true; pk = leaf_start(cur); pend = pk + leaf_count(cur);
-          } else {
-            advance = true;
-          }
+        // An inner node (4-slot box test) and a leaf's slot-0 re-test (A10) run as ONE
+        // code path: a leaf lane's 32-B GLeaf box lands in slot 0 (selects below), its
+        // slots 1-3 are invalid. Mixed waves (nearly every node step) then issue one set
+        // of loads and wait once, instead of running the two branches one after the other.
+        const bool is_leaf = ref_is_leaf(cur);
+        const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
+                                                                   : (const void*)(sc.inner + cur));
+        // leaf lanes read their last five loads from the root node (a cached valid address;
+        // the values are not used)
+        const float4* np = is_leaf ? reinterpret_cast<const float4*>(sc.inner) : lp;
+        const float4 q0 = lp[0], q1 = lp[1];
+        const float4 mnz_ = np[2], mxx_ = np[3], mxy_ = np[4], mxz_ = np[5];
+        const int4 ch_ = *reinterpret_cast<const int4*>(np + 6);
+        // GLeaf = (mn.x, mn.y, mn.z, mx.x), (mx.y, mx.z, start, count)
+        const float4 mnx = q0;
+        const float4 mny = make_float4(is_leaf ? q0.y : q1.x, q1.y, q1.z, q1.w);
+        const float4 mnz = make_float4(is_leaf ? q0.z : mnz_.x, mnz_.y, mnz_.z, mnz_.w);
+        const float4 mxx = make_float4(is_leaf ? q0.w : mxx_.x, mxx_.y, mxx_.z, mxx_.w);
+        const float4 mxy = make_float4(is_leaf ? q1.x : mxy_.x, mxy_.y, mxy_.z, mxy_.w);
+        const float4 mxz = make_float4(is_leaf ? q1.y : mxz_.x, mxz_.y, mxz_.z, mxz_.w);
+        const int4 ch = make_int4(is_leaf ? cur : ch_.x, ch_.y, ch_.z, ch_.w);
+        uint32_t hm;
+        if (wave_fast) {
+          hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
         } else {
-          const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
-          const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
-          const int4 ch = *reinterpret_cast<const int4*>(np + 6);
-          uint32_t hm;
-          if (wave_fast) {
-            hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
-          } else {
-            const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
-                        amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
-                        amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
-            hm = 0;
+          const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
+                      amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
+                      amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+          hm = 0;
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-              if (slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) hm |= 1u << i;
-          }
-          // slots 0..3 with ChildIndex != -1 whose box is hit (bvh4.go:119-146): the first
-          // is visited next, the others are pushed in slot order (popped LIFO). Selects
-          // instead of branches: each divergent branch costs exec-mask and lane-mask
-          // bookkeeping on the scalar unit, which is as busy as the vector unit here.
-          const uint32_t m = hm & ((ch.x != -1 ? 1u : 0u) | (ch.y != -1 ? 2u : 0u) | (ch.z != -1 ? 4u : 0u) |
-                                   (ch.w != -1 ? 8u : 0u));
-          const int32_t c01 = (m & 1u) ? ch.x : ch.y, c23 = (m & 4u) ? ch.z : ch.w;
-          next = m == 0 ? -1 : ((m & 3u) ? c01 : c23);
-          // A leaf visited straight after its parent re-tests the same f32 box with the
-          // same tMax (A10): the result is known to be a hit, so skip its node load and
-          // start on its primitives (the visit is still counted).
-          leaf_next = ref_is_leaf(next) && sc.leaf_shortcut;
-          in_prim = leaf_next;
-          pk = leaf_next ? leaf_start(next) : pk;
-          pend = leaf_next ? leaf_start(next) + leaf_count(next) : pend;
-          next = leaf_next ? -1 : next;
-          // the other hit children, compacted in slot order, are written unconditionally to
-          // ring positions sp..sp+2 (the ring keeps 3 free entries above sp); sp moves by
-          // their count
-          const uint32_t rest = m & (m - 1u);  // bits 1..3 only
-          const int np_ = __builtin_popcount(rest);
-          const int32_t e0 = (rest & 2u) ? ch.y : ((rest & 4u) ? ch.z : ch.w);
-          const int32_t e1 = ((rest & 6u) == 6u) ? ch.z : ch.w;
-          stk[(sp & (S - 1)) * 256] = e0;
-          stk[((sp + 1) & (S - 1)) * 256] = e1;
-          stk[((sp + 2) & (S - 1)) * 256] = ch.w;
-          if (sp + np_ > 64) atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
-          sp += np_;
-          advance = !leaf_next;
+          for (int i = 0; i < 4; i++)
+            if (slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) hm |= 1u << i;
         }
+        // slots 0..3 with ChildIndex != -1 whose box is hit (bvh4.go:119-146): the first
+        // is visited next, the others are pushed in slot order (popped LIFO). Selects
+        // instead of branches: each divergent branch costs exec-mask and lane-mask
+        // bookkeeping on the scalar unit, which is as busy as the vector unit here.
+        const uint32_t valid = is_leaf ? 1u
+                                       : ((ch.x != -1 ? 1u : 0u) | (ch.y != -1 ? 2u : 0u) | (ch.z != -1 ? 4u : 0u) |
+                                          (ch.w != -1 ? 8u : 0u));
+        const uint32_t m = hm & valid;
+        const int32_t c01 = (m & 1u) ? ch.x : ch.y, c23 = (m & 4u) ? ch.z : ch.w;
+        next = m == 0 ? -1 : ((m & 3u) ? c01 : c23);
+        // A passed leaf re-test starts on the leaf's primitives. A leaf visited straight
+        // after its parent re-tests the same f32 box with the same tMax (A10): the result
+        // is known to be a hit, so its node load is skipped too (the visit is still counted).
+        const bool enter = ref_is_leaf(next) && (is_leaf || sc.leaf_shortcut);
+        leaf_next = enter && !is_leaf;
+        in_prim = enter;
+        pk = enter ? leaf_start(next) : pk;
+        pend = enter ? leaf_start(next) + leaf_count(next) : pend;
+        next = enter ? -1 : next;
+        // the other hit children, compacted in slot order, are written unconditionally to
+        // ring positions sp..sp+2 (the ring keeps 3 free entries above sp); sp moves by
+        // their count
+        const uint32_t rest = m & (m - 1u);  // bits 1..3 only
+        const int np_ = __builtin_popcount(rest);
+        const int32_t e0 = (rest & 2u) ? ch.y : ((rest & 4u) ? ch.z : ch.w);
+        const int32_t e1 = ((rest & 6u) == 6u) ? ch.z : ch.w;
+        stk[(sp & (S - 1)) * 256] = e0;
+        stk[((sp + 1) & (S - 1)) * 256] = e1;
+        stk[((sp + 2) & (S - 1)) * 256] = ch.w;
+        if (sp + np_ > 64) atomicOr(err, 1u);  // unreachable: the host rejects BVHs deeper than 64 entries
+        sp += np_;
+        advance = !enter;
       }
     }
 #ifdef IZPI_TRACE_CLOCKS
@@ -878,6 +895,11 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t depth, bo
   if (!spec) r[RecLayout<SAMPLER>::S / 2] = make_double2(s, p);
 }
 
+// Result slot of work unit `unit` (= pixel * chunk_spp + sample). Unit-major: paths of
+// neighbouring units finish close in time and fill whole lines (a sample-major layout
+// made k_accumulate coalesced but cost k_shade 16% in scattered partial-line stores).
+IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.out + (size_t)unit * 3; }
+
 // Write the finished path's radiance after unwinding the recursion of
 // colour.go:80-94 / sampler/spectral.go:161-174 from depth-1 down to 0.
 template <int SAMPLER, bool NO_SPEC = false>
@@ -886,7 +908,7 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
     // +0 radiance through only non-specular records: every level computes
     // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
     // so the result is +0 without reading the records
-    double* out = sp.out + (size_t)P.unit * 3;
+    double* out = sample_out(sp, P.unit);
     out[0] = 0.0; out[1] = 0.0; out[2] = 0.0;
     return;
   }
@@ -917,7 +939,7 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
       }
     }
   }
-  double* out = sp.out + (size_t)P.unit * 3;
+  double* out = sample_out(sp, P.unit);
   if (SAMPLER == IZPI_SAMPLER_COLOUR) {
     V3 c = denan(L);  // rgb.go:36 DeNAN per sample
     out[0] = c.x; out[1] = c.y; out[2] = c.z;
@@ -958,7 +980,7 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slo
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) {
     sample_wavelength(rng.next(), P.lambda, P.lpdf);
     if (P.lpdf == 0) {  // render/spectral.go:78-80: skipped, still counted in 1/spp
-      double* out = sp.out + (size_t)unit * 3;
+      double* out = sample_out(sp, unit);
       out[0] = 0; out[1] = 0; out[2] = 0;
       return false;
     }
@@ -1057,15 +1079,24 @@ IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
   return (want && my < sp.total_units) ? my : 0xFFFFFFFFu;
 }
 
-// Fill empty slots (first pass of a chunk): slot i takes new units until one needs tracing.
+// Fill empty slots (first pass of a chunk): slot i takes unit i (the host starts the unit
+// head at min(slots, units), so no atomic is needed: one counter word serialises ~88
+// atomics/us), then further units from the head while its path needs no tracing.
 template <int SAMPLER>
 __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
   bool want = slot < sp.slots;
   bool push = false;
+  bool first = true;
   // a wave keeps grabbing while any of its lanes still lacks a traceable path
   for (;;) {
-    const uint32_t unit = grab_unit(sp, want);
+    uint32_t unit;
+    if (first) {
+      unit = (want && slot < sp.total_units) ? slot : 0xFFFFFFFFu;
+      first = false;
+    } else {
+      unit = grab_unit(sp, want);
+    }
     if (__ballot(want) == 0) break;
     if (want) {
       if (unit == 0xFFFFFFFFu) {
@@ -1405,7 +1436,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
   if (p >= ap.num_pixels) return;
   double c0 = ap.running[3 * (size_t)p], c1 = ap.running[3 * (size_t)p + 1], c2 = ap.running[3 * (size_t)p + 2];
   const double* s = ap.samples + (size_t)p * ap.chunk_spp * 3;
-  for (uint32_t k = 0; k < ap.chunk_spp; k++) {
+  for (uint32_t k = 0; k < ap.chunk_spp; k++) {  // sample order, as rgb.go:36
     c0 = c0 + s[3 * k];
     c1 = c1 + s[3 * k + 1];
     c2 = c2 + s[3 * k + 2];
@@ -1767,10 +1798,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
   for (uint32_t s0 = 0; s0 < req->spp; s0 += chunk) {
     const uint32_t cs = std::min(chunk, req->spp - s0);
     sp.chunk_spp = cs; sp.s0 = s0; sp.total_units = num_pixels * cs;
-    HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, sizeof(uint32_t), st));          // head
+    const uint32_t start_slots = std::min<uint32_t>(sp.slots, sp.total_units);
+    HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)start_slots, 1, st));       // head: k_start gives slot i unit i
     HIP_TRY(hipMemsetAsync(ctx->d_misc + 3, 0, 2 * sizeof(uint32_t), st));  // queue counts
     wp.q_out = q[0]; wp.q_out_count = qn[0];
-    const uint32_t start_slots = std::min<uint32_t>(sp.slots, sp.total_units);
     ShadeParams sp0 = sp;
     sp0.slots = sp.slots;
     hipLaunchKernelGGL(k_start<SAMPLER>, dim3((start_slots + 255) / 256), dim3(256), 0, st, ctx->sc, sp0, wp);
@@ -2039,7 +2070,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       ref[k] = (int32_t)n_inner++;
     }
   }
-  std::vector<GInner> inner(n_inner);
+  std::vector<GInner> inner(std::max<uint32_t>(1, n_inner));  // >= 1: k_trace2's leaf lanes read a dummy inner node
   std::vector<GLeaf> leaves(std::max<uint32_t>(1, d->num_prims));  // indexed by first primitive
   uint32_t leaf_shortcut = 1;
   for (uint32_t k = 0; k < d->num_nodes; k++) {
@@ -2187,6 +2218,8 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     const float* f = g.mnx;  // the 24 bounds are contiguous
     for (int i = 0; i < 24; i++) if (f[i] != f[i]) sc.nan_free_bounds = 0;
   }
+  for (const GLeaf& L : leaves)  // leaf re-tests run through the same 4-slot test
+    for (int i = 0; i < 3; i++) if (L.mn[i] != L.mn[i] || L.mx[i] != L.mx[i]) sc.nan_free_bounds = 0;
   if (getenv("IZPI_NO_FAST_SLAB")) sc.nan_free_bounds = 0;
   sc.cam = d->camera;
   // traversal stack bound (see host_scene.cpp stack_bound)

@@ -1,0 +1,50 @@
+"""Per-rank render time of a W-way tile shard on ONE GPU (strong-scaling probe).
+
+python tools/shard_probe.py --config C3 --worlds 1,2,4,8
+For each W, renders rank 0's and rank W-1's tiles (packed layout, device memory) and
+prints ms, passes and the implied efficiency T(1) / (W * max rank time), i.e. the
+scaling the multi-GPU bench would see without the gather."""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    a = ap.parse_args()
+    import torch
+    from izpi_amd import _native as N
+    from izpi_amd import configs, sharding
+    from izpi_amd.renderer import GPURenderer, common_tiles
+    cfg = configs.configs()[a.config]
+    spp = a.spp or cfg.spp
+    r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler)
+    all_tiles = common_tiles(cfg.width, cfg.height)
+    t1 = None
+    for w in [int(x) for x in a.worlds.split(",")]:
+        worst = 0.0
+        for rank in sorted({0, w - 1}):
+            mine = sharding.shard_tiles(all_tiles, rank, w)
+            buf = torch.zeros(sharding.packed_len(all_tiles, w), dtype=torch.float64, device="cuda")
+            r.render_device(buf.data_ptr(), tiles=mine, layout=N.OUT_PACKED)  # warm
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            st = r.render_device(buf.data_ptr(), tiles=mine, layout=N.OUT_PACKED)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t) * 1e3
+            worst = max(worst, ms)
+            print("W=%d rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f, %d passes)" %
+                  (w, rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["launches"]), flush=True)
+        if t1 is None:
+            t1 = worst
+        print("W=%d implied efficiency %.3f" % (w, t1 / (w * worst)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
