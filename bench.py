@@ -131,7 +131,7 @@ def main():
     t1 = time.perf_counter()
     agg = {k: 0.0 for k in ("node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests", "rays",
                             "kernel_ms", "shade_ms", "total_ms", "launches", "samples", "node_steps", "prim_steps",
-                            "leaf_shortcuts")}
+                            "leaf_shortcuts", "tail_ms", "tail_node_visits", "tail_tri_tests", "tail_sph_tests")}
     for _ in range(args.steps):
         canvas, st = step()
         for k in agg:
@@ -147,8 +147,10 @@ def main():
     samples_per_step = cfg.width * cfg.height * spp
     value = samples_per_step * args.steps / elapsed / 1e6
 
-    # roofline of the dominant kernel on this rank: algorithmic bytes / k_trace time
-    trace_bytes = 128.0 * agg["node_visits"] + 72.0 * agg["tri_tests"] + 32.0 * agg["sph_tests"]
+    # roofline of the dominant kernel on this rank: algorithmic bytes / k_trace2 time
+    # (the traversals k_tail runs at the end of the frame are counted apart)
+    trace_bytes = (128.0 * (agg["node_visits"] - agg["tail_node_visits"]) + 72.0 * (agg["tri_tests"] - agg["tail_tri_tests"])
+                   + 32.0 * (agg["sph_tests"] - agg["tail_sph_tests"]))
     achieved = trace_bytes / (agg["kernel_ms"] * 1e-3) / 1e9 if agg["kernel_ms"] > 0 else 0.0
     launches = max(agg["launches"], 1.0)
     traffic = pmc_traffic(args.config)
@@ -181,19 +183,22 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
-                     "kernel": "k_trace", "algorithmic_bytes_per_launch": trace_bytes / launches,
+                     "kernel": "k_trace2", "algorithmic_bytes_per_launch": trace_bytes / launches,
                      "avg_launch_ms": agg["kernel_ms"] / launches, "launches": int(agg["launches"])},
         "cpu_baseline": cpu,
         "detail": {
             "rank0_trace_ms_per_step": agg["kernel_ms"] / args.steps,
             "rank0_shade_ms_per_step": agg["shade_ms"] / args.steps,
+            "rank0_tail_ms_per_step": agg["tail_ms"] / args.steps,
             "rank0_render_ms_per_step": agg["total_ms"] / args.steps,
             "rank0_rays_per_step": agg["rays"] / args.steps,
             "rank0_node_visits_per_ray": agg["node_visits"] / max(agg["rays"], 1),
             "rank0_tri_tests_per_ray": agg["tri_tests"] / max(agg["rays"], 1),
             # k_trace2 SIMD efficiency: useful lane-steps / (64 x wave-level steps)
-            "rank0_node_step_lane_util": (agg["node_visits"] - agg["leaf_shortcuts"]) / max(64 * agg["node_steps"], 1),
-            "rank0_prim_step_lane_util": (agg["tri_tests"] + agg["sph_tests"]) / max(64 * agg["prim_steps"], 1),
+            "rank0_node_step_lane_util": (agg["node_visits"] - agg["tail_node_visits"] - agg["leaf_shortcuts"]) /
+                                         max(64 * agg["node_steps"], 1),
+            "rank0_prim_step_lane_util": (agg["tri_tests"] + agg["sph_tests"] - agg["tail_tri_tests"] - agg["tail_sph_tests"]) /
+                                         max(64 * agg["prim_steps"], 1),
             "rank0_leaf_shortcut_frac": agg["leaf_shortcuts"] / max(agg["node_visits"], 1),
             "setup_s": round(setup_s, 2),
             "bvh_build_ms": r.host.build_ms,

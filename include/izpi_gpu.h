@@ -119,6 +119,11 @@ typedef struct izpi_render_stats {
    * loop iterations that ran a node step / a primitive step, and leaf visits taken by a
    * shortcut (no node load). */
   uint64_t node_steps, prim_steps, leaf_shortcuts;
+  /* device time of k_tail, which traces AND shades the last paths once every work unit
+   * has started (not included in kernel_ms / shade_ms) */
+  double tail_ms;
+  /* the part of node_visits / tri_tests / sph_tests done inside k_tail */
+  uint64_t tail_node_visits, tail_tri_tests, tail_sph_tests;
 } izpi_render_stats;
 
 /* Hit record returned by izpi_gpu_trace: BVH4.Hit (bvh4.go:49-164) followed by

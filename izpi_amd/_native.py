@@ -87,7 +87,9 @@ class RenderStats(C.Structure):
                 ("sph_tests", C.c_uint64), ("light_tri_tests", C.c_uint64), ("light_sph_tests", C.c_uint64),
                 ("samples", C.c_uint64), ("kernel_ms", C.c_double), ("shade_ms", C.c_double),
                 ("total_ms", C.c_double), ("launches", C.c_uint32), ("pad", C.c_uint32),
-                ("node_steps", C.c_uint64), ("prim_steps", C.c_uint64), ("leaf_shortcuts", C.c_uint64)]
+                ("node_steps", C.c_uint64), ("prim_steps", C.c_uint64), ("leaf_shortcuts", C.c_uint64),
+                ("tail_ms", C.c_double), ("tail_node_visits", C.c_uint64), ("tail_tri_tests", C.c_uint64),
+                ("tail_sph_tests", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}

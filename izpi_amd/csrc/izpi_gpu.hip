@@ -49,7 +49,7 @@ __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
-       CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_N };  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
+       CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH, CNT_N };  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 
 // ======================================================= textures / spectra
@@ -316,6 +316,83 @@ __global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WavePara
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
     if (lane == 0 && s) atomicAdd(counters + idx[i], s);
   }
+}
+
+// BVH4.Hit (bvh4.go:49-164) of one slot's ray by one lane, from the root to the end,
+// in the reference's visit order (leaf re-test A10, equal-t acceptance A11, f32 box test
+// A15): the per-lane form k_tail uses. Writes the slot's hit record like k_trace2.
+template <int STACK>
+IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot, int32_t* stk, uint32_t& c_rays,
+                        uint32_t& c_nodes, uint32_t& c_tri, uint32_t& c_sph, uint32_t* err) {
+  const RayHot& r = wp.rhot[slot];
+  const RayAux& ra = wp.raux[slot];
+  const V3 o = mk(r.o[0], r.o[1], r.o[2]), d = mk(r.d[0], r.d[1], r.d[2]);
+  const double tmin = r.tmin, time = ra.time;
+  double tmax = r.tmax;
+  if (ra.kind == RAY_MAIN) c_rays++;
+  const float ix = (float)(1.0 / d.x), iy = (float)(1.0 / d.y), iz = (float)(1.0 / d.z);
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  int32_t cur = sc.root;
+  int sp = 0;
+  double bu = 0, bv = 0;
+  int32_t bprim = -1;
+  while (cur != -1) {
+    c_nodes++;
+    const float tm = (float)tmax;
+    int32_t next = -1;
+    if (ref_is_leaf(cur)) {
+      const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_start(cur));
+      const float4 a = lp[0], b = lp[1];
+      if (slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
+        const int32_t start = leaf_start(cur), end = start + leaf_count(cur);
+        for (int32_t k = start; k < end; k++) {  // bvh4.go:123-134
+          const double2* pp = reinterpret_cast<const double2*>(sc.prims + k);
+          const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
+          const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
+          if ((uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE) {
+            c_tri++;
+            double t, u, v;
+            if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) { tmax = t; bu = u; bv = v; bprim = k; }
+          } else {
+            c_sph++;
+            double t; int root;
+            if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) { tmax = t; bu = (double)root; bv = 0; bprim = k; }
+          }
+        }
+      }
+    } else {
+      const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
+      const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
+      const int4 ch = *reinterpret_cast<const int4*>(np + 6);
+      const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
+                  amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
+                  amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+      const int32_t ach[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {  // bvh4.go:119-146
+        if (ach[i] == -1) continue;
+        if (!slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) continue;
+        if (next == -1) {
+          next = ach[i];
+        } else if (sp < STACK) {
+          stk[sp * 256] = ach[i];
+          sp++;
+        } else {
+          atomicOr(err, 1u);  // unreachable: STACK >= host-computed bound
+        }
+      }
+    }
+    if (next != -1) {
+      cur = next;
+    } else if (sp > 0) {
+      sp--;
+      cur = stk[sp * 256];
+    } else {
+      cur = -1;
+    }
+  }
+  wp.hhot[slot] = HitHot{bprim >= 0 ? tmax : 0.0, bprim, 0u};
+  wp.huv[slot] = HitUV{bu, bv};
 }
 
 // BVH4.Hit, step-scheduled variant. Each lane is in one of two modes: NODE (visit
@@ -1113,7 +1190,11 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
       }
     }
   }
-  queue_push(wp, push, slot);
+  // one queue reservation per block (a per-wave atomic on the one count word made this
+  // kernel atomic-bound: 16M slots = 262k serialised atomics)
+  uint32_t parity = 0;
+  const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
+  if (push) wp.q_out[pos] = slot;
 }
 
 #ifndef IZPI_SPLIT_REFILL
@@ -1178,12 +1259,215 @@ IZPI_DEV void store_path_rng_depth(PathHot* ps, uint32_t rng, uint32_t depth) {
   *reinterpret_cast<uint2*>(&ps->rng) = make_uint2(rng, depth);
 }
 
-// One shading pass over the slots traced in the previous k_trace.
 // MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
 // DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
 // footprint small; MATSET_FULL adds Dielectric, Metal and PBR. The host picks the
 // variant from the scene's material kinds (results are identical).
 enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
+
+// One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
+// one bounce deep (colour.go:33-94, sampler/spectral.go:47-80). Sets `push` when the slot
+// has a ray to trace next and `done` when its sample finished.
+template <int SAMPLER, int MATSET>
+IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, bool& push,
+                         bool& done, uint32_t& c_lt, uint32_t& c_ls) {
+  const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
+  PathSt P;
+  {
+    const PathHot ph = wp.phot[slot];
+    P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.pad = 0;
+    P.lambda = 0; P.lpdf = 1;
+    if (!COLOUR) { const PathCold& pc = wp.pcold[slot]; P.lambda = pc.lambda; P.lpdf = pc.lpdf; }
+  }
+  RayRec R;
+  {
+    const RayHot rh = wp.rhot[slot];
+    for (int k = 0; k < 3; k++) { R.o[k] = rh.o[k]; R.d[k] = rh.d[k]; }
+    R.tmin = rh.tmin; R.tmax = rh.tmax;
+    const RayAux& ra = wp.raux[slot];
+    R.kind = ra.kind; R.pad = ra.pad;
+    R.time = 0;  // read below only for sphere hits
+  }
+  HitOut H;
+  {
+    const HitHot hh = wp.hhot[slot];
+    H.t = hh.t; H.prim = hh.prim; H.pad = 0; H.u = 0; H.v = 0;
+  }
+  Lcg rng;
+  rng.s = P.rng;
+  const V3 ro = mk(R.o[0], R.o[1], R.o[2]), rd = mk(R.d[0], R.d[1], R.d[2]);
+  V3 L = mk(0, 0, 0);
+  bool terminal = false;
+  bool spec = false, have_pdf = false;
+  V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
+  V3 hit_n = mk(0, 0, 0);
+  Onb cos_onb;
+  if (MATSET == MATSET_FULL && R.kind == RAY_PATHLEN) {
+    // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
+    const PathCold& pc = wp.pcold[slot];
+    const V3 hp = mk(pc.pend[0], pc.pend[1], pc.pend[2]);
+    double len = 10.0;
+    if (H.prim >= 0) {
+      V3 exit_p = add(ro, smul(rd, H.t));
+      len = length(sub(exit_p, hp));
+      if (len < 0.1) len = 0.1;
+      if (len > 100.0) len = 100.0;
+    }
+    const uint32_t mat_id = (uint32_t)R.pad;  // dielectric material stashed by the glass bounce
+    const izpi_material& gm_ = sc.materials[mat_id];
+    if (COLOUR) att = mk(gm::exp(-gm_.rgb[0] * len), gm::exp(-gm_.rgb[1] * len), gm::exp(-gm_.rgb[2] * len));
+    else att.x = gm_.absorb_tex >= 0 ? gm::exp(-tex_spectral(sc, gm_.absorb_tex, P.lambda) * len) : 1.0;
+    spec = true;
+    next_o = hp;
+    next_d = rd;
+  } else if (H.prim < 0) {
+    L = COLOUR ? mk(sp.background[0], sp.background[1], sp.background[2])
+               : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
+    terminal = true;
+  } else {
+    const GShade gs = sc.shade[H.prim];
+    HitRec h;
+    const double rtime = IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_SPHERE ? wp.raux[slot].time : 0.0;
+    hit_record(sc, H, wp.huv + slot, gs, ro, rd, rtime, (sc.mat_flags[gs.mat] & 1u) != 0, h);
+    hit_n = h.n;
+    next_o = h.p;
+    const izpi_material& m = sc.materials[h.mat];
+    switch (m.kind) {
+      case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
+        if (dot(h.n, rd) < 0.0) {
+          if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+          else L.x = tex_spectral(sc, m.spectral_tex, P.lambda);
+        }
+        terminal = true;
+        break;
+      }
+      case IZPI_MAT_LAMBERT: {  // lambertian.go:44-70: 2 draws for a ray the sampler discards (A6)
+        rng.next();
+        rng.next();
+        cos_onb.build(h.n);
+        if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+        else att.x = tex_spectral(sc, m.spectral_tex, P.lambda);
+        have_pdf = true;
+        break;
+      }
+      case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
+        if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
+        const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
+        bool reflected;
+        next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
+        const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
+        if (!reflected && (!COLOUR || beer_rgb)) {
+          // the extra World.Hit of calculatePathLength: trace it, finish next pass
+          PathCold* pcw = wp.pcold + slot;
+          pcw->pend[0] = h.p.x; pcw->pend[1] = h.p.y; pcw->pend[2] = h.p.z;
+          store_path_rng_depth(wp.phot + slot, rng.s, P.depth);
+          store_ray(wp, slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
+          push = true;
+          break;
+        }
+        att = mk(1.0, 1.0, 1.0);
+        spec = true;
+        break;
+      }
+      case IZPI_MAT_METAL: {  // metal.go:34-41 (RGB only: SpectralScatter is nonSpectral)
+        if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if (!COLOUR) { terminal = true; break; }
+        V3 reflected = reflect(unit(rd), h.n);
+        next_d = add(reflected, smul(random_in_unit_sphere(rng), m.fuzz));
+        att = mk(m.rgb[0], m.rgb[1], m.rgb[2]);
+        spec = true;
+        break;
+      }
+      case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
+        if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
+        double alb_s = 0;
+        if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+        else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda);
+        else { V3 c = tex_rgb(sc, m.albedo_tex, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
+        V3 normal = h.n;
+        if (m.normal_tex >= 0) {
+          V3 nuv = tex_rgb(sc, m.normal_tex, h.u, h.v);
+          V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
+          V3 nn0 = h.n;
+          V3 t = cross(nn0, mk(0, 1, 0));
+          if (dot(t, t) < 0.001) t = cross(nn0, mk(1, 0, 0));
+          t = sdiv(t, length(t));
+          V3 b = cross(nn0, t);
+          b = sdiv(b, length(b));
+          V3 nn = mk(t.x * tn.x + b.x * tn.y + nn0.x * tn.z, t.y * tn.x + b.y * tn.y + nn0.y * tn.z,
+                     t.z * tn.x + b.z * tn.y + nn0.z * tn.z);
+          normal = sdiv(nn, length(nn));
+        }
+        V3 rough = m.roughness_tex >= 0 ? tex_rgb(sc, m.roughness_tex, h.u, h.v) : mk(0.5, 0.5, 0.5);
+        V3 metal = m.metalness_tex >= 0 ? tex_rgb(sc, m.metalness_tex, h.u, h.v) : mk(0.0, 0.0, 0.0);
+        double rv = (rough.x + rough.y + rough.z) / 3.0;
+        double mv = (metal.x + metal.y + metal.z) / 3.0;
+        Onb uvw;
+        uvw.build(normal);
+        V3 reflected = reflect(unit(rd), normal);
+        double cosTheta = gm::abs(dot(unit(rd), normal));
+        double fresnel = 0.04 + (1.0 - 0.04) * gm::pow(1.0 - cosTheta, 5.0);
+        fresnel = fresnel + (mv * 0.5);
+        double sprob = fresnel * (1.0 - rv);
+        if (rng.next() < sprob) {
+          double rf = gm::max(0.01, rv * 0.3);
+          V3 rdir = random_in_unit_sphere(rng);
+          next_d = unit(add(reflected, smul(rdir, rf)));
+          spec = true;
+        } else {
+          next_d = unit(uvw.local(random_cosine_direction(rng)));
+          spec = false;
+          have_pdf = true;  // the sampler ignores this ray and samples the mixture pdf
+        }
+        cos_onb.build(normal);
+        if (!COLOUR) att.x = spec ? alb_s * 1.5 : alb_s;
+        break;
+      }
+      default: {
+        atomicOr(sp.error, 2u);
+        terminal = true;
+      }
+    }
+  }
+  if (!push) {
+    if (terminal) {
+      finish<SAMPLER, MATSET == MATSET_BASIC>(sp, slot, P, L);
+      done = true;
+    } else {
+      if (have_pdf) {
+        // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:85-90, mixture.go:17-33)
+        V3 dir;
+        if (rng.next() < 0.5) dir = lights_random(sc, next_o, rng);
+        else dir = cos_onb.local(random_cosine_direction(rng));
+        // (evaluated in an order that frees the ONB, normal and attenuation before
+        // the light-pdf loop; every value is computed exactly as in the reference)
+        const V3 ud = unit(dir);
+        const double cosv = dot(ud, cos_onb.w);
+        const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
+        double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
+        if (sc_cos < 0) sc_cos = 0;
+        rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, 0);
+        const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
+        rec_ptr<SAMPLER>(sp, slot, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
+        next_d = dir;
+      } else {
+        rec_store<SAMPLER>(sp, slot, P.depth, true, att, 0, 0);
+      }
+      P.depth++;
+      P.rng = rng.s;
+      if (P.depth >= sp.max_depth) {
+        finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
+        done = true;
+      } else {
+        store_path_rng_depth(wp.phot + slot, P.rng, P.depth);
+        store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0, MATSET == MATSET_FULL);
+        push = true;
+      }
+    }
+  }
+}
+
+// One shading pass over the slots traced in the previous k_trace.
 #ifndef IZPI_SHADE_WPE
 #define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (no spill)
 #endif
@@ -1195,7 +1479,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve LDS buffer set
-  const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const uint32_t n = *wp.q_in_count;
   uint32_t c_lt = 0, c_ls = 0;
   const uint32_t stride = gridDim.x * 256;
@@ -1206,201 +1489,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     uint32_t slot = valid ? wp.q_in[i] : 0;
     bool push = false;      // slot has a ray to trace next
     bool done = false;      // slot's sample finished: grab a new unit
-    if (valid) {
-      PathSt P;
-      {
-        const PathHot ph = wp.phot[slot];
-        P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.pad = 0;
-        P.lambda = 0; P.lpdf = 1;
-        if (!COLOUR) { const PathCold& pc = wp.pcold[slot]; P.lambda = pc.lambda; P.lpdf = pc.lpdf; }
-      }
-      RayRec R;
-      {
-        const RayHot rh = wp.rhot[slot];
-        for (int k = 0; k < 3; k++) { R.o[k] = rh.o[k]; R.d[k] = rh.d[k]; }
-        R.tmin = rh.tmin; R.tmax = rh.tmax;
-        const RayAux& ra = wp.raux[slot];
-        R.kind = ra.kind; R.pad = ra.pad;
-        R.time = 0;  // read below only for sphere hits
-      }
-      HitOut H;
-      {
-        const HitHot hh = wp.hhot[slot];
-        H.t = hh.t; H.prim = hh.prim; H.pad = 0; H.u = 0; H.v = 0;
-      }
-      Lcg rng;
-      rng.s = P.rng;
-      const V3 ro = mk(R.o[0], R.o[1], R.o[2]), rd = mk(R.d[0], R.d[1], R.d[2]);
-      V3 L = mk(0, 0, 0);
-      bool terminal = false;
-      bool spec = false, have_pdf = false;
-      V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
-      V3 hit_n = mk(0, 0, 0);
-      Onb cos_onb;
-      if (MATSET == MATSET_FULL && R.kind == RAY_PATHLEN) {
-        // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
-        const PathCold& pc = wp.pcold[slot];
-        const V3 hp = mk(pc.pend[0], pc.pend[1], pc.pend[2]);
-        double len = 10.0;
-        if (H.prim >= 0) {
-          V3 exit_p = add(ro, smul(rd, H.t));
-          len = length(sub(exit_p, hp));
-          if (len < 0.1) len = 0.1;
-          if (len > 100.0) len = 100.0;
-        }
-        const uint32_t mat_id = (uint32_t)R.pad;  // dielectric material stashed by the glass bounce
-        const izpi_material& gm_ = sc.materials[mat_id];
-        if (COLOUR) att = mk(gm::exp(-gm_.rgb[0] * len), gm::exp(-gm_.rgb[1] * len), gm::exp(-gm_.rgb[2] * len));
-        else att.x = gm_.absorb_tex >= 0 ? gm::exp(-tex_spectral(sc, gm_.absorb_tex, P.lambda) * len) : 1.0;
-        spec = true;
-        next_o = hp;
-        next_d = rd;
-      } else if (H.prim < 0) {
-        L = COLOUR ? mk(sp.background[0], sp.background[1], sp.background[2])
-                   : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
-        terminal = true;
-      } else {
-        const GShade gs = sc.shade[H.prim];
-        HitRec h;
-        const double rtime = IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_SPHERE ? wp.raux[slot].time : 0.0;
-        hit_record(sc, H, wp.huv + slot, gs, ro, rd, rtime, (sc.mat_flags[gs.mat] & 1u) != 0, h);
-        hit_n = h.n;
-        next_o = h.p;
-        const izpi_material& m = sc.materials[h.mat];
-        switch (m.kind) {
-          case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
-            if (dot(h.n, rd) < 0.0) {
-              if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-              else L.x = tex_spectral(sc, m.spectral_tex, P.lambda);
-            }
-            terminal = true;
-            break;
-          }
-          case IZPI_MAT_LAMBERT: {  // lambertian.go:44-70: 2 draws for a ray the sampler discards (A6)
-            rng.next();
-            rng.next();
-            cos_onb.build(h.n);
-            if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-            else att.x = tex_spectral(sc, m.spectral_tex, P.lambda);
-            have_pdf = true;
-            break;
-          }
-          case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
-            if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
-            const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
-            bool reflected;
-            next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
-            const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
-            if (!reflected && (!COLOUR || beer_rgb)) {
-              // the extra World.Hit of calculatePathLength: trace it, finish next pass
-              PathCold* pcw = wp.pcold + slot;
-              pcw->pend[0] = h.p.x; pcw->pend[1] = h.p.y; pcw->pend[2] = h.p.z;
-              store_path_rng_depth(wp.phot + slot, rng.s, P.depth);
-              store_ray(wp, slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
-              push = true;
-              break;
-            }
-            att = mk(1.0, 1.0, 1.0);
-            spec = true;
-            break;
-          }
-          case IZPI_MAT_METAL: {  // metal.go:34-41 (RGB only: SpectralScatter is nonSpectral)
-            if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
-            if (!COLOUR) { terminal = true; break; }
-            V3 reflected = reflect(unit(rd), h.n);
-            next_d = add(reflected, smul(random_in_unit_sphere(rng), m.fuzz));
-            att = mk(m.rgb[0], m.rgb[1], m.rgb[2]);
-            spec = true;
-            break;
-          }
-          case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
-            if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
-            double alb_s = 0;
-            if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-            else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda);
-            else { V3 c = tex_rgb(sc, m.albedo_tex, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
-            V3 normal = h.n;
-            if (m.normal_tex >= 0) {
-              V3 nuv = tex_rgb(sc, m.normal_tex, h.u, h.v);
-              V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
-              V3 nn0 = h.n;
-              V3 t = cross(nn0, mk(0, 1, 0));
-              if (dot(t, t) < 0.001) t = cross(nn0, mk(1, 0, 0));
-              t = sdiv(t, length(t));
-              V3 b = cross(nn0, t);
-              b = sdiv(b, length(b));
-              V3 nn = mk(t.x * tn.x + b.x * tn.y + nn0.x * tn.z, t.y * tn.x + b.y * tn.y + nn0.y * tn.z,
-                         t.z * tn.x + b.z * tn.y + nn0.z * tn.z);
-              normal = sdiv(nn, length(nn));
-            }
-            V3 rough = m.roughness_tex >= 0 ? tex_rgb(sc, m.roughness_tex, h.u, h.v) : mk(0.5, 0.5, 0.5);
-            V3 metal = m.metalness_tex >= 0 ? tex_rgb(sc, m.metalness_tex, h.u, h.v) : mk(0.0, 0.0, 0.0);
-            double rv = (rough.x + rough.y + rough.z) / 3.0;
-            double mv = (metal.x + metal.y + metal.z) / 3.0;
-            Onb uvw;
-            uvw.build(normal);
-            V3 reflected = reflect(unit(rd), normal);
-            double cosTheta = gm::abs(dot(unit(rd), normal));
-            double fresnel = 0.04 + (1.0 - 0.04) * gm::pow(1.0 - cosTheta, 5.0);
-            fresnel = fresnel + (mv * 0.5);
-            double sprob = fresnel * (1.0 - rv);
-            if (rng.next() < sprob) {
-              double rf = gm::max(0.01, rv * 0.3);
-              V3 rdir = random_in_unit_sphere(rng);
-              next_d = unit(add(reflected, smul(rdir, rf)));
-              spec = true;
-            } else {
-              next_d = unit(uvw.local(random_cosine_direction(rng)));
-              spec = false;
-              have_pdf = true;  // the sampler ignores this ray and samples the mixture pdf
-            }
-            cos_onb.build(normal);
-            if (!COLOUR) att.x = spec ? alb_s * 1.5 : alb_s;
-            break;
-          }
-          default: {
-            atomicOr(sp.error, 2u);
-            terminal = true;
-          }
-        }
-      }
-      if (!push) {
-        if (terminal) {
-          finish<SAMPLER, MATSET == MATSET_BASIC>(sp, slot, P, L);
-          done = true;
-        } else {
-          if (have_pdf) {
-            // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:85-90, mixture.go:17-33)
-            V3 dir;
-            if (rng.next() < 0.5) dir = lights_random(sc, next_o, rng);
-            else dir = cos_onb.local(random_cosine_direction(rng));
-            // (evaluated in an order that frees the ONB, normal and attenuation before
-            // the light-pdf loop; every value is computed exactly as in the reference)
-            const V3 ud = unit(dir);
-            const double cosv = dot(ud, cos_onb.w);
-            const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
-            double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
-            if (sc_cos < 0) sc_cos = 0;
-            rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, 0);
-            const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
-            rec_ptr<SAMPLER>(sp, slot, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
-            next_d = dir;
-          } else {
-            rec_store<SAMPLER>(sp, slot, P.depth, true, att, 0, 0);
-          }
-          P.depth++;
-          P.rng = rng.s;
-          if (P.depth >= sp.max_depth) {
-            finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
-            done = true;
-          } else {
-            store_path_rng_depth(wp.phot + slot, P.rng, P.depth);
-            store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0, MATSET == MATSET_FULL);
-            push = true;
-          }
-        }
-      }
-    }
+    if (valid) shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, push, done, c_lt, c_ls);
 #if IZPI_SPLIT_REFILL
     {  // finished slots go to the free list; k_refill gives them new units
       const uint32_t fpos = block_reserve(wp.free_count, done, parity);
@@ -1419,6 +1508,37 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     unsigned long long s = vals[k];
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
     if (lane == 0 && s) atomicAdd(sp.counters + idx[k], s);
+  }
+}
+
+// The wavefront's tail. Once every work unit has started and few paths remain, the
+// pass-synchronous loop pays, per pass, the latency of that pass's longest traversal.
+// k_tail instead runs each remaining path to its end in one lane: trace, shade, trace...
+// (no refill: the unit head is exhausted), so the passes of different paths overlap.
+// Same per-ray code paths, results and counters as k_trace + k_shade.
+template <int SAMPLER, int MATSET, int STACK>
+__global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  __shared__ int32_t lds_stack[STACK * 256];
+  int32_t* stk = lds_stack + threadIdx.x;
+  const uint32_t n = *wp.q_in_count;
+  uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_lt = 0, c_ls = 0;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t slot = wp.q_in[i];
+    for (;;) {
+      trace_one<STACK>(sc, wp, slot, stk, c_rays, c_nodes, c_tri, c_sph, sp.error);
+      bool push = false, done = false;
+      shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, push, done, c_lt, c_ls);
+      if (!push) break;
+    }
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long vals[9] = {c_rays, c_nodes, c_tri, c_sph, c_lt, c_ls, c_nodes, c_tri, c_sph};
+  const int idx[9] = {CNT_RAYS, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH};
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    unsigned long long v = vals[k];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+    if (lane == 0 && v) atomicAdd(sp.counters + idx[k], v);
   }
 }
 
@@ -1644,7 +1764,7 @@ struct izpi_ctx {
   uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
-  uint32_t* h_count = nullptr;                        // pinned readback of the queue length
+  uint32_t* h_count = nullptr;                        // pinned readback of d_misc (unit head, queue lengths)
   hipEvent_t ev3 = nullptr;
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
   izpi_render_stats last{};
@@ -1782,7 +1902,7 @@ uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint3
 // per-sample radiance into the pixels in sample order.
 template <int SAMPLER, int MATSET>
 int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveParams& wp, AccumParams& ap,
-               uint32_t num_pixels, uint32_t chunk, float* trace_ms, float* shade_ms, uint32_t* launches) {
+               uint32_t num_pixels, uint32_t chunk, float* trace_ms, float* shade_ms, float* tail_ms, uint32_t* launches) {
   hipStream_t st = ctx->stream;
   int shade_res = 0;
   Tracer tr;
@@ -1791,6 +1911,13 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
   if ((rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res))) return rc;
   int refill_res = 0;
   if ((rc = resident_blocks(ctx, k_refill<SAMPLER>, &refill_res))) return rc;
+  // tail kernel: used once every unit has started and at most `tail_max` paths remain
+  const bool tail_deep = ctx->stack_needed > 32;
+  int tail_res = 0;
+  if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res)
+                      : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
+  uint64_t tail_max = (uint64_t)tail_res * 256;
+  if (const char* e = getenv("IZPI_TAIL")) tail_max = strtoull(e, nullptr, 10);
   uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
   wp.free_q = ctx->d_queue + 2 * (size_t)sp.slots;
   wp.free_count = ctx->d_misc + 5;
@@ -1835,7 +1962,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
       }
-      HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[cur], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->d_misc, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
       for (int b = 0; b < B; b++) {
         float t_ms = 0, s_ms = 0;
@@ -1845,7 +1972,21 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         *shade_ms += s_ms;
         (*launches)++;
       }
-      n = *ctx->h_count;
+      n = ctx->h_count[3 + cur];
+      if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
+        // every unit has started: finish the remaining paths in one k_tail launch
+        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
+        HIP_TRY(hipEventRecord(ctx->evb[0], st));
+        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evb[1], st));
+        HIP_TRY(hipEventSynchronize(ctx->evb[1]));
+        float t_ms = 0;
+        HIP_TRY(hipEventElapsedTime(&t_ms, ctx->evb[0], ctx->evb[1]));
+        *tail_ms += t_ms;
+        n = 0;
+      }
     }
     ap.chunk_spp = cs;
     ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
@@ -1946,10 +2087,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   ap.tile_w = tw; ap.tile_h = th; ap.sampler = req->sampler; ap.out_layout = req->out_layout;
   ap.tiles = ctx->d_tiles; ap.samples = ctx->d_samples; ap.running = ctx->d_running; ap.out = out_dev;
 
-  float trace_ms = 0, shade_ms = 0;
+  float trace_ms = 0, shade_ms = 0, tail_ms = 0;
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
-#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &launches)
+#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &tail_ms, &launches)
   const bool basic = ctx->basic_materials;
   if (req->sampler == IZPI_SAMPLER_COLOUR)
     rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
@@ -1978,8 +2119,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.rays = cnt[CNT_RAYS]; s.node_visits = cnt[CNT_NODES]; s.tri_tests = cnt[CNT_TRI]; s.sph_tests = cnt[CNT_SPH];
   s.light_tri_tests = cnt[CNT_LTRI]; s.light_sph_tests = cnt[CNT_LSPH];
   s.samples = (uint64_t)num_pixels * req->spp;
-  s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches;
+  s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches; s.tail_ms = tail_ms;
   s.node_steps = cnt[CNT_NSTEP]; s.prim_steps = cnt[CNT_PSTEP]; s.leaf_shortcuts = cnt[CNT_SHORT];
+  s.tail_node_visits = cnt[CNT_TAIL_NODES]; s.tail_tri_tests = cnt[CNT_TAIL_TRI]; s.tail_sph_tests = cnt[CNT_TAIL_SPH];
 #ifdef IZPI_TRACE_CLOCKS
   fprintf(stderr, "IZPI_TRACE_CLOCKS refill %llu node %llu prim %llu advance %llu (wave cycles)\n", cnt[CNT_CLK_REFILL],
           cnt[CNT_CLK_NODE], cnt[CNT_CLK_PRIM], cnt[CNT_CLK_ADV]);
@@ -2012,7 +2154,7 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipEventCreate(&ctx->ev2) != hipSuccess || hipEventCreate(&ctx->ev3) != hipSuccess ||
-      hipHostMalloc((void**)&ctx->h_count, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->h_count, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
       hipMalloc((void**)&ctx->d_misc, 8 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) != hipSuccess) {
     delete ctx;

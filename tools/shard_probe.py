@@ -39,8 +39,8 @@ def main():
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t) * 1e3
             worst = max(worst, ms)
-            print("W=%d rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f, %d passes)" %
-                  (w, rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["launches"]), flush=True)
+            print("W=%d rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f tail %.1f, %d passes)" %
+                  (w, rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["tail_ms"], st["launches"]), flush=True)
         if t1 is None:
             t1 = worst
         print("W=%d implied efficiency %.3f" % (w, t1 / (w * worst)), flush=True)
