@@ -148,7 +148,11 @@ def test_render_dragon_small_bitwise(gpu):
     r.close()
 
 
-def test_render_spectral_glass_bitwise(gpu):
+@pytest.mark.parametrize("tail", ["default", "0"])
+def test_render_spectral_glass_bitwise(gpu, tail, monkeypatch):
+    """Dielectric spheres: path-length rays, sphere tests; with and without k_tail."""
+    if tail != "default":
+        monkeypatch.setenv("IZPI_TAIL", tail)
     scene = configs.cornell_glass_spectral()
     r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL)
     img = r.render()
@@ -201,10 +205,13 @@ def test_tiles_packed_and_unpack(gpu):
                                  {"IZPI_PRIM_W": "100000"}, {"IZPI_SLOTS": "3000", "IZPI_CHUNK_UNITS": "5000"},
                                  {"IZPI_NO_LEAF_SHORTCUT": "1"}, {"IZPI_TRACE_CHUNK": "1", "IZPI_REFILL_MIN": "1"},
                                  {"IZPI_TRACE_RING": "8", "IZPI_TRACE_WPE": "5"},
-                                 {"IZPI_TRACE_DIST": "0"}, {"IZPI_TRACE_DIST": "1", "IZPI_TRACE_WPE": "4"}])
+                                 {"IZPI_TRACE_DIST": "0"}, {"IZPI_TRACE_DIST": "1", "IZPI_TRACE_WPE": "4"},
+                                 {"IZPI_TAIL": "0"}, {"IZPI_TAIL": "0", "IZPI_SLOTS": "3000"},
+                                 {"IZPI_TRACE_NO_TRI": "1"}])
 def test_kernel_variants_bitwise(gpu, env, monkeypatch):
-    """Traversal kernel variants, the LDS-ring spill path, step weights and tiny
-    slot/chunk counts are launch knobs only: results and counters must not move."""
+    """Traversal kernel variants, the LDS-ring spill path, step weights, tiny
+    slot/chunk counts, the sphere-capable instance and the pass loop without the k_tail
+    finish are launch knobs only: results and counters must not move."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     scene = configs.cornell_dragon(1.0, n=60)
