@@ -989,30 +989,47 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
     out[0] = 0.0; out[1] = 0.0; out[2] = 0.0;
     return;
   }
-  for (int dd = (int)P.depth - 1; dd >= 0; dd--) {
-    const double* r = rec_ptr<SAMPLER>(sp, slot, (uint32_t)dd);
-    const bool spec = r[0] != 0.0;
-    if (SAMPLER == IZPI_SAMPLER_COLOUR) {
-      V3 att = mk(r[1], r[2], r[3]);
-      if (spec) {
-        L = mul(att, L);                                   // vec3.Mul(att, Sample(...))
-      } else {
-        const double s = r[4], p = r[5];
-        V3 v1 = smul(L, s);                                // ScalarMul(Sample(...), ScatteringPDF)
-        V3 v2 = mul(att, v1);
-        V3 v3 = sdiv(v2, p);
-        L = mk(0.0 + v3.x, 0.0 + v3.y, 0.0 + v3.z);        // Add(emitted == 0, v3)
+  // The records are read four levels at a time (one batch of independent loads, then
+  // the levels applied in order), so a path of depth d waits ~d/4 memory round trips.
+  constexpr uint32_t D = RecLayout<SAMPLER>::D;
+  constexpr int RB = 4;
+  for (int dd = (int)P.depth - 1; dd >= 0; dd -= RB) {
+    double rv[RB][D];
+#pragma unroll
+    for (int j = 0; j < RB; j++) {
+      if (dd - j >= 0) {
+        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER>(sp, slot, (uint32_t)(dd - j)));
+#pragma unroll
+        for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
       }
-    } else {
-      const double att = r[1];
-      if (spec) {
-        L.x = att * L.x;
+    }
+#pragma unroll
+    for (int j = 0; j < RB; j++) {
+      if (dd - j < 0) break;
+      const double* r = rv[j];
+      const bool spec = r[0] != 0.0;
+      if (SAMPLER == IZPI_SAMPLER_COLOUR) {
+        V3 att = mk(r[1], r[2], r[3]);
+        if (spec) {
+          L = mul(att, L);                                   // vec3.Mul(att, Sample(...))
+        } else {
+          const double s = r[4], p = r[5];
+          V3 v1 = smul(L, s);                                // ScalarMul(Sample(...), ScatteringPDF)
+          V3 v2 = mul(att, v1);
+          V3 v3 = sdiv(v2, p);
+          L = mk(0.0 + v3.x, 0.0 + v3.y, 0.0 + v3.z);        // Add(emitted == 0, v3)
+        }
       } else {
-        const double s = r[2], p = r[3];
-        double v1 = L.x * s;
-        double v2 = att * v1;
-        double v3 = v2 / p;
-        L.x = 0.0 + v3;
+        const double att = r[1];
+        if (spec) {
+          L.x = att * L.x;
+        } else {
+          const double s = r[2], p = r[3];
+          double v1 = L.x * s;
+          double v2 = att * v1;
+          double v3 = v2 / p;
+          L.x = 0.0 + v3;
+        }
       }
     }
   }
@@ -1469,7 +1486,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
 
 // One shading pass over the slots traced in the previous k_trace.
 #ifndef IZPI_SHADE_WPE
-#define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (no spill)
+#define IZPI_SHADE_WPE 4  // MATSET_BASIC colour register budget: 4 waves/SIMD (measured 4% faster than 3 despite ~26 spilled VGPRs; 5 is 20% slower)
 #endif
 #ifndef IZPI_SHADE_WPE_OTHER
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
