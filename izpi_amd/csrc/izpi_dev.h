@@ -47,11 +47,15 @@ struct alignas(16) GPrim {
   uint32_t index;   // transport-order index (shading data, lights)
 };
 // Shading record of a primitive, in BVH leaf order next to GPrim: everything the
-// deferred hit record needs for a constant-textured triangle in one 32-B line.
-struct alignas(32) GShade {
+// deferred hit record and a constant-textured Lambert / DiffuseLight bounce need, in one
+// 64-B line (the material and texture records are then not read).
+struct alignas(64) GShade {
   double n[3];      // triangle: unit(e1 x e2) (triangle.go:100); sphere: unused
   uint32_t mat;     // material index
   uint32_t ref;     // IZPI_PRIM_REF(kind, transport index)
+  double c[3];      // value of the material's constant RGB albedo / emit texture (cflags bit0)
+  uint32_t kind;    // material kind (izpi_material.kind)
+  uint32_t cflags;  // bit0: c is valid; bit1: a texture of the material reads the hit (u,v)
 };
 // Light record (Scene.Lights entry, transport order): everything PDFValue/Random read.
 struct alignas(16) GLight {

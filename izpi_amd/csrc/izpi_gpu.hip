@@ -49,7 +49,8 @@ __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
-       CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH, CNT_N };  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
+       CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
+       CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 
 // ======================================================= textures / spectra
@@ -1345,14 +1346,18 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
     const GShade gs = sc.shade[H.prim];
     HitRec h;
     const double rtime = IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_SPHERE ? wp.raux[slot].time : 0.0;
-    hit_record(sc, H, wp.huv + slot, gs, ro, rd, rtime, (sc.mat_flags[gs.mat] & 1u) != 0, h);
+    hit_record(sc, H, wp.huv + slot, gs, ro, rd, rtime, (gs.cflags & 2u) != 0, h);
     hit_n = h.n;
     next_o = h.p;
+    // the shade record carries the material kind and, for a constant RGB texture, its
+    // value: the common Lambert/light hit reads no material or texture record
     const izpi_material& m = sc.materials[h.mat];
-    switch (m.kind) {
+    const bool cconst = COLOUR && (gs.cflags & 1u) != 0;
+    switch (gs.kind) {
       case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
         if (dot(h.n, rd) < 0.0) {
-          if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+          if (cconst) L = mk(gs.c[0], gs.c[1], gs.c[2]);
+          else if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
           else L.x = tex_spectral(sc, m.spectral_tex, P.lambda);
         }
         terminal = true;
@@ -1362,7 +1367,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
         rng.next();
         rng.next();
         cos_onb.build(h.n);
-        if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+        if (cconst) att = mk(gs.c[0], gs.c[1], gs.c[2]);
+        else if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
         else att.x = tex_spectral(sc, m.spectral_tex, P.lambda);
         have_pdf = true;
         break;
@@ -1499,6 +1505,9 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const uint32_t n = *wp.q_in_count;
   uint32_t c_lt = 0, c_ls = 0;
   const uint32_t stride = gridDim.x * 256;
+#ifdef IZPI_SHADE_CLOCKS
+  uint64_t k_item = 0, k_ref = 0, k_push = 0;
+#endif
   // Block-uniform trip count: the queue and unit reservations are block-wide.
   for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
     const uint32_t i = base + threadIdx.x;
@@ -1506,7 +1515,15 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     uint32_t slot = valid ? wp.q_in[i] : 0;
     bool push = false;      // slot has a ray to trace next
     bool done = false;      // slot's sample finished: grab a new unit
+#ifdef IZPI_SHADE_CLOCKS
+    uint64_t t0 = __builtin_readcyclecounter();
+#endif
     if (valid) shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, push, done, c_lt, c_ls);
+#ifdef IZPI_SHADE_CLOCKS
+    uint64_t t1 = __builtin_readcyclecounter();
+    k_item += t1 - t0;
+    t0 = t1;
+#endif
 #if IZPI_SPLIT_REFILL
     {  // finished slots go to the free list; k_refill gives them new units
       const uint32_t fpos = block_reserve(wp.free_count, done, parity);
@@ -1515,10 +1532,26 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 #else
     refill_block<SAMPLER>(sc, sp, wp, slot, done, push, parity);
 #endif
+#ifdef IZPI_SHADE_CLOCKS
+    t1 = __builtin_readcyclecounter();
+    k_ref += t1 - t0;
+    t0 = t1;
+#endif
     const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
     if (push) wp.q_out[pos] = slot;
+#ifdef IZPI_SHADE_CLOCKS
+    t1 = __builtin_readcyclecounter();
+    k_push += t1 - t0;
+#endif
   }
   const uint32_t lane = threadIdx.x & 63;
+#ifdef IZPI_SHADE_CLOCKS
+  if (lane == 0) {
+    atomicAdd(sp.counters + CNT_SCLK_ITEM, (unsigned long long)k_item);
+    atomicAdd(sp.counters + CNT_SCLK_REFILL, (unsigned long long)k_ref);
+    atomicAdd(sp.counters + CNT_SCLK_PUSH, (unsigned long long)k_push);
+  }
+#endif
   unsigned long long vals[2] = {c_lt, c_ls};
   const int idx[2] = {CNT_LTRI, CNT_LSPH};
   for (int k = 0; k < 2; k++) {
@@ -2139,6 +2172,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches; s.tail_ms = tail_ms;
   s.node_steps = cnt[CNT_NSTEP]; s.prim_steps = cnt[CNT_PSTEP]; s.leaf_shortcuts = cnt[CNT_SHORT];
   s.tail_node_visits = cnt[CNT_TAIL_NODES]; s.tail_tri_tests = cnt[CNT_TAIL_TRI]; s.tail_sph_tests = cnt[CNT_TAIL_SPH];
+#ifdef IZPI_SHADE_CLOCKS
+  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu (wave cycles)\n", cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL],
+          cnt[CNT_SCLK_PUSH]);
+#endif
 #ifdef IZPI_TRACE_CLOCKS
   fprintf(stderr, "IZPI_TRACE_CLOCKS refill %llu node %llu prim %llu advance %llu (wave cycles)\n", cnt[CNT_CLK_REFILL],
           cnt[CNT_CLK_NODE], cnt[CNT_CLK_PRIM], cnt[CNT_CLK_ADV]);
@@ -2339,6 +2376,18 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     if (m.kind != IZPI_MAT_LAMBERT && m.kind != IZPI_MAT_DIFFUSE_LIGHT) ctx->basic_materials = false;
     if (rgb) mflags[i] |= 2u; else ctx->mat_ok_rgb = false;
     if (spec) mflags[i] |= 4u; else ctx->mat_ok_spectral = false;
+  }
+  // ---- material essentials in the per-primitive shade records
+  for (GShade& gs : shade) {
+    if (gs.mat >= d->num_materials) { ctx->err = "material index out of range"; return IZPI_ERR_INVALID; }
+    const izpi_material& m = d->materials[gs.mat];
+    gs.kind = m.kind;
+    gs.cflags = (mflags[gs.mat] & 1u) ? 2u : 0u;
+    if ((m.kind == IZPI_MAT_LAMBERT || m.kind == IZPI_MAT_DIFFUSE_LIGHT) && m.albedo_tex >= 0 &&
+        d->textures[m.albedo_tex].kind == IZPI_TEX_CONSTANT) {
+      memcpy(gs.c, d->textures[m.albedo_tex].value, 24);
+      gs.cflags |= 1u;
+    }
   }
   // ---- upload
   DevScene& sc = ctx->sc;
