@@ -40,6 +40,9 @@ def parse():
     p.add_argument("--spp", type=int, default=None, help="override spp (debug only; the metric uses 512)")
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--scene", default=None, help="render a transport.Scene file (.pbtxt/.izpi) at the config's size")
+    p.add_argument("--obj", default=None, help="C3 with this OBJ mesh (e.g. the Stanford dragon) instead of the "
+                                               "synthetic one")
     return p.parse_args()
 
 
@@ -114,6 +117,15 @@ def main():
     spp = args.spp or cfg.spp
     t0 = time.time()
     scene = cfg.build()
+    if args.scene:  # leader.go:43-112: file scene, SPECTRAL scenes use the spectral sampler
+        from izpi_amd import ingest
+        scene = ingest.ProtoScene.from_file(args.scene)
+        cfg = configs.Config("%s (%s)" % (cfg.name, Path(args.scene).name), cfg.width, cfg.height, cfg.spp,
+                             scene.sampler, None, cfg.max_depth)
+    elif args.obj:
+        scene = configs.cornell_obj(args.obj, cfg.width / cfg.height)
+        cfg = configs.Config("%s (mesh %s)" % (cfg.name, Path(args.obj).name), cfg.width, cfg.height, cfg.spp,
+                             cfg.sampler, None, cfg.max_depth)
     r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=local)
     setup_s = time.time() - t0
 

@@ -77,8 +77,112 @@ double izpi_host_gomath(int op, double x, double y);
 
 /* sizeof() of the boundary structs: 0 izpi_bvh4_node 1 izpi_texture 2 izpi_material
  * 3 izpi_camera 4 izpi_scene_desc 5 izpi_render_req 6 izpi_render_stats 7 izpi_hit
- * 8 izpi_tri_in 9 izpi_sphere_in 10 izpi_camera_in 11 izpi_scene_input (0 = unknown). */
+ * 8 izpi_tri_in 9 izpi_sphere_in 10 izpi_camera_in 11 izpi_scene_input 12 izpi_proto_info
+ * 13 izpi_obj_info 14 izpi_obj_group 15 izpi_obj_material (0 = unknown). */
 uint32_t izpi_abi_struct_size(int which);
+
+/* ======================================================================
+ * Scene ingestion — for hosts without Go.
+ * In the Go integration these steps stay in Go (prototext/proto + transport).
+ * ====================================================================== */
+
+/* transport.Scene, parsed from the text (.pbtxt, prototext.Unmarshal, leader.go:64-71)
+ * or binary (.izpi, proto.Unmarshal, leader.go:56-63) encoding of transport.proto.
+ * Text format follows prototext: unknown fields, a repeated singular field and two
+ * members of one oneof are errors. Binary: unknown fields are skipped. */
+typedef struct izpi_proto_scene izpi_proto_scene;
+
+enum { IZPI_COLOUR_RGB = 1, IZPI_COLOUR_SPECTRAL = 2 }; /* transport.proto ColourRepresentation */
+
+typedef struct izpi_proto_info {
+  uint32_t colour_representation; /* IZPI_COLOUR_*, 0 = unspecified */
+  uint32_t stream_triangles;
+  uint64_t total_triangles;
+  uint32_t num_triangles;          /* Scene.objects.triangles (embedded) */
+  uint32_t num_streamed_triangles; /* added with izpi_scene_add_triangles */
+  uint32_t num_spheres, num_materials, num_image_textures, num_displacement_maps;
+  uint32_t num_background;         /* spectral_background entries */
+  uint32_t pad;
+  const char* name;
+  const char* version;
+  const char* warnings;            /* e.g. unknown light source -> CIE A (transport.go:474-478) */
+} izpi_proto_info;
+
+int izpi_scene_parse_text(const char* text, uint64_t len, izpi_proto_scene** out);
+int izpi_scene_parse_binary(const void* buf, uint64_t len, izpi_proto_scene** out);
+int izpi_scene_info(const izpi_proto_scene* s, izpi_proto_info* out);
+/* Filenames of Scene.image_textures, which the host decodes (leader.go:84-98)... */
+const char* izpi_scene_image_file(const izpi_proto_scene* s, uint32_t i);
+/* ...and hands over as float64 NRGBA texels, row 0 = top (texture.ImageTxt). */
+int izpi_scene_set_image(izpi_proto_scene* s, const char* filename, uint32_t width, uint32_t height, const double* rgba);
+/* Streamed triangles (transport.go:574-583, e.g. from izpi_obj_group_to_triangles);
+ * `material` of each izpi_tri_in is ignored, the name is resolved at conversion. */
+int izpi_scene_add_triangles(izpi_proto_scene* s, const izpi_tri_in* tris, uint64_t n, const char* material_name);
+/* Scene.spectral_background; returns its length, copies up to max entries. */
+uint32_t izpi_scene_background(const izpi_proto_scene* s, double* wavelengths, double* values, uint32_t max);
+/* transport.ToScene (transport.go:53-92) up to the BVH build: materials (registered by
+ * Material.name), textures, light-source library, camera, embedded then streamed
+ * triangles, spheres. *out stays valid until the next call or izpi_scene_free; pass
+ * it to izpi_host_build_scene. */
+int izpi_scene_to_input(izpi_proto_scene* s, double aspect_override, uint64_t bvh_seed, const izpi_scene_input** out);
+/* name of material i of the last izpi_scene_to_input */
+const char* izpi_scene_material_name(const izpi_proto_scene* s, uint32_t i);
+void izpi_scene_free(izpi_proto_scene* s);
+
+/* lightsources.GetLightSource (lightsources.go:472-475): copies the 75 values at the CIE
+ * wavelengths (blackbody entries computed as spectral.NewBlackbodySPD); returns 75, or
+ * 0 if the name is unknown. izpi_light_source_name(i) enumerates the library. */
+uint32_t izpi_light_source(const char* name, double* values);
+const char* izpi_light_source_name(uint32_t i);
+
+/* Wavefront OBJ (wavefront.go:107-625). */
+typedef struct izpi_obj izpi_obj;
+#define IZPI_OBJ_IGNORE_NORMALS 1u   /* ParseOption IGNORE_NORMALS */
+#define IZPI_OBJ_IGNORE_MATERIALS 2u /* IGNORE_MATERIALS: mtllib lines are skipped */
+#define IZPI_OBJ_IGNORE_TEXTURES 4u  /* IGNORE_TEXTURES */
+#define IZPI_OBJ_FACE_POLYGON 1u     /* ObjFaceType OBJ_FACE_TYPE_POLYGON */
+
+typedef struct izpi_obj_info {
+  uint32_t has_normals, has_uv, ignore_materials, ignore_normals, ignore_textures;
+  uint32_t num_groups, num_materials, pad;
+  uint64_t num_vertices, num_normals, num_uvs;
+  double centre[3];
+  const char* object_name;
+} izpi_obj_info;
+
+typedef struct izpi_obj_group {
+  const char* name;
+  const char* material;
+  uint32_t face_type;
+  uint32_t is_null;                /* the trailing nil group of a file without faces */
+  uint64_t num_faces;
+  uint64_t num_face_vertices;
+} izpi_obj_group;
+
+typedef struct izpi_obj_material { /* wavefront.Material; Kd/Ka/Ks up to 3 values */
+  const char* name;
+  double kd[3], ka[3], ks[3];
+  uint32_t num_kd, num_ka, num_ks, pad;
+  double ns, ni, d;
+  int64_t sharpness, illum;
+} izpi_obj_material;
+
+/* NewObjFromReader: mtllib files are read from container_dir (wavefront.go:193-204). */
+int izpi_obj_parse(const char* text, uint64_t len, const char* container_dir, uint32_t options, izpi_obj** out);
+int izpi_obj_info_get(const izpi_obj* o, izpi_obj_info* out);
+int izpi_obj_copy_vertices(const izpi_obj* o, double* v, double* vn, double* vt);
+int izpi_obj_group_get(const izpi_obj* o, uint32_t g, izpi_obj_group* out);
+/* per face its vertex count; per face vertex (VIdx, VtIdx, VnIdx) as in the file (1-based) */
+int izpi_obj_copy_faces(const izpi_obj* o, uint32_t g, uint32_t* face_sizes, int64_t* indices);
+/* materials in name order */
+int izpi_obj_material_get(const izpi_obj* o, uint32_t i, izpi_obj_material* out);
+void izpi_obj_translate(izpi_obj* o, double x, double y, double z);
+void izpi_obj_scale(izpi_obj* o, double x, double y, double z);
+void izpi_obj_rotate(izpi_obj* o, double alpha, double beta, double gamma);
+/* GroupToTransportTrianglesWithMaterial (wavefront.go:240-312); out = NULL: count only */
+int izpi_obj_group_to_triangles(const izpi_obj* o, uint32_t g, uint32_t without_uvs, izpi_tri_in* out, uint64_t max,
+                                uint64_t* n);
+void izpi_obj_free(izpi_obj* o);
 
 #ifdef __cplusplus
 }

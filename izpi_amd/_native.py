@@ -125,8 +125,41 @@ class SceneInput(C.Structure):
                 ("aspect_override", C.c_double), ("bvh_seed", C.c_uint64)]
 
 
+COLOUR_RGB, COLOUR_SPECTRAL = 1, 2
+OBJ_IGNORE_NORMALS, OBJ_IGNORE_MATERIALS, OBJ_IGNORE_TEXTURES = 1, 2, 4
+OBJ_FACE_POLYGON = 1
+
+
+class ProtoInfo(C.Structure):
+    _fields_ = [("colour_representation", C.c_uint32), ("stream_triangles", C.c_uint32),
+                ("total_triangles", C.c_uint64), ("num_triangles", C.c_uint32), ("num_streamed_triangles", C.c_uint32),
+                ("num_spheres", C.c_uint32), ("num_materials", C.c_uint32), ("num_image_textures", C.c_uint32),
+                ("num_displacement_maps", C.c_uint32), ("num_background", C.c_uint32), ("pad", C.c_uint32),
+                ("name", C.c_char_p), ("version", C.c_char_p), ("warnings", C.c_char_p)]
+
+
+class ObjInfo(C.Structure):
+    _fields_ = [("has_normals", C.c_uint32), ("has_uv", C.c_uint32), ("ignore_materials", C.c_uint32),
+                ("ignore_normals", C.c_uint32), ("ignore_textures", C.c_uint32), ("num_groups", C.c_uint32),
+                ("num_materials", C.c_uint32), ("pad", C.c_uint32), ("num_vertices", C.c_uint64),
+                ("num_normals", C.c_uint64), ("num_uvs", C.c_uint64), ("centre", C.c_double * 3),
+                ("object_name", C.c_char_p)]
+
+
+class ObjGroup(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("material", C.c_char_p), ("face_type", C.c_uint32), ("is_null", C.c_uint32),
+                ("num_faces", C.c_uint64), ("num_face_vertices", C.c_uint64)]
+
+
+class ObjMaterial(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("kd", C.c_double * 3), ("ka", C.c_double * 3), ("ks", C.c_double * 3),
+                ("num_kd", C.c_uint32), ("num_ka", C.c_uint32), ("num_ks", C.c_uint32), ("pad", C.c_uint32),
+                ("ns", C.c_double), ("ni", C.c_double), ("d", C.c_double), ("sharpness", C.c_int64),
+                ("illum", C.c_int64)]
+
+
 ABI_STRUCTS = [BVH4Node, Texture, Material, Camera, SceneDesc, RenderReq, RenderStats, Hit, TriIn, SphereIn, CameraIn,
-               SceneInput]
+               SceneInput, ProtoInfo, ObjInfo, ObjGroup, ObjMaterial]
 
 # Symbols include/izpi_gpu.h and include/izpi_host.h declare (checked by tests).
 EXPORTS = [
@@ -135,6 +168,12 @@ EXPORTS = [
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
+    "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_info", "izpi_scene_image_file",
+    "izpi_scene_set_image", "izpi_scene_add_triangles", "izpi_scene_background", "izpi_scene_to_input",
+    "izpi_scene_material_name", "izpi_scene_free", "izpi_light_source", "izpi_light_source_name",
+    "izpi_obj_parse", "izpi_obj_info_get", "izpi_obj_copy_vertices", "izpi_obj_group_get", "izpi_obj_copy_faces",
+    "izpi_obj_material_get", "izpi_obj_translate", "izpi_obj_scale", "izpi_obj_rotate",
+    "izpi_obj_group_to_triangles", "izpi_obj_free",
 ]
 
 _lib = None
@@ -181,5 +220,37 @@ def lib():
     L.izpi_host_gomath.restype = C.c_double
     L.izpi_abi_struct_size.argtypes = [C.c_int]
     L.izpi_abi_struct_size.restype = C.c_uint32
+    # scene ingestion (izpi_host.h)
+    vp, vpp = C.c_void_p, C.POINTER(C.c_void_p)
+    L.izpi_scene_parse_text.argtypes = [C.c_char_p, C.c_uint64, vpp]
+    L.izpi_scene_parse_binary.argtypes = [C.c_char_p, C.c_uint64, vpp]
+    L.izpi_scene_info.argtypes = [vp, C.POINTER(ProtoInfo)]
+    L.izpi_scene_image_file.argtypes = [vp, C.c_uint32]
+    L.izpi_scene_image_file.restype = C.c_char_p
+    L.izpi_scene_set_image.argtypes = [vp, C.c_char_p, C.c_uint32, C.c_uint32, c_double_p]
+    L.izpi_scene_add_triangles.argtypes = [vp, vp, C.c_uint64, C.c_char_p]
+    L.izpi_scene_background.argtypes = [vp, c_double_p, c_double_p, C.c_uint32]
+    L.izpi_scene_background.restype = C.c_uint32
+    L.izpi_scene_to_input.argtypes = [vp, C.c_double, C.c_uint64, C.POINTER(C.POINTER(SceneInput))]
+    L.izpi_scene_material_name.argtypes = [vp, C.c_uint32]
+    L.izpi_scene_material_name.restype = C.c_char_p
+    L.izpi_scene_free.argtypes = [vp]
+    L.izpi_scene_free.restype = None
+    L.izpi_light_source.argtypes = [C.c_char_p, c_double_p]
+    L.izpi_light_source.restype = C.c_uint32
+    L.izpi_light_source_name.argtypes = [C.c_uint32]
+    L.izpi_light_source_name.restype = C.c_char_p
+    L.izpi_obj_parse.argtypes = [C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint32, vpp]
+    L.izpi_obj_info_get.argtypes = [vp, C.POINTER(ObjInfo)]
+    L.izpi_obj_copy_vertices.argtypes = [vp, c_double_p, c_double_p, c_double_p]
+    L.izpi_obj_group_get.argtypes = [vp, C.c_uint32, C.POINTER(ObjGroup)]
+    L.izpi_obj_copy_faces.argtypes = [vp, C.c_uint32, c_uint32_p, C.POINTER(C.c_int64)]
+    L.izpi_obj_material_get.argtypes = [vp, C.c_uint32, C.POINTER(ObjMaterial)]
+    for f in ("izpi_obj_translate", "izpi_obj_scale", "izpi_obj_rotate"):
+        getattr(L, f).argtypes = [vp, C.c_double, C.c_double, C.c_double]
+        getattr(L, f).restype = None
+    L.izpi_obj_group_to_triangles.argtypes = [vp, C.c_uint32, C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.izpi_obj_free.argtypes = [vp]
+    L.izpi_obj_free.restype = None
     _lib = L
     return L

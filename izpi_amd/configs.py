@@ -185,6 +185,47 @@ def cornell_glass_spectral(aspect=1.0):
     return s
 
 
+def cornell_rgb_pbtxt(aspect=1.0):
+    """The RGB Cornell box of C1 as transport.Scene text (the format the C++ ingestion
+    reads; RGB materials of scenes.CornellBoxRGB, scenes.go:934)."""
+    def v(name, p):
+        return "%s { x: %r y: %r z: %r }" % (name, float(p[0]), float(p[1]), float(p[2]))
+    out = ['name: "cornell_rgb"', "colour_representation: RGB",
+           "camera { %s %s %s vfov: 40 aspect: %r focusdist: 10 time1: 1 exposure: 1 }"
+           % (v("lookfrom", (50, 50, -140)), v("lookat", (50, 50, 0)), v("vup", (0, 1, 0)), float(aspect))]
+    for name, rgb, kind in (("White", (0.73, 0.73, 0.73), "lambert"), ("Green", (0, 0.73, 0), "lambert"),
+                            ("Red", (0.73, 0, 0), "lambert"), ("light", (15, 15, 15), "diffuselight")):
+        prop = "lambert { albedo { constant { %s } } }" % v("value", rgb) if kind == "lambert" else \
+            "diffuselight { emit { constant { %s } } }" % v("value", rgb)
+        out.append('materials { key: "%s" value { name: "%s" type: %s %s } }'
+                   % (name, name, "LAMBERT" if kind == "lambert" else "DIFFUSE_LIGHT", prop))
+    tris = []
+    for v0, v1, v2, m, uv in _BOX:
+        t = "triangles { %s %s %s" % (v("vertex0", v0), v("vertex1", v1), v("vertex2", v2))
+        if uv is not None:
+            t += " uv0 { u: %r v: %r } uv1 { u: %r v: %r } uv2 { u: %r v: %r }" % tuple(float(c) for p in uv for c in p)
+        tris.append(t + ' material_name: "%s" }' % m)
+    out.append("objects {\n  %s\n}" % "\n  ".join(tris))
+    return "\n".join(out) + "\n"
+
+
+def cornell_obj(path, aspect=1.0):
+    """C3 with a mesh from a Wavefront OBJ file (e.g. the Stanford dragon, which the
+    reference loads from meshes/dragon_tri.obj and this checkout lacks): parsed and
+    transformed as scenes/spectral.go:639-657 does (Scale 90, Rotate Y -60 deg,
+    Translate (50, 25.1, 60), GroupToTransportTrianglesWithMaterial WITHOUT_UVS), then
+    streamed into the RGB Cornell box with the White Lambert material."""
+    from . import ingest
+    mesh = ingest.WavefrontObj.from_file(path)
+    mesh.scale(90.0, 90.0, 90.0)
+    mesh.rotate(0.0, -ingest.go_radians(60), 0.0)
+    mesh.translate(50.0, 25.1, 60.0)
+    scene = ingest.ProtoScene(cornell_rgb_pbtxt(aspect).encode())
+    for g in range(mesh.info()["num_groups"]):
+        scene.add_triangles(mesh.group_to_transport_triangles(g, without_uvs=True), "White")
+    return scene
+
+
 @dataclass
 class Config:
     name: str

@@ -325,6 +325,10 @@ struct izpi_host_scene {
   double build_ms = 0;
 };
 
+namespace izpi_internal {
+void set_host_error(const std::string& s) { g_err = s; }
+}
+
 extern "C" {
 
 const char* izpi_host_last_error(void) { return g_err.c_str(); }
@@ -522,6 +526,10 @@ uint32_t izpi_abi_struct_size(int which) {
     case 9: return sizeof(izpi_sphere_in);
     case 10: return sizeof(izpi_camera_in);
     case 11: return sizeof(izpi_scene_input);
+    case 12: return sizeof(izpi_proto_info);
+    case 13: return sizeof(izpi_obj_info);
+    case 14: return sizeof(izpi_obj_group);
+    case 15: return sizeof(izpi_obj_material);
   }
   return 0;
 }
