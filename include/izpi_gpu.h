@@ -98,7 +98,15 @@ typedef struct izpi_render_req {
 /* Post-processing applied by Render for the Spectral sampler (renderer.go:215-219):
  * spectral.FireflyRejection (firefly_rejection.go:12-113) then spectral.XYZToRGB
  * (rgb_image.go:28-67, ACEScg matrix :13-17) with req->exposure. */
-enum { IZPI_POST_NONE = 0, IZPI_POST_SPECTRAL = 1 };
+enum { IZPI_POST_NONE = 0, IZPI_POST_SPECTRAL = 1,
+       /* bit 2: the leader's "png" output pipeline, Gamma then Clamp(1.0) (leader.go:179-182),
+        * after the spectral post when both are set */
+       IZPI_POST_GAMMA_CLAMP = 2 };
+
+/* postprocess.Filter kinds for izpi_gpu_postprocess (postprocess/api.go:10-14) */
+enum { IZPI_FILTER_GAMMA = 1, /* gamma.go:24-41, R,G,B = math.Sqrt; param unused */
+       IZPI_FILTER_CLAMP = 2  /* clamp.go:27-51, v < max ? v : max; param = max */ };
+#define IZPI_MAX_FILTERS 8
 
 /* Per-render counters. The traversal is bit-identical to the CPU restatement, so
  * these equal the oracle's counts exactly (used for algorithmic bytes, §8(d)). */
@@ -162,6 +170,11 @@ int izpi_gpu_unpack_tiles(izpi_ctx* ctx, const izpi_render_req* req, const doubl
  * rank 0 after the gather. */
 int izpi_gpu_spectral_post(izpi_ctx* ctx, const double* xyz_dev, double* rgba_dev, uint32_t width, uint32_t height,
                            double exposure);
+
+/* postprocess.Pipeline.Apply (pipeline.go:20-31) on a W*H*4 float64 canvas in device
+ * memory, in place: filters[i] (IZPI_FILTER_*) with params[i], in list order. */
+int izpi_gpu_postprocess(izpi_ctx* ctx, double* canvas_dev, uint32_t width, uint32_t height, const uint32_t* filters,
+                         const double* params, uint32_t num_filters);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);

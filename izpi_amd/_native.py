@@ -23,7 +23,9 @@ MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_LAMBERT, MAT_METAL, MAT_PBR = 1, 2, 4, 5,
 MATF_BEER_LAMBERT = 1
 SAMPLER_COLOUR, SAMPLER_SPECTRAL = 2, 5
 OUT_CANVAS, OUT_PACKED = 0, 1
-POST_NONE, POST_SPECTRAL = 0, 1
+POST_NONE, POST_SPECTRAL, POST_GAMMA_CLAMP = 0, 1, 2
+FILTER_GAMMA, FILTER_CLAMP = 1, 2
+MAX_FILTERS = 8
 
 
 def prim_ref(kind, idx):
@@ -165,7 +167,7 @@ ABI_STRUCTS = [BVH4Node, Texture, Material, Camera, SceneDesc, RenderReq, Render
 EXPORTS = [
     "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
     "izpi_gpu_render_device", "izpi_gpu_unpack_tiles", "izpi_gpu_output_bytes", "izpi_gpu_trace",
-    "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post",
+    "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_info", "izpi_scene_image_file",
@@ -205,6 +207,8 @@ def lib():
     L.izpi_gpu_ray_aabb4.argtypes = [C.c_void_p, c_float_p, c_float_p, C.c_uint32, C.POINTER(C.c_uint8)]
     L.izpi_gpu_gomath.argtypes = [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_uint32, c_double_p]
     L.izpi_gpu_spectral_post.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double]
+    L.izpi_gpu_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, c_uint32_p, c_double_p,
+                                       C.c_uint32]
     L.izpi_host_build_scene.argtypes = [C.POINTER(SceneInput), C.POINTER(C.c_void_p)]
     L.izpi_host_scene_desc.argtypes = [C.c_void_p]
     L.izpi_host_scene_desc.restype = C.POINTER(SceneDesc)

@@ -1695,6 +1695,35 @@ __global__ void __launch_bounds__(256) k_spectral_post(const double* in, double*
   *reinterpret_cast<double2*>(out + pi + 2) = ba;
 }
 
+// postprocess.Pipeline (pipeline.go:20-31) of Gamma (gamma.go:24-41: R,G,B = math.Sqrt)
+// and Clamp (clamp.go:27-51: v < max ? v : max, so NaN -> max) filters, applied in list
+// order to each pixel; alpha unchanged. The reference walks x <= Max.X, y <= Max.Y: the
+// extra row/column reads zero and its Set is dropped, so only in-bounds pixels change.
+// HBM-streaming, 32 B in + 32 B out per pixel.
+struct PostFilters {
+  uint32_t n;
+  uint32_t kind[IZPI_MAX_FILTERS];
+  double param[IZPI_MAX_FILTERS];
+};
+
+__global__ void __launch_bounds__(256) k_postprocess(double* canvas, uint64_t num_pixels, const PostFilters pf) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= num_pixels) return;
+  double2* p = reinterpret_cast<double2*>(canvas + i * 4);
+  double2 rg = p[0], ba = p[1];
+  double c[3] = {rg.x, rg.y, ba.x};
+  for (uint32_t f = 0; f < pf.n; f++) {
+    if (pf.kind[f] == IZPI_FILTER_GAMMA) {
+      for (int k = 0; k < 3; k++) c[k] = gm::sqrt(c[k]);
+    } else {
+      const double mx = pf.param[f];
+      for (int k = 0; k < 3; k++) c[k] = c[k] < mx ? c[k] : mx;
+    }
+  }
+  p[0] = make_double2(c[0], c[1]);
+  p[1] = make_double2(c[2], ba.y);
+}
+
 __global__ void k_unpack(const uint32_t* tiles, uint32_t num_pixels, uint32_t tile_w, uint32_t tile_h, uint32_t width,
                          uint32_t height, const double* packed, double* canvas) {
   const uint32_t p = blockIdx.x * 256 + threadIdx.x;
@@ -2051,7 +2080,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
   if (req->sampler != IZPI_SAMPLER_COLOUR && req->sampler != IZPI_SAMPLER_SPECTRAL) { ctx->err = "unsupported sampler"; return IZPI_ERR_UNSUPPORTED; }
   if (req->post != IZPI_POST_NONE &&
-      (req->post != IZPI_POST_SPECTRAL || req->out_layout != IZPI_OUT_CANVAS || req->num_tiles != 0)) {
+      ((req->post & ~(uint32_t)(IZPI_POST_SPECTRAL | IZPI_POST_GAMMA_CLAMP)) || req->out_layout != IZPI_OUT_CANVAS ||
+       req->num_tiles != 0)) {
     ctx->err = "post-processing needs a whole-frame IZPI_OUT_CANVAS request";
     return IZPI_ERR_INVALID;
   }
@@ -2149,13 +2179,21 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
 #undef IZPI_RUN
   if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, st));
-  if (req->post == IZPI_POST_SPECTRAL) {  // renderer.go:215-219, outside the timed render like the reference
+  if (req->post & IZPI_POST_SPECTRAL) {  // renderer.go:215-219, outside the timed render like the reference
     if ((rc = grow(ctx, (void**)&ctx->d_post, &ctx->post_cap, (size_t)req->width * req->height * 4 * sizeof(double)))) return rc;
     dim3 g((req->width + 15) / 16, (req->height + 15) / 16);
     hipLaunchKernelGGL(k_spectral_post, g, dim3(256), 0, st, out_dev, ctx->d_post, req->width, req->height, req->exposure);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out_dev, ctx->d_post, (size_t)req->width * req->height * 4 * sizeof(double),
                            hipMemcpyDeviceToDevice, st));
+  }
+  if (req->post & IZPI_POST_GAMMA_CLAMP) {  // leader.go:179-182 ("png" output mode): Gamma, then Clamp(1.0)
+    PostFilters pf;
+    memset(&pf, 0, sizeof pf);
+    pf.n = 2; pf.kind[0] = IZPI_FILTER_GAMMA; pf.kind[1] = IZPI_FILTER_CLAMP; pf.param[1] = 1.0;
+    const uint64_t np = (uint64_t)req->width * req->height;
+    hipLaunchKernelGGL(k_postprocess, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, out_dev, np, pf);
+    HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventSynchronize(ctx->ev1));
   float total_ms = 0;
@@ -2501,6 +2539,33 @@ int izpi_gpu_spectral_post(izpi_ctx* ctx, const double* xyz_dev, double* rgba_de
   HIP_TRY(hipSetDevice(ctx->device));
   dim3 g((width + 15) / 16, (height + 15) / 16);
   hipLaunchKernelGGL(k_spectral_post, g, dim3(256), 0, ctx->stream, xyz_dev, rgba_dev, width, height, exposure);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return IZPI_OK;
+}
+
+int izpi_gpu_postprocess(izpi_ctx* ctx, double* canvas_dev, uint32_t width, uint32_t height, const uint32_t* filters,
+                         const double* params, uint32_t num_filters) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  if (!canvas_dev || num_filters > IZPI_MAX_FILTERS || (num_filters && (!filters || !params))) {
+    ctx->err = "postprocess: bad arguments";
+    return IZPI_ERR_INVALID;
+  }
+  PostFilters pf;
+  memset(&pf, 0, sizeof pf);
+  pf.n = num_filters;
+  for (uint32_t i = 0; i < num_filters; i++) {
+    if (filters[i] != IZPI_FILTER_GAMMA && filters[i] != IZPI_FILTER_CLAMP) {
+      ctx->err = "postprocess: unknown filter (colour grading needs a .cube LUT reader, not on this path)";
+      return IZPI_ERR_UNSUPPORTED;
+    }
+    pf.kind[i] = filters[i];
+    pf.param[i] = params[i];
+  }
+  const uint64_t np = (uint64_t)width * height;
+  if (np == 0 || num_filters == 0) return IZPI_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_postprocess, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, ctx->stream, canvas_dev, np, pf);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return IZPI_OK;

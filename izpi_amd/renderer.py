@@ -94,7 +94,8 @@ class GPURenderer:
     def render(self, tiles=None, canvas=None, spp=None, post=N.POST_NONE):
         """Render.Render(): returns the (H, W, 4) float64 canvas (host memory). With
         post=POST_SPECTRAL (whole frame only) the XYZ canvas goes through
-        FireflyRejection + XYZToRGB on the GPU, as Render does for the Spectral sampler."""
+        FireflyRejection + XYZToRGB on the GPU, as Render does for the Spectral sampler;
+        with POST_GAMMA_CLAMP the leader's png pipeline (Gamma, Clamp(1.0)) follows."""
         if canvas is None:
             canvas = np.zeros((self.height, self.width, 4), np.float64)
         req = self.request(tiles, N.OUT_CANVAS, spp, post)
@@ -114,6 +115,15 @@ class GPURenderer:
         _check(N.lib().izpi_gpu_spectral_post(self.ctx, C.c_void_p(xyz_ptr), C.c_void_p(rgba_ptr), self.width,
                                               self.height, C.c_double(self.exposure)), self.ctx,
                "izpi_gpu_spectral_post")
+
+    def postprocess(self, canvas_ptr, filters):
+        """postprocess.Pipeline.Apply on a device canvas, in place: filters is a list of
+        (N.FILTER_GAMMA | N.FILTER_CLAMP, param) applied in order (pipeline.go:20-31)."""
+        k = np.array([f[0] for f in filters], np.uint32)
+        p = np.array([f[1] for f in filters], np.float64)
+        _check(N.lib().izpi_gpu_postprocess(self.ctx, C.c_void_p(canvas_ptr), self.width, self.height,
+                                            k.ctypes.data_as(N.c_uint32_p), p.ctypes.data_as(N.c_double_p), len(k)),
+               self.ctx, "izpi_gpu_postprocess")
 
     def render_device(self, out_ptr, tiles=None, layout=N.OUT_CANVAS, spp=None):
         """Render into device memory at `out_ptr` (e.g. torch tensor .data_ptr())."""
@@ -156,10 +166,12 @@ class GPURenderer:
             rt = sharding.shard_tiles(all_tiles, r, world)
             if len(rt):
                 self.unpack(rt, gathered[r].data_ptr(), canvas.data_ptr())
-        if post == N.POST_SPECTRAL:
+        if post & N.POST_SPECTRAL:
             rgb = torch.empty_like(canvas)
             self.spectral_post(canvas.data_ptr(), rgb.data_ptr())
             canvas = rgb
+        if post & N.POST_GAMMA_CLAMP:  # leader.go:179-182
+            self.postprocess(canvas.data_ptr(), [(N.FILTER_GAMMA, 0.0), (N.FILTER_CLAMP, 1.0)])
         torch.cuda.synchronize(dev)
         return canvas, self.stats
 

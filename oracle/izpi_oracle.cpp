@@ -1561,6 +1561,21 @@ void oracle_xyz_to_rgb(const double* in, double* out, int width, int height, dou
   }
 }
 
+/* postprocess.Pipeline (pipeline.go:20-31) over the whole canvas, written the way the
+ * reference loops (gamma.go:30-38, clamp.go:33-41): every filter walks every pixel, then
+ * the next filter runs. kind 1 = Gamma (math.Sqrt of R, G, B), 2 = Clamp(max). */
+void oracle_postprocess(double* pix, int width, int height, const uint32_t* kinds, const double* params, int n) {
+  for (int f = 0; f < n; f++)
+    for (int y = 0; y < height; y++)
+      for (int x = 0; x < width; x++) {
+        double* p = pix + ((size_t)y * width + x) * 4;
+        for (int c = 0; c < 3; c++) {
+          if (kinds[f] == 1) p[c] = std::sqrt(p[c]);
+          else if (p[c] >= params[f] || p[c] != p[c]) p[c] = params[f];  /* clamp(): `if v < max {return v}; return max` */
+        }
+      }
+}
+
 /* common.Tiles (tiles.go:6-24) + grid.WalkGrid spiral (grid.go:48-125). */
 uint32_t oracle_tiles(uint32_t W, uint32_t H, uint32_t* tiles, uint32_t max_tiles) {
   static const int steps[] = {32, 25, 24, 20, 16, 12, 10, 8, 5, 4};

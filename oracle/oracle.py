@@ -66,6 +66,8 @@ def lib():
                                 C.c_int]
     L.oracle_firefly.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int]
     L.oracle_xyz_to_rgb.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int, C.c_double]
+    L.oracle_postprocess.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_double), C.c_int]
     L.oracle_tiles.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]
     L.oracle_tiles.restype = C.c_uint32
     L.oracle_sample_wavelength.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -156,6 +158,15 @@ def xyz_to_rgb(canvas, width, height, exposure):
     out = np.zeros_like(src)
     lib().oracle_xyz_to_rgb(dptr(src), dptr(out), width, height, float(exposure))
     return out
+
+
+def postprocess(canvas, width, height, filters):
+    """filters: [(kind, param)], kind 1 = Gamma, 2 = Clamp."""
+    c = np.ascontiguousarray(canvas, np.float64).copy()
+    k = np.array([f[0] for f in filters], np.uint32)
+    p = np.array([f[1] for f in filters], np.float64)
+    lib().oracle_postprocess(dptr(c), width, height, k.ctypes.data_as(C.POINTER(C.c_uint32)), dptr(p), len(filters))
+    return c
 
 
 def tiles(width, height):

@@ -381,3 +381,25 @@ def test_ingested_obj_mesh_bitwise(gpu):
     ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
+
+
+def test_postprocess_kernel_bitwise(gpu):
+    """izpi_gpu_postprocess == the oracle's postprocess.Pipeline restatement, including
+    NaN / negative / infinite inputs; the render flag applies Gamma, Clamp(1.0)."""
+    import torch
+    W, H = 97, 33
+    rng = np.random.default_rng(11)
+    c = rng.uniform(-0.5, 3.0, (H, W, 4))
+    c[0, 0, :3] = [np.nan, np.inf, -0.0]
+    r = GPURenderer(configs.cornell_rgb(), W, H, 2)
+    for filters in ([(N.FILTER_GAMMA, 0.0), (N.FILTER_CLAMP, 1.0)], [(N.FILTER_CLAMP, 0.3)], [(N.FILTER_GAMMA, 0.0)]):
+        d = torch.from_numpy(c.copy()).cuda()
+        r.postprocess(d.data_ptr(), filters)
+        torch.cuda.synchronize()
+        ref = O.postprocess(c.ravel(), W, H, filters).reshape(H, W, 4)
+        assert d.cpu().numpy().tobytes() == ref.tobytes(), filters
+    img = r.render(post=N.POST_GAMMA_CLAMP)
+    raw, _ = oracle_canvas(configs.cornell_rgb(), W, H, 2, N.SAMPLER_COLOUR)
+    ref = O.postprocess(raw.ravel(), W, H, [(1, 0.0), (2, 1.0)]).reshape(H, W, 4)
+    assert img.tobytes() == ref.tobytes()
+    r.close()
