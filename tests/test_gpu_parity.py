@@ -387,7 +387,7 @@ def test_postprocess_kernel_bitwise(gpu):
     """izpi_gpu_postprocess == the oracle's postprocess.Pipeline restatement, including
     NaN / negative / infinite inputs; the render flag applies Gamma, Clamp(1.0)."""
     import torch
-    W, H = 97, 33
+    W, H = 100, 40  # a common.Tiles size (render part)
     rng = np.random.default_rng(11)
     c = rng.uniform(-0.5, 3.0, (H, W, 4))
     c[0, 0, :3] = [np.nan, np.inf, -0.0]
