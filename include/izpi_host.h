@@ -60,6 +60,18 @@ typedef struct izpi_host_scene izpi_host_scene;
 
 /* Build; on failure returns non-zero and *out = NULL. */
 int izpi_host_build_scene(const izpi_scene_input* in, izpi_host_scene** out);
+/* flags: IZPI_HOST_SKIP_BVH leaves the BVH out (num_nodes = 0, primitives in transport
+ * order) for another builder, e.g. izpi_gpu_build_bvh4, to attach with
+ * izpi_host_scene_set_bvh. */
+#define IZPI_HOST_SKIP_BVH 1u
+int izpi_host_build_scene_ex(const izpi_scene_input* in, uint32_t flags, izpi_host_scene** out);
+/* The f64 primitive boxes the BVH is built over ([num_tris + num_spheres][6]: min xyz,
+ * max xyz; triangles first, transport order): Triangle.BoundingBox with its relative
+ * epsilon (triangle.go:100-113), Sphere.BoundingBox (sphere.go). */
+int izpi_host_scene_prim_boxes(const izpi_host_scene* s, double* boxes);
+/* Attach a BVH4 built elsewhere: nodes in BVH4Node format with children after their
+ * parents, order[k] = primitive (triangles then spheres) at leaf position k. */
+int izpi_host_scene_set_bvh(izpi_host_scene* s, const izpi_bvh4_node* nodes, uint32_t num_nodes, const uint32_t* order);
 const izpi_scene_desc* izpi_host_scene_desc(const izpi_host_scene* s);
 /* Max stack depth the traversal of this BVH can reach (host-computed bound). */
 uint32_t izpi_host_scene_stack_bound(const izpi_host_scene* s);

@@ -26,6 +26,7 @@ OUT_CANVAS, OUT_PACKED = 0, 1
 POST_NONE, POST_SPECTRAL, POST_GAMMA_CLAMP = 0, 1, 2
 FILTER_GAMMA, FILTER_CLAMP = 1, 2
 MAX_FILTERS = 8
+HOST_SKIP_BVH = 1
 
 
 def prim_ref(kind, idx):
@@ -168,6 +169,7 @@ EXPORTS = [
     "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
     "izpi_gpu_render_device", "izpi_gpu_unpack_tiles", "izpi_gpu_output_bytes", "izpi_gpu_trace",
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
+    "izpi_gpu_build_bvh4", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_info", "izpi_scene_image_file",
@@ -209,6 +211,11 @@ def lib():
     L.izpi_gpu_spectral_post.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double]
     L.izpi_gpu_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, c_uint32_p, c_double_p,
                                        C.c_uint32]
+    L.izpi_gpu_build_bvh4.argtypes = [C.c_void_p, c_double_p, C.c_uint32, C.c_uint32, C.POINTER(BVH4Node), C.c_uint32,
+                                      c_uint32_p, c_uint32_p, c_double_p]
+    L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]
+    L.izpi_host_scene_prim_boxes.argtypes = [C.c_void_p, c_double_p]
+    L.izpi_host_scene_set_bvh.argtypes = [C.c_void_p, C.POINTER(BVH4Node), C.c_uint32, c_uint32_p]
     L.izpi_host_build_scene.argtypes = [C.POINTER(SceneInput), C.POINTER(C.c_void_p)]
     L.izpi_host_scene_desc.argtypes = [C.c_void_p]
     L.izpi_host_scene_desc.restype = C.POINTER(SceneDesc)

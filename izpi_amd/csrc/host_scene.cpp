@@ -318,6 +318,7 @@ struct izpi_host_scene {
   std::vector<uint32_t> prim_ref, tri_mat, sph_mat, light_ref;
   std::vector<double> v0, v1, v2, e1, e2, nrm, tan, bitan, uv, area;
   std::vector<double> c0, c1, stime, rad;
+  std::vector<double> boxes;  // [prims][6] f64 primitive boxes (transport order), for other BVH builders
   std::vector<izpi_material> mats;
   std::vector<izpi_texture> texs;
   std::vector<double> texels, spd_wl, spd_val;
@@ -334,6 +335,10 @@ extern "C" {
 const char* izpi_host_last_error(void) { return g_err.c_str(); }
 
 int izpi_host_build_scene(const izpi_scene_input* in, izpi_host_scene** out) {
+  return izpi_host_build_scene_ex(in, 0, out);
+}
+
+int izpi_host_build_scene_ex(const izpi_scene_input* in, uint32_t flags, izpi_host_scene** out) {
   *out = nullptr;
   if (!in) { g_err = "null input"; return IZPI_ERR_INVALID; }
   auto t0 = std::chrono::steady_clock::now();
@@ -408,8 +413,15 @@ int izpi_host_build_scene(const izpi_scene_input* in, izpi_host_scene** out) {
   };
   for (uint32_t i = 0; i < nt; i++) if (emitter(in->tris[i].material)) s->light_ref.push_back(IZPI_PRIM_REF(IZPI_PRIM_TRIANGLE, i));
   for (uint32_t i = 0; i < ns; i++) if (emitter(in->spheres[i].material)) s->light_ref.push_back(IZPI_PRIM_REF(IZPI_PRIM_SPHERE, i));
+  s->boxes.resize(6 * boxes.size());
+  for (size_t i = 0; i < boxes.size(); i++)
+    for (int k = 0; k < 3; k++) { s->boxes[6 * i + k] = boxes[i].mn[k]; s->boxes[6 * i + 3 + k] = boxes[i].mx[k]; }
   // --- BVH4 (bvh4.go:517-593)
-  if (nt + ns > 0) {
+  if (flags & IZPI_HOST_SKIP_BVH) {  // another builder attaches its tree (izpi_host_scene_set_bvh)
+    s->prim_ref.resize((size_t)nt + ns);
+    for (uint32_t i = 0; i < nt; i++) s->prim_ref[i] = IZPI_PRIM_REF(IZPI_PRIM_TRIANGLE, i);
+    for (uint32_t i = 0; i < ns; i++) s->prim_ref[(size_t)nt + i] = IZPI_PRIM_REF(IZPI_PRIM_SPHERE, i);
+  } else if (nt + ns > 0) {
     Builder b(boxes, in->bvh_seed);
     int root = b.build(0, (int)(nt + ns));
     std::vector<int> prim_order;
@@ -470,6 +482,44 @@ int izpi_host_build_scene(const izpi_scene_input* in, izpi_host_scene** out) {
 }
 
 const izpi_scene_desc* izpi_host_scene_desc(const izpi_host_scene* s) { return s ? &s->desc : nullptr; }
+
+int izpi_host_scene_prim_boxes(const izpi_host_scene* s, double* boxes) {
+  if (!s || !boxes) { g_err = "null argument"; return IZPI_ERR_INVALID; }
+  if (!s->boxes.empty()) memcpy(boxes, s->boxes.data(), s->boxes.size() * sizeof(double));
+  return IZPI_OK;
+}
+
+int izpi_host_scene_set_bvh(izpi_host_scene* s, const izpi_bvh4_node* nodes, uint32_t num_nodes, const uint32_t* order) {
+  if (!s || (!nodes && num_nodes) || !order) { g_err = "null argument"; return IZPI_ERR_INVALID; }
+  const uint32_t np = s->desc.num_tris + s->desc.num_spheres, nt = s->desc.num_tris;
+  if (np > 0 && num_nodes == 0) { g_err = "empty BVH for a non-empty scene"; return IZPI_ERR_INVALID; }
+  std::vector<uint8_t> seen(np, 0);
+  for (uint32_t k = 0; k < np; k++) {
+    if (order[k] >= np || seen[order[k]]) { g_err = "order is not a permutation of the primitives"; return IZPI_ERR_INVALID; }
+    seen[order[k]] = 1;
+  }
+  for (uint32_t k = 0; k < num_nodes; k++) {  // children after parents (stack_bound's single backward pass)
+    const izpi_bvh4_node& n = nodes[k];
+    if (n.prim_count[0] > 0) {
+      if (n.child[0] < 0 || (uint64_t)n.child[0] + (uint64_t)n.prim_count[0] > np) { g_err = "leaf range out of bounds"; return IZPI_ERR_INVALID; }
+      continue;
+    }
+    for (int i = 0; i < 4; i++)
+      if (n.child[i] != -1 && (n.child[i] <= (int32_t)k || (uint32_t)n.child[i] >= num_nodes)) {
+        g_err = "child index must be in (parent, num_nodes)";
+        return IZPI_ERR_INVALID;
+      }
+  }
+  s->nodes.assign(nodes, nodes + num_nodes);
+  for (uint32_t k = 0; k < np; k++)
+    s->prim_ref[k] = order[k] < nt ? IZPI_PRIM_REF(IZPI_PRIM_TRIANGLE, order[k]) : IZPI_PRIM_REF(IZPI_PRIM_SPHERE, order[k] - nt);
+  s->stack_bound = stack_bound(s->nodes);
+  s->desc.num_nodes = num_nodes;
+  s->desc.nodes = s->nodes.data();
+  s->desc.num_prims = np;
+  s->desc.prim_ref = s->prim_ref.data();
+  return IZPI_OK;
+}
 uint32_t izpi_host_scene_stack_bound(const izpi_host_scene* s) { return s ? s->stack_bound : 0; }
 double izpi_host_scene_build_ms(const izpi_host_scene* s) { return s ? s->build_ms : 0; }
 void izpi_host_scene_free(izpi_host_scene* s) { delete s; }

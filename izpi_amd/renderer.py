@@ -37,14 +37,20 @@ def common_tiles(width, height):
 
 class GPURenderer:
     def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
-                 spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None):
+                 spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference"):
+        """bvh="reference": hitable.NewBVH4's tree, rebuilt bit for bit on the host (the
+        parity default); bvh="gpu": the GPU linear BVH4 builder (izpi_gpu_build_bvh4),
+        same node format, different topology."""
+        if bvh not in ("reference", "gpu"):
+            raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
         self.sampler = int(sampler)
         self.background = tuple(float(b) for b in background)
         self.seed = int(seed)
         self.device = int(device)
         # leader mode: aspect = W/H overrides the scene camera (transport.go aspectOverride)
-        self.host = host_scene or HostScene(scene, aspect_override=float(width) / float(height), bvh_seed=bvh_seed)
+        self.host = host_scene or HostScene(scene, aspect_override=float(width) / float(height), bvh_seed=bvh_seed,
+                                            skip_bvh=bvh == "gpu")
         if spectral_background is None:
             self._bg_wl = np.zeros(0)
             self._bg_val = np.zeros(0)
@@ -58,8 +64,26 @@ class GPURenderer:
         if rc != 0:
             raise RuntimeError("izpi_gpu_open(%d) failed: no HIP device?" % self.device)
         self.ctx = ctx
+        self.bvh_build_ms = None
+        if bvh == "gpu" and host_scene is None:
+            nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes())
+            self.host.set_bvh(nodes, order)
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None
+
+    def build_bvh4(self, boxes, leaf_max=4):
+        """izpi_gpu_build_bvh4 over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
+        boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
+        n = len(boxes)
+        nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
+        order = np.zeros(max(1, n), np.uint32)
+        m = C.c_uint32()
+        ms = C.c_double()
+        _check(N.lib().izpi_gpu_build_bvh4(self.ctx, boxes.ctypes.data_as(N.c_double_p), n, leaf_max,
+                                            nodes.ctypes.data_as(C.POINTER(N.BVH4Node)), len(nodes), C.byref(m),
+                                            order.ctypes.data_as(N.c_uint32_p), C.byref(ms)),
+               self.ctx, "izpi_gpu_build_bvh4")
+        return nodes[:m.value].copy(), order[:n].copy(), ms.value
 
     # -------------------------------------------------------------- request
     def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None, post=N.POST_NONE):

@@ -196,17 +196,36 @@ class HostScene:
     """izpi_host_build_scene result: the flattened izpi_scene_desc (Go host's
     transport.ToScene + NewBVH4 output)."""
 
-    def __init__(self, scene, aspect_override=0.0, bvh_seed=12345):
+    def __init__(self, scene, aspect_override=0.0, bvh_seed=12345, skip_bvh=False):
         L = N.lib()
         self._input = scene.to_input(aspect_override, bvh_seed)
         h = C.c_void_p()
-        rc = L.izpi_host_build_scene(self._input.ref(), C.byref(h))
+        rc = L.izpi_host_build_scene_ex(self._input.ref(), N.HOST_SKIP_BVH if skip_bvh else 0, C.byref(h))
         if rc != 0:
             raise RuntimeError("izpi_host_build_scene failed (%d): %s" % (rc, L.izpi_host_last_error().decode()))
         self.handle = h
         self.desc = L.izpi_host_scene_desc(h).contents
         self.stack_bound = L.izpi_host_scene_stack_bound(h)
         self.build_ms = L.izpi_host_scene_build_ms(h)
+
+    def prim_boxes(self):
+        """[num_tris + num_spheres][6] f64 boxes the BVH is built over."""
+        d = self.desc
+        out = np.zeros((d.num_tris + d.num_spheres, 6))
+        N.lib().izpi_host_scene_prim_boxes(self.handle, out.ctypes.data_as(N.c_double_p))
+        return out
+
+    def set_bvh(self, nodes, order):
+        """Attach a BVH4 built elsewhere (e.g. izpi_gpu_build_bvh4)."""
+        nodes = np.ascontiguousarray(nodes, np.uint8).reshape(-1, 128)
+        order = np.ascontiguousarray(order, np.uint32)
+        self._bvh_keep = (nodes, order)  # the host scene copies them; kept for inspection
+        rc = N.lib().izpi_host_scene_set_bvh(self.handle, nodes.ctypes.data_as(C.POINTER(N.BVH4Node)), len(nodes),
+                                              order.ctypes.data_as(N.c_uint32_p))
+        if rc != 0:
+            raise RuntimeError("izpi_host_scene_set_bvh failed (%d): %s" % (rc, N.lib().izpi_host_last_error().decode()))
+        self.desc = N.lib().izpi_host_scene_desc(self.handle).contents
+        self.stack_bound = N.lib().izpi_host_scene_stack_bound(self.handle)
 
     def nodes(self):
         d = self.desc

@@ -27,6 +27,11 @@
  *   render/rgb.go:12-57, render/spectral.go:71-106, common/tiles.go, grid/grid.go
  *   transport/transport.go:53-92, 551-680  (lights = IsEmitter hitables; World = Slice{BVH4})
  *   sort.Slice (Go stdlib pdqsort_func, zsortfunc.go) — used by the BVH build
+ * Also (not the reference): oracle_lbvh4, a sequential restatement of the GPU BVH4
+ * builder of izpi_amd/csrc/bvh_build.hip written from its
+ * algorithm description — top-down binary radix splits instead of Karras' parallel
+ * construction, a sequential breadth-first collapse — and oracle_set_bvh, which makes
+ * the oracle traverse an externally built tree.
  *
  * Documented deviations from the reference:
  *   * RNG streams are per pixel-sample (splitmix64 of seed and (sample,pixel)), both
@@ -47,6 +52,7 @@
 #include <thread>
 #include <vector>
 #include <string>
+#include <algorithm>
 
 #include "../include/izpi_host.h"
 #include "go_math_ref.h"
@@ -1307,6 +1313,149 @@ oracle_scene* oracle_build(const izpi_scene_input* in) {
   double aspect = in->aspect_override != 0.0 ? in->aspect_override : c.aspect;
   W.camera = Camera::New(Load(c.look_from), Load(c.look_at), Load(c.vup), c.vfov, aspect, c.aperture, c.focus_dist, c.time0, c.time1, c.exposure);
   return s;
+}
+
+/* Attach an external BVH4 (e.g. the GPU builder's): nodes + leaf order of the
+ * transport-order primitives (triangles, then spheres). */
+void oracle_set_bvh(oracle_scene* s, const izpi_bvh4_node* nodes, uint32_t num_nodes, const uint32_t* order) {
+  World& W = s->w;
+  W.bvh.Nodes.assign(nodes, nodes + num_nodes);
+  W.bvh.Primitives.clear();
+  for (size_t k = 0; k < W.byRef.size(); k++) W.bvh.Primitives.push_back(W.byRef[order[k]]);
+}
+
+/* Primitive boxes in transport order ([n][6]): Triangle.bb / Sphere.BoundingBox. */
+void oracle_prim_boxes(oracle_scene* s, double* out) {
+  const World& W = s->w;
+  for (size_t i = 0; i < W.byRef.size(); i++) {
+    const AABB b = W.byRef[i]->BoundingBox();
+    out[6 * i] = b.min.X; out[6 * i + 1] = b.min.Y; out[6 * i + 2] = b.min.Z;
+    out[6 * i + 3] = b.max.X; out[6 * i + 4] = b.max.Y; out[6 * i + 5] = b.max.Z;
+  }
+}
+
+/* Sequential restatement of the GPU LBVH4 builder (see the file header). Returns the
+ * node count; nodes needs 2n entries, order n. */
+uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, izpi_bvh4_node* nodes, uint32_t* order) {
+  if (n == 0) return 0;
+  // Morton codes of the centroids, 21 bits per axis
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (uint32_t i = 0; i < n; i++)
+    for (int k = 0; k < 3; k++) {
+      const double c = (boxes[6 * i + k] + boxes[6 * i + 3 + k]) * 0.5;
+      lo[k] = fmin(lo[k], c); hi[k] = fmax(hi[k], c);
+    }
+  std::vector<std::pair<uint64_t, uint32_t>> key(n);
+  for (uint32_t i = 0; i < n; i++) {
+    uint64_t code = 0;
+    for (int k = 0; k < 3; k++) {
+      const double c = (boxes[6 * i + k] + boxes[6 * i + 3 + k]) * 0.5;
+      const double ext = hi[k] - lo[k];
+      double t = ext > 0 ? (c - lo[k]) / ext : 0.0;
+      t = fmin(fmax(t * 2097152.0, 0.0), 2097151.0);
+      const uint64_t q = (uint64_t)t;
+      for (int b = 0; b < 21; b++) code |= ((q >> b) & 1ull) << (3 * b + (2 - k));
+    }
+    key[i] = {code, i};
+  }
+  std::sort(key.begin(), key.end());  // equal codes keep input order (stable radix sort)
+  for (uint32_t i = 0; i < n; i++) order[i] = key[i].second;
+  // binary radix tree over the augmented keys (code, position), built top-down
+  struct BN { int lo, hi, l, r; double box[6]; };
+  std::vector<BN> bn;
+  auto clz64 = [](uint64_t x) { return x ? __builtin_clzll(x) : 64; };
+  std::vector<int> stack;
+  bn.push_back(BN{0, (int)n - 1, -1, -1, {0}});
+  stack.push_back(0);
+  while (!stack.empty()) {
+    const int id = stack.back(); stack.pop_back();
+    const int a = bn[id].lo, b = bn[id].hi;
+    if (a == b) continue;
+    int split;  // last position of the left half
+    if (key[a].first != key[b].first) {
+      const int bit = 63 - clz64(key[a].first ^ key[b].first);
+      int p = a;  // last position whose code has `bit` clear
+      while (p + 1 <= b && !((key[p + 1].first >> bit) & 1)) p++;
+      split = p;
+    } else {
+      const int bit = 31 - __builtin_clz((unsigned)(a ^ b));
+      split = ((b >> bit) << bit) - 1;
+    }
+    const int l = (int)bn.size(); bn.push_back(BN{a, split, -1, -1, {0}});
+    const int r = (int)bn.size(); bn.push_back(BN{split + 1, b, -1, -1, {0}});
+    bn[id].l = l; bn[id].r = r;
+    stack.push_back(l); stack.push_back(r);
+  }
+  for (size_t id = bn.size(); id-- > 0;) {  // children were created after their parent
+    BN& x = bn[id];
+    if (x.l < 0) {
+      for (int k = 0; k < 6; k++) x.box[k] = boxes[6 * (size_t)order[x.lo] + k];
+    } else {
+      for (int k = 0; k < 3; k++) {
+        x.box[k] = fmin(bn[x.l].box[k], bn[x.r].box[k]);
+        x.box[k + 3] = fmax(bn[x.l].box[k + 3], bn[x.r].box[k + 3]);
+      }
+    }
+  }
+  auto size = [&](int id) { return bn[id].hi - bn[id].lo + 1; };
+  auto is_leaf = [&](int id) { return size(id) <= (int)leaf_max; };
+  auto empty = [](izpi_bvh4_node& nd) {
+    for (int s2 = 0; s2 < 4; s2++) {
+      nd.child[s2] = -1; nd.prim_count[s2] = 0;
+      nd.min_x[s2] = nd.min_y[s2] = nd.min_z[s2] = nd.max_x[s2] = nd.max_y[s2] = nd.max_z[s2] = 3.40282346638528859811704183484516925440e+38f;
+    }
+  };
+  auto slot = [&](izpi_bvh4_node& nd, int s2, int id) {
+    const double* b = bn[id].box;
+    nd.min_x[s2] = conservativeFloat32Min(b[0]); nd.min_y[s2] = conservativeFloat32Min(b[1]); nd.min_z[s2] = conservativeFloat32Min(b[2]);
+    nd.max_x[s2] = conservativeFloat32Max(b[3]); nd.max_y[s2] = conservativeFloat32Max(b[4]); nd.max_z[s2] = conservativeFloat32Max(b[5]);
+  };
+  if (is_leaf(0)) {
+    empty(nodes[0]);
+    nodes[0].child[0] = 0; nodes[0].prim_count[0] = (int32_t)n;
+    slot(nodes[0], 0, 0);
+    return 1;
+  }
+  // breadth-first collapse: node indices in allocation order
+  std::vector<std::pair<int, uint32_t>> frontier{{0, 0u}}, next;
+  uint32_t total = 1;
+  while (!frontier.empty()) {
+    next.clear();
+    for (auto& fe : frontier) {
+      int res[4], c = 0;
+      res[c++] = bn[fe.first].l; res[c++] = bn[fe.first].r;
+      bool expanded = true;
+      while (expanded && c < 4) {  // collectChildren (bvh4.go:796-855)
+        expanded = false;
+        for (int i = 0; i < c; i++) {
+          if (is_leaf(res[i])) continue;
+          const int cur = res[i];
+          for (int k = i; k + 1 < c; k++) res[k] = res[k + 1];
+          c--;
+          res[c++] = bn[cur].l; res[c++] = bn[cur].r;
+          expanded = true;
+          break;
+        }
+      }
+      izpi_bvh4_node nd; empty(nd);
+      for (int s2 = 0; s2 < c; s2++) {
+        const uint32_t idx = total++;
+        nd.child[s2] = (int32_t)idx;
+        slot(nd, s2, res[s2]);
+        if (is_leaf(res[s2])) {
+          izpi_bvh4_node lf; empty(lf);
+          lf.child[0] = bn[res[s2]].lo; lf.prim_count[0] = size(res[s2]);
+          slot(lf, 0, res[s2]);
+          nodes[idx] = lf;
+        } else {
+          next.push_back({res[s2], idx});
+        }
+      }
+      nodes[fe.second] = nd;
+    }
+    frontier.swap(next);
+  }
+  return total;
 }
 
 const char* oracle_error(oracle_scene* s) { return s->err.empty() ? nullptr : s->err.c_str(); }

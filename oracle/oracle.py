@@ -68,6 +68,10 @@ def lib():
     L.oracle_xyz_to_rgb.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int, C.c_double]
     L.oracle_postprocess.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_double), C.c_int]
+    L.oracle_set_bvh.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.oracle_prim_boxes.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    L.oracle_lbvh4.argtypes = [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.c_void_p, C.POINTER(C.c_uint32)]
+    L.oracle_lbvh4.restype = C.c_uint32
     L.oracle_tiles.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]
     L.oracle_tiles.restype = C.c_uint32
     L.oracle_sample_wavelength.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -113,6 +117,17 @@ class OracleScene:
         if out.size:
             L.oracle_copy_light_refs(self.h, out.ctypes.data)
         return out
+
+    def prim_boxes(self):
+        out = np.zeros((self._input.struct.num_tris + self._input.struct.num_spheres, 6))
+        lib().oracle_prim_boxes(self.h, dptr(out))
+        return out
+
+    def set_bvh(self, nodes, order):
+        """Traverse an external tree: nodes (n, 128) uint8 BVH4Node records, order (leaf order)."""
+        nodes = np.ascontiguousarray(nodes, np.uint8)
+        order = np.ascontiguousarray(order, np.uint32)
+        lib().oracle_set_bvh(self.h, nodes.ctypes.data, len(nodes), order.ctypes.data_as(C.POINTER(C.c_uint32)))
 
     def camera(self):
         from izpi_amd import _native as N
@@ -167,6 +182,16 @@ def postprocess(canvas, width, height, filters):
     p = np.array([f[1] for f in filters], np.float64)
     lib().oracle_postprocess(dptr(c), width, height, k.ctypes.data_as(C.POINTER(C.c_uint32)), dptr(p), len(filters))
     return c
+
+
+def lbvh4(boxes, leaf_max=4):
+    """Sequential restatement of the GPU BVH4 builder: (nodes (m, 128) uint8, order)."""
+    boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
+    n = len(boxes)
+    nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
+    order = np.zeros(max(1, n), np.uint32)
+    m = lib().oracle_lbvh4(dptr(boxes), n, leaf_max, nodes.ctypes.data, order.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return nodes[:m].copy(), order[:n].copy()
 
 
 def tiles(width, height):
