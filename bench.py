@@ -41,13 +41,19 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--scene", default=None, help="render a transport.Scene file (.pbtxt/.izpi) at the config's size")
+    p.add_argument("--bvh", default="gpu", choices=["reference", "gpu"],
+                   help="gpu (default): the GPU linear BVH4 builder, checked at N=1 against a frame on the "
+                        "reference tree; reference: hitable.NewBVH4's tree rebuilt bit for bit on the host")
+    p.add_argument("--no-reference-check", action="store_true",
+                   help="skip the reference-tree frame (timing and image comparison) of --bvh gpu")
     p.add_argument("--obj", default=None, help="C3 with this OBJ mesh (e.g. the Stanford dragon) instead of the "
                                                "synthetic one")
     return p.parse_args()
 
 
 def pmc_traffic(config):
-    """HBM bytes per k_trace launch from the committed rocprofv3 PMC pass, if any."""
+    """HBM bytes per k_trace launch from the committed rocprofv3 PMC pass, if any
+    (keyed "<config>/<bvh>", e.g. "C3/gpu")."""
     f = ROOT / "profiles" / "pmc_summary.json"
     if not f.exists():
         return None
@@ -116,7 +122,7 @@ def main():
     cfg = configs.configs()[args.config]
     spp = args.spp or cfg.spp
     t0 = time.time()
-    scene = cfg.build()
+    scene = None if (args.scene or args.obj) else cfg.build()
     if args.scene:  # leader.go:43-112: file scene, SPECTRAL scenes use the spectral sampler
         from izpi_amd import ingest
         scene = ingest.ProtoScene.from_file(args.scene)
@@ -126,38 +132,71 @@ def main():
         scene = configs.cornell_obj(args.obj, cfg.width / cfg.height)
         cfg = configs.Config("%s (mesh %s)" % (cfg.name, Path(args.obj).name), cfg.width, cfg.height, cfg.spp,
                              cfg.sampler, None, cfg.max_depth)
-    r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=local)
-    setup_s = time.time() - t0
-
+    scene_s = time.time() - t0
     from izpi_amd import _native as N
     post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
+    keys = ("node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests", "rays", "kernel_ms",
+            "shade_ms", "total_ms", "launches", "samples", "node_steps", "prim_steps", "leaf_shortcuts", "tail_ms",
+            "tail_node_visits", "tail_tri_tests", "tail_sph_tests")
 
-    def step():  # Render(): spectral configs include FireflyRejection + XYZToRGB (renderer.go:215-219)
-        return r.render_distributed(rank, world, post=post)
+    def timed(bvh):
+        """W untimed + K timed frames on tree `bvh`; returns (elapsed, stats sums, canvas, renderer info)."""
+        ts = time.time()
+        r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=local,
+                        bvh=bvh)
+        setup = time.time() - ts
 
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    agg = {k: 0.0 for k in ("node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests", "rays",
-                            "kernel_ms", "shade_ms", "total_ms", "launches", "samples", "node_steps", "prim_steps",
-                            "leaf_shortcuts", "tail_ms", "tail_node_visits", "tail_tri_tests", "tail_sph_tests")}
-    for _ in range(args.steps):
-        canvas, st = step()
-        for k in agg:
-            agg[k] += float(st[k]) if st else 0.0
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t1
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        def step():  # Render(): spectral configs include FireflyRejection + XYZToRGB (renderer.go:215-219)
+            return r.render_distributed(rank, world, post=post)
+
+        for _ in range(args.warmup):
+            step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        agg = {k: 0.0 for k in keys}
+        canvas = None
+        for _ in range(args.steps):
+            canvas, st = step()
+            for k in agg:
+                agg[k] += float(st[k]) if st else 0.0
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t1
+        if world > 1:
+            e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            elapsed = float(e.item())
+        info = {"triangles": int(r.host.desc.num_tris), "nodes": int(r.host.desc.num_nodes),
+                "build_ms": r.bvh_build_ms if bvh == "gpu" else r.host.build_ms, "setup_s": setup}
+        img = canvas.cpu().numpy() if canvas is not None else None
+        r.close()
+        return elapsed, agg, img, info
+
+    elapsed, agg, img, info = timed(args.bvh)
+    setup_s = info["setup_s"]  # host scene (+ reference BVH) build and upload of the timed renderer
     samples_per_step = cfg.width * cfg.height * spp
     value = samples_per_step * args.steps / elapsed / 1e6
+    ref_check = None
+    if world == 1 and args.bvh == "gpu" and not args.no_reference_check:
+        # The same frame on hitable.NewBVH4's own tree (rebuilt bit for bit on the host):
+        # the GPU-built tree only counts if its image is the reference tree's image.
+        import numpy as np
+        r_elapsed, r_agg, r_img, r_info = timed("reference")
+        equal = img.tobytes() == r_img.tobytes()
+        rmse = float(np.sqrt(np.mean((img - r_img) ** 2)))
+        ref_value = samples_per_step * args.steps / r_elapsed / 1e6
+        ref_check = {"value": round(ref_value, 3), "ms_per_step": round(r_elapsed / args.steps * 1e3, 3),
+                     "image_bitwise_equal": equal, "image_rmse": rmse,
+                     "node_visits_per_ray": r_agg["node_visits"] / max(r_agg["rays"], 1),
+                     "trace_ms_per_step": r_agg["kernel_ms"] / args.steps, "bvh_build_ms": r_info["build_ms"]}
+        if not rmse < 1e-6:  # north-star tolerance: fall back to the reference tree's numbers
+            print("WARNING: GPU-built BVH image differs from the reference tree's (rmse %g); reporting the "
+                  "reference tree" % rmse, file=sys.stderr)
+            elapsed, agg, img, info, value = r_elapsed, r_agg, r_img, r_info, ref_value
+            args.bvh = "reference"
 
     # roofline of the dominant kernel on this rank: algorithmic bytes / k_trace2 time
     # (the traversals k_tail runs at the end of the frame are counted apart)
@@ -165,13 +204,11 @@ def main():
                    + 32.0 * (agg["sph_tests"] - agg["tail_sph_tests"]))
     achieved = trace_bytes / (agg["kernel_ms"] * 1e-3) / 1e9 if agg["kernel_ms"] > 0 else 0.0
     launches = max(agg["launches"], 1.0)
-    traffic = pmc_traffic(args.config)
+    traffic = pmc_traffic("%s/%s" % (args.config, args.bvh))
     if rank != 0:
-        r.close()
         if world > 1:
             dist.destroy_process_group()
         return
-    img = canvas.cpu().numpy() if canvas is not None else None
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, scene, args.cpu_seconds, spp)
@@ -189,8 +226,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic (deterministic Cornell box + 817k-triangle displaced cube-sphere dragon)",
         "config": {"workload": cfg.name, "width": cfg.width, "height": cfg.height, "spp": spp,
-                   "max_depth": cfg.max_depth, "triangles": int(r.host.desc.num_tris),
-                   "bvh4_nodes": int(r.host.desc.num_nodes), "parallelism": "tiles%d" % world,
+                   "max_depth": cfg.max_depth, "triangles": info["triangles"],
+                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "parallelism": "tiles%d" % world,
                    "samples_per_step": samples_per_step},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -212,13 +249,14 @@ def main():
             "rank0_prim_step_lane_util": (agg["tri_tests"] + agg["sph_tests"] - agg["tail_tri_tests"] - agg["tail_sph_tests"]) /
                                          max(64 * agg["prim_steps"], 1),
             "rank0_leaf_shortcut_frac": agg["leaf_shortcuts"] / max(agg["node_visits"], 1),
+            "scene_gen_s": round(scene_s, 2),
             "setup_s": round(setup_s, 2),
-            "bvh_build_ms": r.host.build_ms,
+            "bvh_build_ms": info["build_ms"],
+            "reference_tree": ref_check,
             "image_mean_rgb": [float(x) for x in img[1:, :, :3].mean(axis=(0, 1))] if img is not None else None,
         },
     }
     print(json.dumps(line), flush=True)
-    r.close()
     if world > 1:
         dist.destroy_process_group()
 
