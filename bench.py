@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--bvh", default="gpu", choices=["reference", "gpu"],
                    help="gpu (default): the GPU linear BVH4 builder, checked at N=1 against a frame on the "
                         "reference tree; reference: hitable.NewBVH4's tree rebuilt bit for bit on the host")
+    p.add_argument("--bvh-leaf-max", type=int, default=None, help="primitives per leaf of the GPU-built tree")
     p.add_argument("--no-reference-check", action="store_true",
                    help="skip the reference-tree frame (timing and image comparison) of --bvh gpu")
     p.add_argument("--obj", default=None, help="C3 with this OBJ mesh (e.g. the Stanford dragon) instead of the "
@@ -143,7 +144,7 @@ def main():
         """W untimed + K timed frames on tree `bvh`; returns (elapsed, stats sums, canvas, renderer info)."""
         ts = time.time()
         r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=local,
-                        bvh=bvh)
+                        bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
         setup = time.time() - ts
 
         def step():  # Render(): spectral configs include FireflyRejection + XYZToRGB (renderer.go:215-219)
@@ -191,7 +192,8 @@ def main():
         ref_check = {"value": round(ref_value, 3), "ms_per_step": round(r_elapsed / args.steps * 1e3, 3),
                      "image_bitwise_equal": equal, "image_rmse": rmse,
                      "node_visits_per_ray": r_agg["node_visits"] / max(r_agg["rays"], 1),
-                     "trace_ms_per_step": r_agg["kernel_ms"] / args.steps, "bvh_build_ms": r_info["build_ms"]}
+                     "trace_ms_per_step": r_agg["kernel_ms"] / args.steps,
+                     "shade_ms_per_step": r_agg["shade_ms"] / args.steps, "bvh_build_ms": r_info["build_ms"]}
         if not rmse < 1e-6:  # north-star tolerance: fall back to the reference tree's numbers
             print("WARNING: GPU-built BVH image differs from the reference tree's (rmse %g); reporting the "
                   "reference tree" % rmse, file=sys.stderr)

@@ -20,6 +20,10 @@ from . import _native as N
 from .scene import HostScene
 
 
+# primitives per leaf of the GPU-built tree (the reference allows up to 4, bvh4.go:638)
+GPU_BVH_LEAF_MAX = 3  # measured on C3: 3 -> 1146, 2 -> 1137, 4 -> 1065 Msamples/s
+
+
 def _check(rc, ctx, what):
     if rc != 0:
         msg = N.lib().izpi_gpu_last_error(ctx).decode() if ctx else ""
@@ -37,7 +41,8 @@ def common_tiles(width, height):
 
 class GPURenderer:
     def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
-                 spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference"):
+                 spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference",
+                 bvh_leaf_max=None):
         """bvh="reference": hitable.NewBVH4's tree, rebuilt bit for bit on the host (the
         parity default); bvh="gpu": the GPU linear BVH4 builder (izpi_gpu_build_bvh4),
         same node format, different topology."""
@@ -66,7 +71,8 @@ class GPURenderer:
         self.ctx = ctx
         self.bvh_build_ms = None
         if bvh == "gpu" and host_scene is None:
-            nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes())
+            nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes(),
+                                                              bvh_leaf_max or GPU_BVH_LEAF_MAX)
             self.host.set_bvh(nodes, order)
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None

@@ -30,7 +30,8 @@
  * Also (not the reference): oracle_lbvh4, a sequential restatement of the GPU BVH4
  * builder of izpi_amd/csrc/bvh_build.hip written from its
  * algorithm description — top-down binary radix splits instead of Karras' parallel
- * construction, a sequential breadth-first collapse — and oracle_set_bvh, which makes
+ * construction, a sequential breadth-first collapse (collectChildren's rule, but the
+ * inner child with the largest surface area is expanded first) — and oracle_set_bvh, which makes
  * the oracle traverse an externally built tree.
  *
  * Documented deviations from the reference:
@@ -1425,16 +1426,23 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, izpi_b
       int res[4], c = 0;
       res[c++] = bn[fe.first].l; res[c++] = bn[fe.first].r;
       bool expanded = true;
-      while (expanded && c < 4) {  // collectChildren (bvh4.go:796-855)
+      while (expanded && c < 4) {  // collectChildren (bvh4.go:796-855), largest surface area first
         expanded = false;
+        int pick = -1;
+        double best = -1.0;
         for (int i = 0; i < c; i++) {
           if (is_leaf(res[i])) continue;
-          const int cur = res[i];
-          for (int k = i; k + 1 < c; k++) res[k] = res[k + 1];
+          const double* b = bn[res[i]].box;
+          const double dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+          const double area = dx * dy + dy * dz + dz * dx;
+          if (area > best) { best = area; pick = i; }
+        }
+        if (pick >= 0) {
+          const int cur = res[pick];
+          for (int k = pick; k + 1 < c; k++) res[k] = res[k + 1];
           c--;
           res[c++] = bn[cur].l; res[c++] = bn[cur].r;
           expanded = true;
-          break;
         }
       }
       izpi_bvh4_node nd; empty(nd);
