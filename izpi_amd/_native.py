@@ -27,6 +27,7 @@ POST_NONE, POST_SPECTRAL, POST_GAMMA_CLAMP = 0, 1, 2
 FILTER_GAMMA, FILTER_CLAMP = 1, 2
 MAX_FILTERS = 8
 HOST_SKIP_BVH = 1
+BVH_LBVH, BVH_PLOC = 0, 1
 
 
 def prim_ref(kind, idx):
@@ -211,8 +212,8 @@ def lib():
     L.izpi_gpu_spectral_post.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double]
     L.izpi_gpu_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, c_uint32_p, c_double_p,
                                        C.c_uint32]
-    L.izpi_gpu_build_bvh4.argtypes = [C.c_void_p, c_double_p, C.c_uint32, C.c_uint32, C.POINTER(BVH4Node), C.c_uint32,
-                                      c_uint32_p, c_uint32_p, c_double_p]
+    L.izpi_gpu_build_bvh4.argtypes = [C.c_void_p, c_double_p, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(BVH4Node),
+                                      C.c_uint32, c_uint32_p, c_uint32_p, c_double_p]
     L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]
     L.izpi_host_scene_prim_boxes.argtypes = [C.c_void_p, c_double_p]
     L.izpi_host_scene_set_bvh.argtypes = [C.c_void_p, C.POINTER(BVH4Node), C.c_uint32, c_uint32_p]

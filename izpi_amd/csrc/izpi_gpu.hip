@@ -47,8 +47,8 @@ __constant__ double c_cie_y[IZPI_CIE_N] = IZPI_CIE_Y_INIT;
 __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
 
 namespace izpi_bvh {  // bvh_build.hip
-int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, std::vector<izpi_bvh4_node>& nodes,
-          std::vector<uint32_t>& order, float* ms, std::string& err);
+int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, uint32_t method,
+          std::vector<izpi_bvh4_node>& nodes, std::vector<uint32_t>& order, float* ms, std::string& err);
 }
 
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
@@ -2549,8 +2549,8 @@ int izpi_gpu_spectral_post(izpi_ctx* ctx, const double* xyz_dev, double* rgba_de
   return IZPI_OK;
 }
 
-int izpi_gpu_build_bvh4(izpi_ctx* ctx, const double* boxes, uint32_t n, uint32_t leaf_max, izpi_bvh4_node* nodes,
-                        uint32_t max_nodes, uint32_t* num_nodes, uint32_t* order, double* build_ms) {
+int izpi_gpu_build_bvh4(izpi_ctx* ctx, const double* boxes, uint32_t n, uint32_t leaf_max, uint32_t method,
+                        izpi_bvh4_node* nodes, uint32_t max_nodes, uint32_t* num_nodes, uint32_t* order, double* build_ms) {
   if (!ctx) return IZPI_ERR_INVALID;
   if (num_nodes) *num_nodes = 0;
   if ((n && (!boxes || !nodes || !order)) || !num_nodes || (uint64_t)max_nodes < 2ull * n) {
@@ -2561,7 +2561,7 @@ int izpi_gpu_build_bvh4(izpi_ctx* ctx, const double* boxes, uint32_t n, uint32_t
   std::vector<izpi_bvh4_node> out;
   std::vector<uint32_t> ord;
   float ms = 0;
-  const int rc = izpi_bvh::build(ctx->stream, boxes, n, leaf_max, out, ord, &ms, ctx->err);
+  const int rc = izpi_bvh::build(ctx->stream, boxes, n, leaf_max, method, out, ord, &ms, ctx->err);
   if (rc) return rc;
   if (!out.empty()) memcpy(nodes, out.data(), out.size() * sizeof(izpi_bvh4_node));
   if (!ord.empty()) memcpy(order, ord.data(), ord.size() * sizeof(uint32_t));

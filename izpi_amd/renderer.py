@@ -21,6 +21,7 @@ from .scene import HostScene
 
 
 # primitives per leaf of the GPU-built tree (the reference allows up to 4, bvh4.go:638)
+GPU_BVH_METHOD = N.BVH_PLOC
 GPU_BVH_LEAF_MAX = 3  # measured on C3: 3 -> 1146, 2 -> 1137, 4 -> 1065 Msamples/s
 
 
@@ -77,15 +78,16 @@ class GPURenderer:
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None
 
-    def build_bvh4(self, boxes, leaf_max=4):
+    def build_bvh4(self, boxes, leaf_max=4, method=None):
         """izpi_gpu_build_bvh4 over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
+        method = GPU_BVH_METHOD if method is None else method
         boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
         n = len(boxes)
         nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
         order = np.zeros(max(1, n), np.uint32)
         m = C.c_uint32()
         ms = C.c_double()
-        _check(N.lib().izpi_gpu_build_bvh4(self.ctx, boxes.ctypes.data_as(N.c_double_p), n, leaf_max,
+        _check(N.lib().izpi_gpu_build_bvh4(self.ctx, boxes.ctypes.data_as(N.c_double_p), n, leaf_max, method,
                                             nodes.ctypes.data_as(C.POINTER(N.BVH4Node)), len(nodes), C.byref(m),
                                             order.ctypes.data_as(N.c_uint32_p), C.byref(ms)),
                self.ctx, "izpi_gpu_build_bvh4")

@@ -54,6 +54,7 @@
 #include <vector>
 #include <string>
 #include <algorithm>
+#include <array>
 
 #include "../include/izpi_host.h"
 #include "go_math_ref.h"
@@ -1337,7 +1338,8 @@ void oracle_prim_boxes(oracle_scene* s, double* out) {
 
 /* Sequential restatement of the GPU LBVH4 builder (see the file header). Returns the
  * node count; nodes needs 2n entries, order n. */
-uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, izpi_bvh4_node* nodes, uint32_t* order) {
+uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32_t method, izpi_bvh4_node* nodes,
+                      uint32_t* order) {
   if (n == 0) return 0;
   // Morton codes of the centroids, 21 bits per axis
   double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -1361,9 +1363,77 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, izpi_b
   }
   std::sort(key.begin(), key.end());  // equal codes keep input order (stable radix sort)
   for (uint32_t i = 0; i < n; i++) order[i] = key[i].second;
-  // binary radix tree over the augmented keys (code, position), built top-down
   struct BN { int lo, hi, l, r; double box[6]; };
   std::vector<BN> bn;
+  if (method == 1) {
+    // PLOC: clusters in Morton order; nearest neighbour by merged half-area within +-8
+    // (ties: lower position); mutual pairs merge at the lower position; repeat.
+    const int R = 8, N2 = 2 * (int)n - 1;
+    std::vector<int> pl(N2, -1), pr(N2, -1), psz(N2, 1), off(N2, 0);
+    std::vector<std::array<double, 6>> pb(N2);
+    for (uint32_t i = 0; i < n; i++)
+      for (int k = 0; k < 6; k++) pb[i][k] = boxes[6 * (size_t)key[i].second + k];
+    auto uni = [&](int a, int b) {
+      std::array<double, 6> r2;
+      for (int k = 0; k < 3; k++) { r2[k] = fmin(pb[a][k], pb[b][k]); r2[k + 3] = fmax(pb[a][k + 3], pb[b][k + 3]); }
+      return r2;
+    };
+    auto ha = [](const std::array<double, 6>& x) {
+      const double dx = x[3] - x[0], dy = x[4] - x[1], dz = x[5] - x[2];
+      return dx * dy + dy * dz + dz * dx;
+    };
+    std::vector<int> cl(n);
+    for (uint32_t i = 0; i < n; i++) cl[i] = (int)i;
+    int nxt = (int)n;
+    while (cl.size() > 1) {
+      const int m = (int)cl.size();
+      std::vector<int> nn(m);
+      for (int i = 0; i < m; i++) {
+        double best = INFINITY;
+        int bj = -1;
+        for (int j = std::max(0, i - R); j <= std::min(m - 1, i + R); j++) {
+          if (j == i) continue;
+          const double a = ha(uni(cl[i], cl[j]));
+          if (a < best) { best = a; bj = j; }
+        }
+        nn[i] = bj;
+      }
+      std::vector<int> nc;
+      for (int i = 0; i < m; i++) {
+        const int j = nn[i];
+        const bool mutual = j >= 0 && nn[j] == i;
+        if (mutual && i > j) continue;  // merged into its partner's position
+        if (mutual) {
+          const int c = nxt++;
+          pl[c] = cl[i]; pr[c] = cl[j]; pb[c] = uni(cl[i], cl[j]); psz[c] = psz[cl[i]] + psz[cl[j]];
+          nc.push_back(c);
+        } else {
+          nc.push_back(cl[i]);
+        }
+      }
+      cl.swap(nc);
+    }
+    const int root = cl[0];
+    std::vector<int> stk{root};
+    while (!stk.empty()) {  // DFS positions: subtrees become contiguous ranges
+      const int x = stk.back(); stk.pop_back();
+      if (pl[x] < 0) continue;
+      off[pl[x]] = off[x]; off[pr[x]] = off[x] + psz[pl[x]];
+      stk.push_back(pr[x]); stk.push_back(pl[x]);
+    }
+    auto map = [&](int x) { return x < (int)n ? (int)n - 1 + off[x] : N2 - 1 - x; };
+    bn.assign(N2, BN{0, 0, -1, -1, {0}});
+    std::vector<uint32_t> ord(n);
+    for (int x = 0; x < N2 && (x < (int)n || x < nxt); x++) {
+      BN& b = bn[map(x)];
+      b.lo = off[x]; b.hi = off[x] + psz[x] - 1;
+      b.l = pl[x] < 0 ? -1 : map(pl[x]); b.r = pr[x] < 0 ? -1 : map(pr[x]);
+      for (int k = 0; k < 6; k++) b.box[k] = pb[x][k];
+      if (x < (int)n) ord[off[x]] = key[x].second;
+    }
+    for (uint32_t i = 0; i < n; i++) order[i] = ord[i];
+  } else {
+  // binary radix tree over the augmented keys (code, position), built top-down
   auto clz64 = [](uint64_t x) { return x ? __builtin_clzll(x) : 64; };
   std::vector<int> stack;
   bn.push_back(BN{0, (int)n - 1, -1, -1, {0}});
@@ -1398,6 +1468,7 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, izpi_b
       }
     }
   }
+  }  // method
   auto size = [&](int id) { return bn[id].hi - bn[id].lo + 1; };
   auto is_leaf = [&](int id) { return size(id) <= (int)leaf_max; };
   auto empty = [](izpi_bvh4_node& nd) {

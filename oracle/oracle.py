@@ -70,7 +70,8 @@ def lib():
                                      C.POINTER(C.c_double), C.c_int]
     L.oracle_set_bvh.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
     L.oracle_prim_boxes.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
-    L.oracle_lbvh4.argtypes = [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.c_void_p, C.POINTER(C.c_uint32)]
+    L.oracle_lbvh4.argtypes = [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                               C.POINTER(C.c_uint32)]
     L.oracle_lbvh4.restype = C.c_uint32
     L.oracle_tiles.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]
     L.oracle_tiles.restype = C.c_uint32
@@ -184,13 +185,15 @@ def postprocess(canvas, width, height, filters):
     return c
 
 
-def lbvh4(boxes, leaf_max=4):
-    """Sequential restatement of the GPU BVH4 builder: (nodes (m, 128) uint8, order)."""
+def lbvh4(boxes, leaf_max=4, method=1):
+    """Sequential restatement of the GPU BVH4 builder (method 0 LBVH, 1 PLOC):
+    (nodes (m, 128) uint8, order)."""
     boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
     n = len(boxes)
     nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
     order = np.zeros(max(1, n), np.uint32)
-    m = lib().oracle_lbvh4(dptr(boxes), n, leaf_max, nodes.ctypes.data, order.ctypes.data_as(C.POINTER(C.c_uint32)))
+    m = lib().oracle_lbvh4(dptr(boxes), n, leaf_max, method, nodes.ctypes.data,
+                           order.ctypes.data_as(C.POINTER(C.c_uint32)))
     return nodes[:m].copy(), order[:n].copy()
 
 

@@ -1,5 +1,6 @@
-"""The alternative BVH4 builder: a linear BVH collapsed with
-collectChildren's rule into the reference's BVH4Node format.
+"""The alternative BVH4 builder: a Morton-ordered binary tree
+(PLOC clustering or an LBVH radix tree) collapsed with collectChildren's rule into the
+reference's BVH4Node format.
 
 CPU side (here): the oracle's sequential restatement of the builder (oracle_lbvh4)
 yields valid BVH4 trees (the invariants of bvh4_test.go:13-83,453-496 that do not
@@ -77,29 +78,33 @@ def test_host_prim_boxes_equal_oracle():
         assert h.prim_boxes().tobytes() == o.prim_boxes().tobytes()
 
 
+@pytest.mark.parametrize("method", [N.BVH_LBVH, N.BVH_PLOC])
 @pytest.mark.parametrize("n_side", [1, 3, 24])
-def test_lbvh4_tree_invariants(n_side):
+def test_lbvh4_tree_invariants(n_side, method):
     scene = configs.cornell_dragon(1.0, n=n_side)
     boxes = HostScene(scene, 1.0, skip_bvh=True).prim_boxes()
-    nodes, order = O.lbvh4(boxes)
-    check_tree(nodes, order, boxes)
+    for lm in (3, 4):
+        nodes, order = O.lbvh4(boxes, lm, method)
+        check_tree(nodes, order, boxes, leaf_max=lm)
 
 
-def test_lbvh4_small_and_degenerate_inputs():
+@pytest.mark.parametrize("method", [N.BVH_LBVH, N.BVH_PLOC])
+def test_lbvh4_small_and_degenerate_inputs(method):
     rng = np.random.default_rng(2)
     for n in (1, 2, 4, 5, 17):
         lo = rng.uniform(0, 10, (n, 3))
         boxes = np.concatenate([lo, lo + rng.uniform(0.1, 1, (n, 3))], 1)
-        nodes, order = O.lbvh4(boxes)
+        nodes, order = O.lbvh4(boxes, 4, method)
         check_tree(nodes, order, boxes)
         if n <= 4:
             assert len(nodes) == 1
-    same = np.tile([1.0, 1.0, 1.0, 2.0, 2.0, 2.0], (37, 1))  # one Morton code: split by position
-    nodes, order = O.lbvh4(same)
+    same = np.tile([1.0, 1.0, 1.0, 2.0, 2.0, 2.0], (37, 1))  # one Morton code, equal boxes
+    nodes, order = O.lbvh4(same, 4, method)
     check_tree(nodes, order, same)
-    assert order.tolist() == list(range(37))
+    if method == N.BVH_LBVH:
+        assert order.tolist() == list(range(37))  # split by position
     for lm in (1, 2, 3):
-        nodes, order = O.lbvh4(boxes, leaf_max=lm)
+        nodes, order = O.lbvh4(boxes, lm, method)
         check_tree(nodes, order, boxes, leaf_max=lm)
 
 
@@ -109,7 +114,7 @@ def test_lbvh4_scene_finds_the_reference_closest_hits():
     scene = configs.cornell_dragon(1.0, n=24)
     ref = O.OracleScene(scene, 1.0)
     alt = O.OracleScene(scene, 1.0)
-    nodes, order = O.lbvh4(alt.prim_boxes())
+    nodes, order = O.lbvh4(alt.prim_boxes(), 3)
     alt.set_bvh(nodes, order)
     rng = np.random.default_rng(7)
     n = 4000

@@ -405,8 +405,9 @@ def test_postprocess_kernel_bitwise(gpu):
     r.close()
 
 
+@pytest.mark.parametrize("method", [N.BVH_PLOC, N.BVH_LBVH])
 @pytest.mark.parametrize("which", ["cornell", "dragon", "glass", "degenerate", "tiny"])
-def test_gpu_bvh4_builder_equals_oracle_restatement(gpu, which):
+def test_gpu_bvh4_builder_equals_oracle_restatement(gpu, which, method):
     """izpi_gpu_build_bvh4 (Morton sort + Karras tree + refit + collapse on the GPU) ==
     the oracle's sequential restatement, node for node and in leaf order."""
     from izpi_amd.scene import HostScene
@@ -420,12 +421,12 @@ def test_gpu_bvh4_builder_equals_oracle_restatement(gpu, which):
                  "glass": configs.cornell_glass_spectral()}[which]
         boxes = HostScene(scene, 1.0, skip_bvh=True).prim_boxes()
     r = GPURenderer(configs.cornell_rgb(), 8, 8, 1)
-    nodes, order, ms = r.build_bvh4(boxes)
-    ref_nodes, ref_order = O.lbvh4(boxes)
+    nodes, order, ms = r.build_bvh4(boxes, 3, method)
+    ref_nodes, ref_order = O.lbvh4(boxes, 3, method)
     assert order.tolist() == ref_order.tolist()
     assert nodes.tobytes() == ref_nodes.tobytes()
-    check_tree(nodes, order, boxes)
-    again, order2, _ = r.build_bvh4(boxes)  # deterministic
+    check_tree(nodes, order, boxes, leaf_max=3)
+    again, order2, _ = r.build_bvh4(boxes, 3, method)  # deterministic
     assert again.tobytes() == nodes.tobytes() and (order2 == order).all()
     r.close()
 

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--bvh", default="gpu")
     a = ap.parse_args()
     import torch
     from izpi_amd import _native as N
@@ -24,7 +25,7 @@ def main():
     from izpi_amd.renderer import GPURenderer, common_tiles
     cfg = configs.configs()[a.config]
     spp = a.spp or cfg.spp
-    r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler)
+    r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, bvh=a.bvh)
     all_tiles = common_tiles(cfg.width, cfg.height)
     t1 = None
     for w in [int(x) for x in a.worlds.split(",")]:

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--bvh", default="gpu")
     ap.add_argument("--var", action="append", default=[], help="NAME=v1,v2,... (env knob)")
     a = ap.parse_args()
     import numpy as np
@@ -25,7 +26,7 @@ def main():
     from izpi_amd.renderer import GPURenderer
     cfg = configs.configs()[a.config]
     scene = cfg.build()
-    r = GPURenderer(scene, cfg.width, cfg.height, a.spp, max_depth=cfg.max_depth, sampler=cfg.sampler)
+    r = GPURenderer(scene, cfg.width, cfg.height, a.spp, max_depth=cfg.max_depth, sampler=cfg.sampler, bvh=a.bvh)
     variants = [{}]
     for v in a.var:
         name, vals = v.split("=")
