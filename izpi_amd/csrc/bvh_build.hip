@@ -236,13 +236,16 @@ __global__ void k_ploc_nn(const int32_t* cl, uint32_t m, const Box6* pbox, int r
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= (int)m) return;
   const Box6 bi = pbox[cl[i]];
+  // ties (equal merged areas, e.g. coincident primitives) go to the nearer position and
+  // then to i+1 for even i, i-1 for odd i: equal clusters pair up instead of chaining
   double best = __builtin_inf();
-  int bj = -1;
+  int bj = -1, bkey = 0;
   const int lo = max(0, i - radius), hi = min((int)m - 1, i + radius);
   for (int j = lo; j <= hi; j++) {
     if (j == i) continue;
     const double a = half_area(unite(bi, pbox[cl[j]]));
-    if (a < best) { best = a; bj = j; }
+    const int key = 2 * abs(j - i) + (((j > i) == ((i & 1) == 0)) ? 0 : 1);
+    if (a < best || (a == best && key < bkey)) { best = a; bj = j; bkey = key; }
   }
   nn[i] = bj;
 }

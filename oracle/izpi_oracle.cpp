@@ -1366,8 +1366,8 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32
   struct BN { int lo, hi, l, r; double box[6]; };
   std::vector<BN> bn;
   if (method == 1) {
-    // PLOC: clusters in Morton order; nearest neighbour by merged half-area within +-8
-    // (ties: lower position); mutual pairs merge at the lower position; repeat.
+    // PLOC: clusters in Morton order; nearest neighbour by merged half-area within +-8;
+    // mutual pairs merge at the lower position; repeat.
     const int R = 8, N2 = 2 * (int)n - 1;
     std::vector<int> pl(N2, -1), pr(N2, -1), psz(N2, 1), off(N2, 0);
     std::vector<std::array<double, 6>> pb(N2);
@@ -1390,11 +1390,15 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32
       std::vector<int> nn(m);
       for (int i = 0; i < m; i++) {
         double best = INFINITY;
-        int bj = -1;
+        int bj = -1, bkey = 0;
         for (int j = std::max(0, i - R); j <= std::min(m - 1, i + R); j++) {
           if (j == i) continue;
           const double a = ha(uni(cl[i], cl[j]));
-          if (a < best) { best = a; bj = j; }
+          // equal areas: nearer position first, then i+1 for even i and i-1 for odd i
+          const int dist = j > i ? j - i : i - j;
+          const bool pref = (j > i) == (i % 2 == 0);
+          const int k2 = 2 * dist + (pref ? 0 : 1);
+          if (a < best || (a == best && k2 < bkey)) { best = a; bj = j; bkey = k2; }
         }
         nn[i] = bj;
       }

@@ -101,8 +101,9 @@ def test_lbvh4_small_and_degenerate_inputs(method):
     same = np.tile([1.0, 1.0, 1.0, 2.0, 2.0, 2.0], (37, 1))  # one Morton code, equal boxes
     nodes, order = O.lbvh4(same, 4, method)
     check_tree(nodes, order, same)
-    if method == N.BVH_LBVH:
-        assert order.tolist() == list(range(37))  # split by position
+    assert order.tolist() == list(range(37))  # split by position / paired by position
+    f, child, count = node_view(nodes)
+    assert len(nodes) < 40  # balanced, not a chain
     for lm in (1, 2, 3):
         nodes, order = O.lbvh4(boxes, lm, method)
         check_tree(nodes, order, boxes, leaf_max=lm)
