@@ -2124,11 +2124,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // 48 B per depth level of unwinding records).
   uint64_t slot_cap = 1ull << 24;
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
-  {  // keep the wavefront state within a quarter of the free HBM
+  {  // keep the wavefront state within half of the free HBM (the per-sample results take at most a quarter)
     if (free_b > 0) {
       const uint64_t per_slot = sizeof(RayHot) + sizeof(RayAux) + sizeof(HitHot) + sizeof(HitUV) + sizeof(PathHot) + sizeof(PathCold) + 12 +
                                 (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
-      slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 4) / per_slot));
+      slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 2) / per_slot));
     }
   }
   const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);

@@ -13,6 +13,7 @@ canvas on its GPU (izpi_gpu_unpack_tiles). Per pixel-sample RNG streams make the
 independent of the partition.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -80,7 +81,8 @@ class GPURenderer:
 
     def build_bvh4(self, boxes, leaf_max=4, method=None):
         """izpi_gpu_build_bvh4 over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
-        method = GPU_BVH_METHOD if method is None else method
+        if method is None:  # IZPI_BVH_METHOD=lbvh|ploc overrides the default (experiments)
+            method = {"lbvh": N.BVH_LBVH, "ploc": N.BVH_PLOC}.get(os.environ.get("IZPI_BVH_METHOD", ""), GPU_BVH_METHOD)
         boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
         n = len(boxes)
         nodes = np.zeros((max(1, 2 * n), 128), np.uint8)

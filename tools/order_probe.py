@@ -11,13 +11,16 @@ def main():
     from izpi_amd.renderer import GPURenderer
     cfg = configs.configs()["C3"]
     scene = cfg.build()
-    for bvh in sys.argv[1].split(","):
+    import os
+    for spec in sys.argv[1].split(","):
+        bvh, _, method = spec.partition(":")  # e.g. gpu:lbvh
+        os.environ["IZPI_BVH_METHOD"] = method
         r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp, bvh=bvh)
         for i in range(3):
             t = time.perf_counter()
             r.render()
             st = r.stats
-            print(bvh, i, "%.1f ms wall, trace %.1f shade %.1f total %.1f" % ((time.perf_counter() - t) * 1e3, st["kernel_ms"],
+            print(spec, i, "%.1f ms wall, trace %.1f shade %.1f total %.1f" % ((time.perf_counter() - t) * 1e3, st["kernel_ms"],
                                                                           st["shade_ms"], st["total_ms"]), flush=True)
         r.close()
 
