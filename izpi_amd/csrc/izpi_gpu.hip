@@ -2122,7 +2122,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // Paths in flight per wavefront pass. Larger = fewer k_trace/k_shade launches and
   // a smaller share of launch tails; costs HBM for the per-slot state (~176 B +
   // 48 B per depth level of unwinding records).
-  uint64_t slot_cap = 1ull << 24;
+  uint64_t slot_cap = 40ull << 20;  // C3: 16M -> 435 ms/frame, 24M -> 414, 40M -> 407 (fewer passes, fewer pass tails)
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
   {  // keep the wavefront state within half of the free HBM (the per-sample results take at most a quarter)
     if (free_b > 0) {
