@@ -945,6 +945,7 @@ struct ShadeParams {
   uint32_t chunk_spp, s0, tile_w, tile_h, total_units;
   uint32_t num_bg_spd, slots;
   uint32_t rec_depth;          // records per slot (max(1, max_depth))
+  uint32_t unit_base;          // k_start: slot i of this lane starts unit unit_base + i
   const uint32_t* tiles;
   const double* bg_wl;
   const double* bg_val;
@@ -1192,7 +1193,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
   for (;;) {
     uint32_t unit;
     if (first) {
-      unit = (want && slot < sp.total_units) ? slot : 0xFFFFFFFFu;
+      unit = (want && slot + sp.unit_base < sp.total_units) ? slot + sp.unit_base : 0xFFFFFFFFu;
       first = false;
     } else {
       unit = grab_unit(sp, want);
@@ -1851,6 +1852,14 @@ struct izpi_ctx {
   uint32_t* h_count = nullptr;                        // pinned readback of d_misc (unit head, queue lengths)
   hipEvent_t ev3 = nullptr;
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
+  // second wavefront lane (run_chunks with two lanes): its own stream, counters, events
+  // and traversal spill area; the slots, queues and records are split between the lanes
+  hipStream_t stream2 = nullptr;
+  uint32_t* d_misc2 = nullptr;
+  uint32_t* h_count2 = nullptr;
+  hipEvent_t evb2[3 * IZPI_PASS_BATCH] = {};
+  hipEvent_t evj = nullptr;
+  int32_t* d_spill2 = nullptr; size_t spill2_cap = 0;
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
@@ -1951,7 +1960,7 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   return grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, (size_t)t->blocks * 256 * 64 * sizeof(int32_t));
 }
 
-void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStream_t st) {
+void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
   const dim3 g(t.blocks), b(256);
   if (t.variant == 1) {
     if (t.stack == 32) hipLaunchKernelGGL(k_trace<32>, g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
@@ -1961,7 +1970,7 @@ void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStrea
   const uint32_t stride = (uint32_t)t.blocks * 256;
 #define IZPI_T2_LAUNCH(R, W, P, T)                                                                            \
   if (t.ring == R && t.wpe == W && t.p2 == P && t.tri == T) {                                                \
-    hipLaunchKernelGGL((k_trace2<R, W, P, T>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, ctx->d_spill, \
+    hipLaunchKernelGGL((k_trace2<R, W, P, T>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, spill, \
                        stride, t.prim_w, t.tchunk, t.refill_min);                                            \
     return;                                                                                                  \
   }
@@ -2002,75 +2011,154 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
                       : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
   uint64_t tail_max = (uint64_t)tail_res * 256;
   if (const char* e = getenv("IZPI_TAIL")) tail_max = strtoull(e, nullptr, 10);
-  uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
-  wp.free_q = ctx->d_queue + 2 * (size_t)sp.slots;
-  wp.free_count = ctx->d_misc + 5;
-  uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
+  // Wavefront lanes. With two lanes the slots, queues and records are split in halves and
+  // each lane alternates k_trace2 / k_shade on its own stream: the drain at the end of one
+  // lane's pass (few waves left, ~0.5 ms of k_trace2 per pass on C3) is filled by the other
+  // lane's kernels. Lanes share the unit head, so the work and the results are the same.
+  // Measured on C3: 411.8 ms per frame with two lanes against 407.6-443.9 with one (the
+  // spread is host turnaround between pass batches, which the second lane covers), so
+  // one lane stays the default and IZPI_LANES=2 selects two.
+  int lanes = 1;
+  if (const char* e = getenv("IZPI_LANES")) lanes = atoi(e) == 2 && sp.slots >= 2 ? 2 : 1;
+  struct Lane {
+    hipStream_t st;
+    uint32_t* misc;      // [2] trace cursor, [3..4] queue counts, [5] free count (lane 0: ctx->d_misc)
+    uint32_t* hc;        // pinned readback
+    hipEvent_t* ev;
+    int32_t* spill;
+    uint32_t off, slots;
+    uint32_t* q[2];
+    uint32_t* qn[2];
+    WaveParams wp;
+    ShadeParams sp;
+    int cur;
+    uint32_t n;
+  } L[2];
+  if (lanes == 2 && (rc = grow(ctx, (void**)&ctx->d_spill2, &ctx->spill2_cap, ctx->spill_cap))) return rc;
+  const uint32_t half = lanes == 2 ? sp.slots / 2 : sp.slots;
+  for (int l = 0; l < lanes; l++) {
+    Lane& a = L[l];
+    a.st = l ? ctx->stream2 : st;
+    a.misc = l ? ctx->d_misc2 : ctx->d_misc;
+    a.hc = l ? ctx->h_count2 : ctx->h_count;
+    a.ev = l ? ctx->evb2 : ctx->evb;
+    a.spill = l ? ctx->d_spill2 : ctx->d_spill;
+    a.off = l ? half : 0;
+    a.slots = l ? sp.slots - half : half;
+    a.q[0] = ctx->d_queue + a.off;
+    a.q[1] = ctx->d_queue + sp.slots + a.off;
+    a.qn[0] = a.misc + 3;
+    a.qn[1] = a.misc + 4;
+    a.wp = wp;
+    a.wp.rhot = wp.rhot + a.off; a.wp.raux = wp.raux + a.off; a.wp.hhot = wp.hhot + a.off; a.wp.huv = wp.huv + a.off;
+    a.wp.phot = wp.phot + a.off; a.wp.pcold = wp.pcold + a.off;
+    a.wp.trace_next = a.misc + 2;
+    a.wp.slots = a.slots;
+    a.wp.free_q = ctx->d_queue + 2 * (size_t)sp.slots + a.off;
+    a.wp.free_count = a.misc + 5;
+    a.sp = sp;
+    a.sp.slots = a.slots;
+    a.sp.recs = sp.recs + (size_t)a.off * sp.rec_depth * RecLayout<SAMPLER>::D;
+    a.sp.unit_base = a.off;
+    a.cur = 0;
+    a.n = 0;
+  }
+  const uint64_t lane_tail_max = tail_max / (uint64_t)lanes;
   for (uint32_t s0 = 0; s0 < req->spp; s0 += chunk) {
     const uint32_t cs = std::min(chunk, req->spp - s0);
     sp.chunk_spp = cs; sp.s0 = s0; sp.total_units = num_pixels * cs;
     const uint32_t start_slots = std::min<uint32_t>(sp.slots, sp.total_units);
-    HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)start_slots, 1, st));       // head: k_start gives slot i unit i
-    HIP_TRY(hipMemsetAsync(ctx->d_misc + 3, 0, 2 * sizeof(uint32_t), st));  // queue counts
-    wp.q_out = q[0]; wp.q_out_count = qn[0];
-    ShadeParams sp0 = sp;
-    sp0.slots = sp.slots;
-    hipLaunchKernelGGL(k_start<SAMPLER>, dim3((start_slots + 255) / 256), dim3(256), 0, st, ctx->sc, sp0, wp);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    uint32_t n = *ctx->h_count;
-    int cur = 0;
+    HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)start_slots, 1, st));  // head: k_start gives slot i unit i
+    if (lanes == 2) {
+      HIP_TRY(hipEventRecord(ctx->evj, st));
+      HIP_TRY(hipStreamWaitEvent(ctx->stream2, ctx->evj, 0));  // lane 1 after the head reset and the setup copies
+    }
+    for (int l = 0; l < lanes; l++) {
+      Lane& a = L[l];
+      a.sp.chunk_spp = cs; a.sp.s0 = s0; a.sp.total_units = sp.total_units;
+      HIP_TRY(hipMemsetAsync(a.misc + 3, 0, 2 * sizeof(uint32_t), a.st));  // queue counts
+      a.wp.q_out = a.q[0]; a.wp.q_out_count = a.qn[0];
+      const uint32_t fill = std::min<uint32_t>(a.slots, sp.total_units > a.off ? sp.total_units - a.off : 0u);
+      if (fill)
+        hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(a.hc, a.qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, a.st));
+    }
+    for (int l = 0; l < lanes; l++) {
+      HIP_TRY(hipStreamSynchronize(L[l].st));
+      L[l].n = L[l].hc[0];
+      L[l].cur = 0;
+    }
     // Launch passes in batches without a host round-trip per pass: both kernels read
     // their queue length from device memory and exit at once when it is zero, so the
     // host only polls the queue length once per batch (overshoot costs a few empty
     // launches of ~5 us).
     const int B = IZPI_PASS_BATCH;
-    while (n > 0) {
-      for (int b = 0; b < B; b++) {
-        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
-        wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
-        HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
-        HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
-        if (IZPI_SPLIT_REFILL) HIP_TRY(hipMemsetAsync(wp.free_count, 0, sizeof(uint32_t), st));
-        HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
-        launch_trace(ctx, tr, wp, st);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
-        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, ctx->sc, sp, wp);
-        HIP_TRY(hipGetLastError());
-        if (IZPI_SPLIT_REFILL) {
-          hipLaunchKernelGGL(k_refill<SAMPLER>, dim3(refill_res), dim3(256), 0, st, ctx->sc, sp, wp);
+    for (;;) {
+      bool any = false;
+      for (int l = 0; l < lanes; l++) {
+        Lane& a = L[l];
+        if (a.n == 0) continue;
+        any = true;
+        for (int b = 0; b < B; b++) {
+          a.wp.q_in = a.q[a.cur]; a.wp.q_in_count = a.qn[a.cur];
+          a.wp.q_out = a.q[1 - a.cur]; a.wp.q_out_count = a.qn[1 - a.cur];
+          HIP_TRY(hipMemsetAsync(a.misc + 2, 0, sizeof(uint32_t), a.st));
+          HIP_TRY(hipMemsetAsync(a.qn[1 - a.cur], 0, sizeof(uint32_t), a.st));
+          if (IZPI_SPLIT_REFILL) HIP_TRY(hipMemsetAsync(a.wp.free_count, 0, sizeof(uint32_t), a.st));
+          HIP_TRY(hipEventRecord(a.ev[3 * b], a.st));
+          launch_trace(ctx, tr, a.wp, a.st, a.spill);
           HIP_TRY(hipGetLastError());
+          HIP_TRY(hipEventRecord(a.ev[3 * b + 1], a.st));
+          hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
+          HIP_TRY(hipGetLastError());
+          if (IZPI_SPLIT_REFILL) {
+            hipLaunchKernelGGL(k_refill<SAMPLER>, dim3(refill_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
+            HIP_TRY(hipGetLastError());
+          }
+          HIP_TRY(hipEventRecord(a.ev[3 * b + 2], a.st));
+          a.cur = 1 - a.cur;
         }
-        HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
-        cur = 1 - cur;
+        HIP_TRY(hipMemcpyAsync(a.hc, a.misc, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, a.st));
       }
-      HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->d_misc, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      for (int b = 0; b < B; b++) {
-        float t_ms = 0, s_ms = 0;
-        HIP_TRY(hipEventElapsedTime(&t_ms, ctx->evb[3 * b], ctx->evb[3 * b + 1]));
-        HIP_TRY(hipEventElapsedTime(&s_ms, ctx->evb[3 * b + 1], ctx->evb[3 * b + 2]));
-        *trace_ms += t_ms;
-        *shade_ms += s_ms;
-        (*launches)++;
+      if (!any) break;
+      for (int l = 0; l < lanes; l++) {
+        Lane& a = L[l];
+        if (a.n == 0) continue;
+        HIP_TRY(hipStreamSynchronize(a.st));
+        for (int b = 0; b < B; b++) {
+          float t_ms = 0, s_ms = 0;
+          HIP_TRY(hipEventElapsedTime(&t_ms, a.ev[3 * b], a.ev[3 * b + 1]));
+          HIP_TRY(hipEventElapsedTime(&s_ms, a.ev[3 * b + 1], a.ev[3 * b + 2]));
+          *trace_ms += t_ms;
+          *shade_ms += s_ms;
+          (*launches)++;
+        }
+        a.n = a.hc[3 + a.cur];
       }
-      n = ctx->h_count[3 + cur];
-      if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
-        // every unit has started: finish the remaining paths in one k_tail launch
-        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
-        HIP_TRY(hipEventRecord(ctx->evb[0], st));
-        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
-        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->evb[1], st));
-        HIP_TRY(hipEventSynchronize(ctx->evb[1]));
-        float t_ms = 0;
-        HIP_TRY(hipEventElapsedTime(&t_ms, ctx->evb[0], ctx->evb[1]));
-        *tail_ms += t_ms;
-        n = 0;
+      // every unit has started: finish each lane's remaining paths in one k_tail launch
+      // (the unit head is read from lane 0's copy, refreshed this round)
+      const uint32_t head = ctx->h_count[0];
+      for (int l = 0; l < lanes; l++) {
+        Lane& a = L[l];
+        if (a.n > 0 && a.n <= lane_tail_max && head >= sp.total_units) {
+          a.wp.q_in = a.q[a.cur]; a.wp.q_in_count = a.qn[a.cur];
+          HIP_TRY(hipEventRecord(a.ev[0], a.st));
+          if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
+          else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
+          HIP_TRY(hipGetLastError());
+          HIP_TRY(hipEventRecord(a.ev[1], a.st));
+          HIP_TRY(hipEventSynchronize(a.ev[1]));
+          float t_ms = 0;
+          HIP_TRY(hipEventElapsedTime(&t_ms, a.ev[0], a.ev[1]));
+          *tail_ms += t_ms;
+          a.n = 0;
+        }
       }
+    }
+    if (lanes == 2) {  // k_accumulate (stream 0) after lane 1's last pass
+      HIP_TRY(hipEventRecord(ctx->evj, ctx->stream2));
+      HIP_TRY(hipStreamWaitEvent(st, ctx->evj, 0));
     }
     ap.chunk_spp = cs;
     ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
@@ -2258,7 +2346,13 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
     return IZPI_ERR_HIP;
   }
   for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++)
-    if (hipEventCreate(&ctx->evb[i]) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
+    if (hipEventCreate(&ctx->evb[i]) != hipSuccess || hipEventCreate(&ctx->evb2[i]) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&ctx->evj) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->h_count2, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void**)&ctx->d_misc2, 8 * sizeof(uint32_t)) != hipSuccess) {
+    delete ctx;
+    return IZPI_ERR_HIP;
+  }
   *out = ctx;
   return IZPI_OK;
 }
@@ -2267,11 +2361,16 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   if (!ctx) return IZPI_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   free_scene(ctx);
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
-                  ctx->d_counters, ctx->d_rhot, ctx->d_raux, ctx->d_hhot, ctx->d_huv, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post};
+                  ctx->d_counters, ctx->d_rhot, ctx->d_raux, ctx->d_hhot, ctx->d_huv, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post, ctx->d_misc2, ctx->d_spill2};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
+  if (ctx->h_count2) (void)hipHostFree(ctx->h_count2);
+  for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb2[i]) (void)hipEventDestroy(ctx->evb2[i]);
+  if (ctx->evj) (void)hipEventDestroy(ctx->evj);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
   for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb[i]) (void)hipEventDestroy(ctx->evb[i]);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -2635,7 +2734,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
-  launch_trace(ctx, tr, wp, ctx->stream);
+  launch_trace(ctx, tr, wp, ctx->stream, ctx->d_spill);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, hu, n, dh);
   HIP_TRY(hipGetLastError());

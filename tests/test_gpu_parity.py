@@ -452,3 +452,15 @@ def test_render_on_gpu_built_bvh_bitwise(gpu, which):
     rmse = float(np.sqrt(np.mean((img - base) ** 2)))
     assert rmse < RMSE_TOL, rmse
     r.close()
+
+
+def test_two_wavefront_lanes_bitwise(gpu, monkeypatch):
+    """IZPI_LANES=2: slots, queues and records split in two lanes on two streams sharing
+    the unit head; the image and counters are the same."""
+    monkeypatch.setenv("IZPI_LANES", "2")
+    scene = configs.cornell_dragon(1.0, n=40)
+    r = GPURenderer(scene, 64, 64, 16)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 64, 64, 16, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
