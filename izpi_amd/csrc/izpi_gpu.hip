@@ -415,11 +415,15 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot,
 // spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
 // are kept per wave in SGPRs (popcounts of ballots).
 // TRI: the scene holds no spheres (DevScene::tri_only), so the sphere code is compiled out.
+#ifndef IZPI_TRACE_PREQ
+#define IZPI_TRACE_PREQ 1  // prefetch a chunk's queue entries when the chunk is taken
+#endif
 template <int S, int WPE, bool DIST, bool TRI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
+  constexpr bool PREQ = IZPI_TRACE_PREQ != 0;  // chunks of <= 128 entries (make_tracer clamps)
   __shared__ int32_t lds_stack[S * 256];
   // DIST: one wave-wide batch of leaf tests: (primitive << 6 | owner lane), then the
   // test's result flags in the same word; distances and barycentrics
@@ -454,6 +458,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
   uint32_t c_pos = 0, c_end = 0;  // wave-private range [c_pos, c_end) of the input queue
+  // the chunk's queue entries, loaded when the chunk is taken (lane i: entries c_beg + i and
+  // c_beg + 64 + i), so a refill reads its slot with a lane shuffle instead of a dependent
+  // load ahead of the ray load
+  uint32_t c_beg = 0, pre0 = 0, pre1 = 0;
 #ifdef IZPI_TRACE_CLOCKS
   uint64_t k_refill = 0, k_node = 0, k_prim = 0, k_adv = 0, k0 = 0, k1 = 0;
 #define IZPI_CLK(v) (v) = __builtin_readcyclecounter()
@@ -474,17 +482,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (b >= n) exhausted = true;
         c_pos = b;
         c_end = b + chunk < n ? b + chunk : n;
+        c_beg = b;
+        if (PREQ) {
+          pre0 = b + lane < c_end ? wp.q_in[b + lane] : 0u;
+          pre1 = b + 64 + lane < c_end ? wp.q_in[b + 64 + lane] : 0u;
+        }
       }
       if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos < c_end) {
         const uint32_t take = nidle < c_end - c_pos ? nidle : c_end - c_pos;
         const uint32_t base = c_pos;
         c_pos += take;
         bool main_ray = false;
+        const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
+        const uint32_t my = base + rank;
+        uint32_t pslot = 0;
+        if (PREQ) {  // all lanes shuffle (wave-uniform here), idle lanes keep the result
+          const uint32_t k = my - c_beg;
+          const uint32_t s0 = (uint32_t)__shfl((int)pre0, (int)(k & 63));
+          const uint32_t s1 = (uint32_t)__shfl((int)pre1, (int)(k & 63));
+          pslot = k < 64 ? s0 : s1;
+        }
         if (!busy) {
-          const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
-          const uint32_t my = base + rank;
           if (rank < take) {
-            slot = wp.q_in[my];
+            slot = PREQ ? pslot : wp.q_in[my];
             const RayHot& r = wp.rhot[slot];
             tmax = r.tmax;
             main_ray = wp.raux[slot].kind == RAY_MAIN;
@@ -1933,6 +1953,7 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   if (const char* e = getenv("IZPI_TRACE_DIST")) t->p2 = atoi(e) != 0;
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
+  if (IZPI_TRACE_PREQ) t->tchunk = std::min<uint32_t>(t->tchunk, 128);  // two prefetched entries per lane
   if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
   // DIST packs (primitive << 6 | lane) into one LDS word
   if (ctx->num_prims >= (1u << 26)) t->p2 = false;

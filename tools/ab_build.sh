@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p izpi_amd/_lib/variants
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -shared"
-SRC="izpi_amd/csrc/izpi_gpu.hip izpi_amd/csrc/host_scene.cpp"
+SRC="izpi_amd/csrc/izpi_gpu.hip izpi_amd/csrc/bvh_build.hip izpi_amd/csrc/host_scene.cpp izpi_amd/csrc/scene_io.cpp"
 $H $B_FLAGS -o izpi_amd/_lib/variants/B.so $SRC &
 if [ -n "$CLK" ]; then $H -DIZPI_TRACE_CLOCKS -o izpi_amd/_lib/variants/CLK.so $SRC & fi
 wait
