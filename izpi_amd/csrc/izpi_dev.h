@@ -89,6 +89,7 @@ struct DevScene {
   uint32_t nan_free_bounds;     // no NaN in any inner-node bound: slab4_fast allowed
   uint32_t leaf_shortcut;       // every leaf's slot-0 box equals its parent slot's box
   uint32_t tri_only;            // no spheres: leaf tests may be spread over the wave
+  uint32_t no_pathlen;          // no dielectric material: every traced ray is a sampler ray (RAY_MAIN)
   izpi_camera cam;
 };
 

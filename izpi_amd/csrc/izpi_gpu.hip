@@ -507,7 +507,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             slot = PREQ ? pslot : wp.q_in[my];
             const RayHot& r = wp.rhot[slot];
             tmax = r.tmax;
-            main_ray = wp.raux[slot].kind == RAY_MAIN;
+            // ray kinds other than RAY_MAIN exist only with dielectrics (path-length rays)
+            main_ray = sc.no_pathlen || wp.raux[slot].kind == RAY_MAIN;
             ix = (float)(1.0 / r.d[0]); iy = (float)(1.0 / r.d[1]); iz = (float)(1.0 / r.d[2]);
             ox = (float)r.o[0]; oy = (float)r.o[1]; oz = (float)r.o[2];
             fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
@@ -2582,6 +2583,9 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
   sc.tri_only = d->num_spheres == 0 ? 1u : 0u;
+  sc.no_pathlen = 1;
+  for (uint32_t i = 0; i < d->num_materials; i++)
+    if (d->materials[i].kind == IZPI_MAT_DIELECTRIC) sc.no_pathlen = 0;
   sc.leaf_shortcut = leaf_shortcut;
   if (getenv("IZPI_NO_LEAF_SHORTCUT")) sc.leaf_shortcut = 0;
   sc.nan_free_bounds = 1;
