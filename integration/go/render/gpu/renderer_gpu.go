@@ -1,0 +1,253 @@
+//go:build izpi_gpu
+
+// Package gpu is the drop-in MI355X renderer for izpi (SURVEY.md §8(f) row 1).
+//
+// It implements render.Renderer (internal/render/renderer.go:26-28) on top of the C ABI
+// of libizpi_gpu.so (include/izpi_gpu.h, include/izpi_host.h). Copy this directory to
+// internal/render/gpu/ in the izpi tree, put the library and headers under
+// third_party/izpi_amd/{lib,include}, and build with -tags izpi_gpu.
+//
+// The scene crosses the boundary as the transport.Scene protobuf the leader already
+// holds (leader.go:43-112): proto.Marshal on the Go side, izpi_scene_parse_binary and
+// izpi_scene_to_input (transport.ToScene's rules restated in C++) on the other. Image
+// textures are decoded by Go (texture.NewFromFile, leader.go:84-98) and handed over as
+// float64 texels; streamed triangles are appended to the marshalled scene. Nothing here
+// is compiled in this repository (no Go toolchain); it is written against the
+// reference's exported API and the C headers.
+package gpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../third_party/izpi_amd/include
+#cgo LDFLAGS: -L${SRCDIR}/../../../third_party/izpi_amd/lib -lizpi_gpu -Wl,-rpath,${SRCDIR}/../../../third_party/izpi_amd/lib
+#include <stdlib.h>
+#include "izpi_gpu.h"
+#include "izpi_host.h"
+*/
+import "C"
+
+import (
+	"context"
+	"errors"
+	"fmt"
+	"image"
+	"image/color"
+	"unsafe"
+
+	"github.com/flynn-nrg/floatimage/floatimage"
+	pb_transport "github.com/flynn-nrg/izpi/internal/proto/transport"
+	"github.com/flynn-nrg/izpi/internal/render"
+	"github.com/flynn-nrg/izpi/internal/sampler"
+	"github.com/flynn-nrg/izpi/internal/texture"
+	"google.golang.org/protobuf/proto"
+)
+
+// Ensure interface compliance (renderer.go:26-28).
+var _ render.Renderer = (*Renderer)(nil)
+
+// BVH selects the acceleration structure.
+type BVH int
+
+const (
+	// BVHReference rebuilds hitable.NewBVH4's tree bit for bit on the host (≈0.6 s for 800k triangles).
+	BVHReference BVH = iota
+	// BVHGPU builds a PLOC BVH4 on the GPU (≈20 ms); images equal the reference tree's on C1-C5.
+	BVHGPU
+)
+
+// Options are the render.New parameters (renderer.go:73-104) the GPU path uses, plus the device.
+type Options struct {
+	SizeX, SizeY, NumSamples, MaxDepth int
+	Background                         [3]float64    // colours.Black in leader mode (leader.go:140)
+	SpectralBackground                 []float64     // 75 values at the CIE wavelengths, nil = black
+	SamplerType                        sampler.SamplerType
+	Device                             int
+	Seed                               uint64        // master seed of the per-sample LCG streams
+	BVH                                BVH
+	PNGPipeline                        bool          // Gamma + Clamp(1.0) on the GPU (leader.go:179-182)
+}
+
+// Renderer renders one frame per Render call on one MI355X.
+type Renderer struct {
+	ctx   *C.izpi_ctx
+	ps    *C.izpi_proto_scene
+	host  *C.izpi_host_scene
+	req   C.izpi_render_req
+	bgWl  []float64
+	bgVal []float64
+	sizeX int
+	sizeY int
+}
+
+func lastHostError() error { return errors.New(C.GoString(C.izpi_host_last_error())) }
+
+func (r *Renderer) deviceError(what string, rc C.int) error {
+	return fmt.Errorf("%s: status %d: %s", what, int(rc), C.GoString(C.izpi_gpu_last_error(r.ctx)))
+}
+
+// New mirrors render.New for the leader: protoScene as read from the .pbtxt/.izpi file,
+// textures as loaded by the leader (filename -> ImageTxt), streamed triangles if any.
+func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
+	streamed []*pb_transport.Triangle, opt Options) (*Renderer, error) {
+	r := &Renderer{sizeX: opt.SizeX, sizeY: opt.SizeY}
+	ok := false
+	defer func() {
+		if !ok {
+			r.Close()
+		}
+	}()
+	// 1. the scene, in the wire format the C++ ingestion reads
+	scene := proto.Clone(protoScene).(*pb_transport.Scene)
+	if len(streamed) > 0 {
+		if scene.Objects == nil {
+			scene.Objects = &pb_transport.SceneObjects{}
+		}
+		// streamed triangles are embedded after the file's own (transport.go:568-583)
+		scene.Objects.Triangles = append(scene.Objects.Triangles, streamed...)
+	}
+	buf, err := proto.Marshal(scene)
+	if err != nil {
+		return nil, err
+	}
+	if len(buf) == 0 {
+		return nil, errors.New("empty scene")
+	}
+	if rc := C.izpi_scene_parse_binary(unsafe.Pointer(&buf[0]), C.uint64_t(len(buf)), &r.ps); rc != 0 {
+		return nil, lastHostError()
+	}
+	// 2. image textures as float64 NRGBA texels, row 0 = image top, with ImageTxt.Value's
+	//    conversion for 8-bit images (image.go:91-100)
+	for name, it := range textures {
+		texels := toFloat64NRGBA(it.GetData())
+		b := it.GetData().Bounds()
+		cname := C.CString(name)
+		rc := C.izpi_scene_set_image(r.ps, cname, C.uint32_t(b.Dx()), C.uint32_t(b.Dy()), (*C.double)(unsafe.Pointer(&texels[0])))
+		C.free(unsafe.Pointer(cname))
+		if rc != 0 {
+			return nil, lastHostError()
+		}
+	}
+	// 3. transport.ToScene up to the BVH, leader mode aspect W/H (transport.go:522-529)
+	var in *C.izpi_scene_input
+	if rc := C.izpi_scene_to_input(r.ps, C.double(float64(opt.SizeX)/float64(opt.SizeY)), 12345, &in); rc != 0 {
+		return nil, lastHostError()
+	}
+	flags := C.uint32_t(0)
+	if opt.BVH == BVHGPU {
+		flags = C.IZPI_HOST_SKIP_BVH
+	}
+	if rc := C.izpi_host_build_scene_ex(in, flags, &r.host); rc != 0 {
+		return nil, lastHostError()
+	}
+	if rc := C.izpi_gpu_open(C.int(opt.Device), &r.ctx); rc != 0 {
+		return nil, fmt.Errorf("izpi_gpu_open(%d): status %d", opt.Device, int(rc))
+	}
+	// 4. optional GPU BVH4 build, then the upload
+	if opt.BVH == BVHGPU {
+		desc := C.izpi_host_scene_desc(r.host)
+		n := int(desc.num_tris + desc.num_spheres)
+		boxes := make([]float64, 6*n)
+		nodes := make([]C.izpi_bvh4_node, 2*n)
+		order := make([]uint32, n)
+		var numNodes C.uint32_t
+		var ms C.double
+		if n > 0 {
+			C.izpi_host_scene_prim_boxes(r.host, (*C.double)(unsafe.Pointer(&boxes[0])))
+			if rc := C.izpi_gpu_build_bvh4(r.ctx, (*C.double)(unsafe.Pointer(&boxes[0])), C.uint32_t(n), 3, C.IZPI_BVH_PLOC,
+				&nodes[0], C.uint32_t(len(nodes)), &numNodes, (*C.uint32_t)(unsafe.Pointer(&order[0])), &ms); rc != 0 {
+				return nil, r.deviceError("izpi_gpu_build_bvh4", rc)
+			}
+			if rc := C.izpi_host_scene_set_bvh(r.host, &nodes[0], numNodes, (*C.uint32_t)(unsafe.Pointer(&order[0]))); rc != 0 {
+				return nil, lastHostError()
+			}
+		}
+	}
+	if rc := C.izpi_gpu_upload_scene(r.ctx, C.izpi_host_scene_desc(r.host)); rc != 0 {
+		return nil, r.deviceError("izpi_gpu_upload_scene", rc)
+	}
+	// 5. the request: whole frame, Render's post-processing (renderer.go:215-219)
+	desc := C.izpi_host_scene_desc(r.host)
+	r.req.width, r.req.height = C.uint32_t(opt.SizeX), C.uint32_t(opt.SizeY)
+	r.req.spp, r.req.max_depth = C.uint32_t(opt.NumSamples), C.uint32_t(opt.MaxDepth)
+	r.req.out_layout = C.IZPI_OUT_CANVAS
+	r.req.seed = C.uint64_t(opt.Seed)
+	r.req.exposure = desc.camera.exposure // Scene.Exposure = camera exposure
+	for i := 0; i < 3; i++ {
+		r.req.background[i] = C.double(opt.Background[i])
+	}
+	post := C.uint32_t(C.IZPI_POST_NONE)
+	r.req.sampler = C.IZPI_SAMPLER_COLOUR
+	if opt.SamplerType == sampler.SpectralSampler {
+		r.req.sampler = C.IZPI_SAMPLER_SPECTRAL
+		post |= C.IZPI_POST_SPECTRAL // FireflyRejection + XYZToRGB
+		if len(opt.SpectralBackground) == 75 {
+			r.bgWl = make([]float64, 75)
+			r.bgVal = append([]float64(nil), opt.SpectralBackground...)
+			for i := range r.bgWl {
+				r.bgWl[i] = 380 + 5*float64(i)
+			}
+		}
+	}
+	if opt.PNGPipeline {
+		post |= C.IZPI_POST_GAMMA_CLAMP
+	}
+	r.req.post = post
+	ok = true
+	return r, nil
+}
+
+// Render mirrors RendererImpl.Render (renderer.go:108-222): the whole frame in one call.
+func (r *Renderer) Render(ctx context.Context) image.Image {
+	pix := make([]float64, r.sizeX*r.sizeY*4) // floatimage.NewFloat64NRGBA backing store (renderer.go:88)
+	req := r.req
+	if len(r.bgWl) > 0 {
+		// Go slices passed for the duration of the call: they hold no Go pointers
+		req.num_bg_spd = C.uint32_t(len(r.bgWl))
+		req.bg_spd_wavelengths = (*C.double)(unsafe.Pointer(&r.bgWl[0]))
+		req.bg_spd_values = (*C.double)(unsafe.Pointer(&r.bgVal[0]))
+	}
+	var st C.izpi_render_stats
+	if rc := C.izpi_gpu_render(r.ctx, &req, (*C.double)(unsafe.Pointer(&pix[0])), &st); rc != 0 {
+		panic(r.deviceError("izpi_gpu_render", rc)) // the reference log.Fatals on render errors
+	}
+	return floatimage.NewFloat64NRGBA(image.Rect(0, 0, r.sizeX, r.sizeY), pix)
+}
+
+// Close releases the device context and the host-side scene.
+func (r *Renderer) Close() {
+	if r.ctx != nil {
+		C.izpi_gpu_close(r.ctx)
+		r.ctx = nil
+	}
+	if r.host != nil {
+		C.izpi_host_scene_free(r.host)
+		r.host = nil
+	}
+	if r.ps != nil {
+		C.izpi_scene_free(r.ps)
+		r.ps = nil
+	}
+}
+
+// toFloat64NRGBA returns W*H*4 float64 texels, row 0 = image top. Float64NRGBA images are
+// copied as they are; other images go through color.NRGBAModel and /255, which is what
+// ImageTxt.Value does per lookup (image.go:91-100; alpha is not read by the path).
+func toFloat64NRGBA(img image.Image) []float64 {
+	b := img.Bounds()
+	out := make([]float64, 0, b.Dx()*b.Dy()*4)
+	if f, ok := img.(*floatimage.Float64NRGBA); ok {
+		for y := b.Min.Y; y < b.Max.Y; y++ {
+			for x := b.Min.X; x < b.Max.X; x++ {
+				p := f.Float64NRGBAAt(x, y)
+				out = append(out, p.R, p.G, p.B, p.A)
+			}
+		}
+		return out
+	}
+	for y := b.Min.Y; y < b.Max.Y; y++ {
+		for x := b.Min.X; x < b.Max.X; x++ {
+			p := color.NRGBAModel.Convert(img.At(x, y)).(color.NRGBA)
+			out = append(out, float64(p.R)/255.0, float64(p.G)/255.0, float64(p.B)/255.0, float64(p.A)/255.0)
+		}
+	}
+	return out
+}
