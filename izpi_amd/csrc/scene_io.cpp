@@ -308,10 +308,13 @@ double getf(const PMsg* m, const char* name) { return m ? m->num(name) : 0.0; }
 // ------------------------------------------------------------------ text format
 // prototext.Unmarshal (google.golang.org/protobuf/encoding/prototext): unknown fields,
 // a repeated non-repeated field and two members of one oneof are errors.
+constexpr int kMaxNesting = 64;  // transport.proto nests 8 deep; deeper input is malformed
+
 struct TextParser {
   const char* p;
   const char* e;
   int line = 1;
+  int depth = 0;
 
   [[noreturn]] void err(const std::string& m) {
     invalid("pbtxt line " + std::to_string(line) + ": " + m);
@@ -488,7 +491,9 @@ struct TextParser {
           else if (accept('<')) open = '>';
           else err("expected '{' for message field " + name);
           v.m = std::make_shared<PMsg>(msg_def(fd.sub));
+          if (++depth > kMaxNesting) err("messages nested too deeply");
           message_body(*v.m, open);
+          depth--;
           expect(open);
         } else {
           v = scalar(fd);
@@ -508,6 +513,7 @@ struct TextParser {
 struct WireParser {
   const uint8_t* p;
   const uint8_t* e;
+  int depth = 0;
 
   [[noreturn]] void err(const std::string& m) { invalid("izpi (binary protobuf): " + m); }
   uint64_t varint() {
@@ -601,7 +607,8 @@ struct WireParser {
           PVal v; v.s.assign((const char*)p, n); p = end; put(m, fi, std::move(v));
         } else if (fd.type == T_MSG) {
           PVal v; v.m = std::make_shared<PMsg>(msg_def(fd.sub));
-          WireParser sub{p, end}; sub.parse(*v.m); p = end;
+          if (depth + 1 > kMaxNesting) err("messages nested too deeply");
+          WireParser sub{p, end, depth + 1}; sub.parse(*v.m); p = end;
           put(m, fi, std::move(v));
         } else if (fd.repeated) {  // packed
           while (p < end) {

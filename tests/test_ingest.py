@@ -429,3 +429,53 @@ def test_cornell_obj_streams_a_transformed_mesh(tmp_path):
     v = mesh.vertices()[0].astype(np.float32).astype(np.float64)
     assert tris[12:, 0:3].tobytes() == v[:n].tobytes() and tris[12:, 3:6].tobytes() == v[n:2 * n].tobytes()
     HostScene(s, 1.0)
+
+
+def test_parsers_survive_malformed_input():
+    """Mutated scene files, truncated wire data and random OBJ lines end in a status code,
+    never in a crash (the C++ parsers sit behind the C ABI)."""
+    rng = np.random.default_rng(3)
+    text = EXAMPLE.read_bytes()
+    for _ in range(300):
+        b = bytearray(text)
+        for _ in range(rng.integers(1, 6)):
+            i = int(rng.integers(0, len(b)))
+            b[i] = int(rng.integers(0, 256))
+        try:
+            s = ingest.ProtoScene(bytes(b))
+            s.to_input()
+        except RuntimeError:
+            pass
+    wire = _ld(1, b"t") + _ld(4, _vec3(1, 1, 2, 3)) + _ld(8, _ld(2, _vec3(1, 5, 5, 5) + _f32(2, 1) + _ld(3, b"m")))
+    for cut in range(len(wire)):
+        try:
+            ingest.ProtoScene(wire[:cut], binary=True).to_input()
+        except RuntimeError:
+            pass
+    for _ in range(200):
+        junk = bytes(rng.integers(0, 256, int(rng.integers(0, 64)), dtype=np.uint8))
+        try:
+            ingest.ProtoScene(junk, binary=True)
+        except RuntimeError:
+            pass
+    deep = (b'materials { value { lambert { albedo { ' + b"checker { odd { " * 50 + b"}" * 100 + b"} } } }")
+    with pytest.raises(RuntimeError, match="nested"):
+        ingest.ProtoScene(deep)
+    tex = b""
+    for _ in range(100):  # Texture.checker.odd.checker.odd... (CheckerTexture nests Textures)
+        tex = _ld(4, _ld(1, tex))
+    with pytest.raises(RuntimeError, match="nested"):
+        ingest.ProtoScene(_ld(5, _ld(2, _ld(6, _ld(1, tex)))), binary=True)
+    lines = ["v 1 2 3", "vt 0.5 0.5", "vn 0 0 1", "f 1/1/1 1/1/1 1/1/1", "g x", "usemtl m", "o y", "f 1//", "v", "f",
+             "g", "mtllib none.mtl", "s off", "# c"]
+    for _ in range(200):
+        obj = "\n".join(lines[int(k)] for k in rng.integers(0, len(lines), int(rng.integers(1, 20))))
+        try:
+            o = ingest.WavefrontObj(obj, "/nonexistent", 0)
+            for g in range(o.info()["num_groups"]):
+                try:
+                    o.group_to_transport_triangles(g)
+                except RuntimeError:
+                    pass
+        except RuntimeError:
+            pass
