@@ -1521,6 +1521,9 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
 #ifndef IZPI_SHADE_WPE
 #define IZPI_SHADE_WPE 4  // MATSET_BASIC colour register budget: 4 waves/SIMD (measured 4% faster than 3 despite ~26 spilled VGPRs; 5 is 20% slower)
 #endif
+#ifndef IZPI_SHADE_PREQ
+#define IZPI_SHADE_PREQ 1
+#endif
 #ifndef IZPI_SHADE_WPE_OTHER
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
 #endif
@@ -1536,10 +1539,15 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint64_t k_item = 0, k_ref = 0, k_push = 0;
 #endif
   // Block-uniform trip count: the queue and unit reservations are block-wide.
+  // The next iteration's queue entry is loaded one iteration ahead (software pipelining:
+  // one dependent load less in front of the slot's records).
+  uint32_t next_slot = blockIdx.x * 256 + threadIdx.x < n ? wp.q_in[blockIdx.x * 256 + threadIdx.x] : 0u;
   for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < n;
-    uint32_t slot = valid ? wp.q_in[i] : 0;
+    uint32_t slot = next_slot;
+    next_slot = IZPI_SHADE_PREQ && i + stride < n ? wp.q_in[i + stride] : 0u;
+    if (!IZPI_SHADE_PREQ) slot = valid ? wp.q_in[i] : 0;
     bool push = false;      // slot has a ray to trace next
     bool done = false;      // slot's sample finished: grab a new unit
 #ifdef IZPI_SHADE_CLOCKS
