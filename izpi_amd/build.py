@@ -32,8 +32,25 @@ def _stale(target, deps):
     return any(d.stat().st_mtime > t for d in deps)
 
 
+CLI = LIBDIR / "izpi-render"
+CLI_SRC = CSRC / "izpi_render.cpp"
+
+
+def build_cli(force=False, verbose=True):
+    """izpi-render: the C++ host (izpi_amd/csrc/izpi_render.cpp) linked to the library."""
+    if not force and not _stale(CLI, [CLI_SRC, LIB, ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h"]):
+        return CLI
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-o", str(CLI), str(CLI_SRC), "-L" + str(LIBDIR),
+           "-lizpi_gpu", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return CLI
+
+
 def build_gpu(force=False, verbose=True):
     if not force and not _stale(LIB, DEPS):
+        build_cli(force, verbose)
         return LIB
     LIBDIR.mkdir(parents=True, exist_ok=True)
     tmp = LIB.with_suffix(".so.tmp")
@@ -42,6 +59,7 @@ def build_gpu(force=False, verbose=True):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    build_cli(True, verbose)
     return LIB
 
 

@@ -464,3 +464,39 @@ def test_two_wavefront_lanes_bitwise(gpu, monkeypatch):
     ref, ostats = oracle_canvas(scene, 64, 64, 16, N.SAMPLER_COLOUR)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
+
+
+def test_cli_renders_like_the_python_host(gpu, tmp_path):
+    """izpi-render (C++ host, C ABI only) == GPURenderer on the same scene file, bit for bit:
+    the spectral example with Render's post-processing, and an OBJ mesh streamed into the
+    RGB box through the dragon transforms."""
+    import json
+    import subprocess
+    from pathlib import Path
+    from izpi_amd import ingest
+    root = Path(__file__).resolve().parents[1]
+    cli = root / "izpi_amd" / "_lib" / "izpi-render"
+    example = root / "izpi_amd" / "data" / "scenes" / "cornell_box_transparent_pyramid_spectral.pbtxt"
+    raw = tmp_path / "c.f64"
+    out = subprocess.run([str(cli), "--scene", str(example), "--x", "40", "--y", "40", "--samples", "4",
+                          "--raw", str(raw)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["sampler"] == "spectral" and line["bvh"] == "gpu"
+    s = ingest.ProtoScene.from_file(example)
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu")
+    img = r.render(post=N.POST_SPECTRAL)
+    r.close()
+    assert np.fromfile(raw, np.float64).tobytes() == img.tobytes()
+    box = tmp_path / "box.pbtxt"
+    box.write_text(configs.cornell_rgb_pbtxt(1.0))
+    cube = root / "tests" / "golden" / "wavefront" / "cube.obj"
+    out = subprocess.run([str(cli), "--scene", str(box), "--obj", str(cube), "--x", "40", "--y", "40", "--samples", "4",
+                          "--bvh", "reference", "--png-pipeline", "--raw", str(raw)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    sc = configs.cornell_obj(cube)
+    r = GPURenderer(sc, 40, 40, 4)
+    img = r.render(post=N.POST_GAMMA_CLAMP)
+    r.close()
+    assert np.fromfile(raw, np.float64).tobytes() == img.tobytes()

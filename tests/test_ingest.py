@@ -479,3 +479,27 @@ def test_parsers_survive_malformed_input():
                     pass
         except RuntimeError:
             pass
+
+
+def test_cli_constant_and_cpu_behaviour(tmp_path):
+    """izpi-render (the C++ host over the C ABI): its dragon rotation constant is Go's,
+    and on a host without a GPU it reads the scene, then fails cleanly at izpi_gpu_open."""
+    import re
+    import subprocess
+    src = (ROOT / "izpi_amd" / "csrc" / "izpi_render.cpp").read_text()
+    m = re.search(r"kMinus60Deg = (-0x[0-9a-fp.+-]+);", src)
+    assert float.fromhex(m.group(1)) == -ingest.go_radians(60)
+    cli = ROOT / "izpi_amd" / "_lib" / "izpi-render"
+    bad = tmp_path / "scene.json"
+    bad.write_text("{}")
+    r = subprocess.run([str(cli), "--scene", str(bad)], capture_output=True, text=True)
+    assert r.returncode == 1 and "Unknown scene file extension" in r.stderr
+    r = subprocess.run([str(cli), "--scene", str(EXAMPLE), "--x", "8", "--y", "8", "--samples", "1"],
+                       capture_output=True, text=True)
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if not has_gpu:
+        assert r.returncode == 1 and "izpi_gpu_open failed" in r.stderr, r.stderr
