@@ -74,6 +74,19 @@ IZPI_DEV V3 tex_rgb(const DevScene& sc, int32_t id, double u, double v) {
   }
   return mk(t.value[0], t.value[1], t.value[2]);
 }
+// First interval [wl[i], wl[i+1]] of a NON-DECREASING table that holds w, for
+// n >= 2 and wl[0] <= w <= wl[n-1]: i = (first j >= 1 with wl[j] >= w) - 1, which is the interval
+// the reference's linear scan stops at (spectral.go:151-181, spectral_constant.go:88-106):
+// every earlier interval ends below w. ~log2(n) dependent loads instead of up to n.
+IZPI_DEV uint32_t sorted_interval(const double* wl, uint32_t n, double w) {
+  uint32_t lo = 1, hi = n - 1;  // wl[n-1] >= w, so the answer is in [1, n-1]
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (wl[mid] >= w) hi = mid; else lo = mid + 1;
+  }
+  return lo - 1;
+}
+
 // texture.SpectralConstant.Value (spectral_constant.go:65-106)
 IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda) {
   const izpi_texture& t = sc.textures[id];
@@ -84,6 +97,12 @@ IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda) {
     if (n == 0) return 0.0;
     if (lambda < wl[0]) return vl[0];
     if (lambda > wl[n - 1]) return vl[n - 1];
+    if (t.pad0 && lambda == lambda) {  // pad0: wavelengths non-decreasing (set at upload)
+      const uint32_t i = sorted_interval(wl, n, lambda);
+      const double w1 = wl[i], w2 = wl[i + 1];
+      const double tt = (lambda - w1) / (w2 - w1);
+      return vl[i] + tt * (vl[i + 1] - vl[i]);
+    }
     for (uint32_t i = 0; i + 1 < n; i++) {
       double w1 = wl[i], w2 = wl[i + 1];
       if (lambda >= w1 && lambda <= w2) {
@@ -97,10 +116,16 @@ IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda) {
   return t.peak * gm::exp(exponent);
 }
 // SpectralPowerDistribution.Value (spectral.go:151-181)
-IZPI_DEV double spd_value(const double* wl, const double* vl, uint32_t n, double w) {
+IZPI_DEV double spd_value(const double* wl, const double* vl, uint32_t n, double w, bool sorted = false) {
   if (n == 0) return 0.0;
   if (w <= wl[0]) return vl[0];
   if (w >= wl[n - 1]) return vl[n - 1];
+  if (sorted && w == w) {  // (NaN falls through to the scan, which matches no interval)
+    const uint32_t i = sorted_interval(wl, n, w);
+    const double w1 = wl[i], w2 = wl[i + 1];
+    const double t = (w - w1) / (w2 - w1);
+    return vl[i] + t * (vl[i + 1] - vl[i]);
+  }
   for (uint32_t i = 0; i + 1 < n; i++) {
     double w1 = wl[i], w2 = wl[i + 1];
     if (w >= w1 && w <= w2) {
@@ -967,6 +992,7 @@ struct ShadeParams {
   uint32_t num_bg_spd, slots;
   uint32_t rec_depth;          // records per slot (max(1, max_depth))
   uint32_t unit_base;          // k_start: slot i of this lane starts unit unit_base + i
+  uint32_t bg_sorted;          // background SPD wavelengths non-decreasing (binary-search lookups)
   const uint32_t* tiles;
   const double* bg_wl;
   const double* bg_val;
@@ -1076,7 +1102,7 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
 
 IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colour) {
   // colour.go:34-36 returns blue; sampler/spectral.go:48-51 the background SPD.
-  return colour ? mk(0, 0, 1.0) : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
+  return colour ? mk(0, 0, 1.0) : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda, sp.bg_sorted != 0), 0, 0);
 }
 
 // Start the path of work unit `unit` in `slot`: per-sample LCG streams, wavelength
@@ -1367,7 +1393,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
     next_d = rd;
   } else if (H.prim < 0) {
     L = COLOUR ? mk(sp.background[0], sp.background[1], sp.background[2])
-               : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda), 0, 0);
+               : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda, sp.bg_sorted != 0), 0, 0);
     terminal = true;
   } else {
     const GShade gs = sc.shade[H.prim];
@@ -2278,6 +2304,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   ShadeParams sp{};
   sp.width = req->width; sp.height = req->height; sp.max_depth = req->max_depth;
   sp.tile_w = tw; sp.tile_h = th; sp.num_bg_spd = (uint32_t)nbg; sp.slots = slots;
+  sp.bg_sorted = nbg >= 2;
+  for (size_t i = 1; i < nbg; i++)
+    if (!(req->bg_spd_wavelengths[i - 1] <= req->bg_spd_wavelengths[i])) sp.bg_sorted = 0;
   sp.tiles = ctx->d_tiles; sp.bg_wl = ctx->d_bg; sp.bg_val = ctx->d_bg + nbg;
   sp.background[0] = req->background[0]; sp.background[1] = req->background[1]; sp.background[2] = req->background[2];
   sp.rec_depth = depth_cap;
@@ -2581,7 +2610,19 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(lights.data(), lights.size(), &dlt);
   UP(d->materials, d->num_materials, &dm);
   UP(mflags.data(), mflags.size(), &dmf);
-  UP(d->textures, d->num_textures, &dtx);
+  // device copy of the textures: pad0 = 1 marks a tabulated SPD with non-decreasing
+  // wavelengths, which tex_spectral searches by bisection
+  std::vector<izpi_texture> texs(d->textures, d->textures + d->num_textures);
+  for (izpi_texture& t : texs) {
+    t.pad0 = 0;
+    if (t.kind != IZPI_TEX_SPECTRAL_TABULATED || t.spd_count < 2) continue;  // n = 1: the scan returns 0.0
+    if ((uint64_t)t.spd_offset + t.spd_count > d->num_spd) { ctx->err = "SPD range out of bounds"; return IZPI_ERR_INVALID; }
+    bool sorted = true;
+    for (uint32_t i = 1; i < t.spd_count; i++)
+      if (!(d->spd_wavelengths[t.spd_offset + i - 1] <= d->spd_wavelengths[t.spd_offset + i])) sorted = false;
+    t.pad0 = sorted ? 1u : 0u;
+  }
+  UP(texs.data(), d->num_textures, &dtx);
   UP(d->texels, d->num_texels, &dtex);
   UP(d->spd_wavelengths, d->num_spd, &dswl);
   UP(d->spd_values, d->num_spd, &dsv);

@@ -500,3 +500,41 @@ def test_cli_renders_like_the_python_host(gpu, tmp_path):
     img = r.render(post=N.POST_GAMMA_CLAMP)
     r.close()
     assert np.fromfile(raw, np.float64).tobytes() == img.tobytes()
+
+
+@pytest.mark.parametrize("table", ["duplicates", "unsorted", "single"])
+def test_spectral_table_lookups_bitwise(gpu, table):
+    """Tabulated SPD lookups (spectral_constant.go:88-106, spectral.go:151-181): the device
+    bisects non-decreasing tables and scans the others; both must pick the reference's
+    first matching interval. Tables with repeated wavelengths (0/0 at the tie), out of
+    order, and with one entry, in the light, the glass index and a background SPD."""
+    from izpi_amd.scene import Scene
+    tabs = configs.spectral_tables()
+    wl = list(tabs["cie_wavelengths"])
+    light = list(tabs["light_sources"]["cie_f1_daylight_fluorescent"])
+    if table == "duplicates":
+        wl_l = wl[:10] + [wl[10]] * 3 + wl[13:]
+        ref = ([380, 500, 500, 500, 620, 750], [1.55, 1.5, 1.52, 1.49, 1.47, 1.45])
+        bg = (np.array([380.0, 450, 450, 600, 780]), np.array([0.1, 0.2, 0.3, 0.05, 0.4]))
+    elif table == "unsorted":
+        wl_l = wl[:20] + [wl[25], wl[21], wl[22], wl[23], wl[24], wl[20]] + wl[26:]
+        ref = ([380, 620, 500, 560, 750], [1.55, 1.47, 1.5, 1.48, 1.45])
+        bg = (np.array([380.0, 600, 450, 780]), np.array([0.1, 0.2, 0.3, 0.4]))
+    else:
+        wl_l = wl
+        ref = ([550], [1.5])
+        bg = (np.array([550.0]), np.array([0.25]))
+    s = Scene("spd_tables")
+    mats = {"Green": s.lambert(spectral=s.spectral_gaussian(0.9, 540, 40)),
+            "Red": s.lambert(spectral=s.spectral_tabulated([400, 600, 600, 700], [0.1, 0.8, 0.6, 0.9])),
+            "White": s.lambert(spectral=s.spectral_neutral(0.73)),
+            "light": s.diffuse_light(spectral=s.spectral_spd(wl_l, light))}
+    glass = s.dielectric(spectral_refidx=s.spectral_tabulated(*ref), spectral_absorb=s.spectral_neutral(0.01))
+    configs.add_box(s, mats)
+    s.add_sphere((50, 30, 50), 15, glass)
+    s.set_camera((50, 50, -120), (50, 50, 50), (0, 1, 0), 35, 1.0, 0, 10, 0, 1, 1.0)
+    r = GPURenderer(s, 40, 40, 8, sampler=N.SAMPLER_SPECTRAL, spectral_background=bg)
+    img = r.render()
+    ref_img, ostats = oracle_canvas(s, 40, 40, 8, N.SAMPLER_SPECTRAL, bg=bg)
+    assert_parity(img, ref_img, r.stats, ostats)
+    r.close()
