@@ -45,6 +45,17 @@ __constant__ double c_cie_wl[IZPI_CIE_N] = IZPI_CIE_WAVELENGTHS_INIT;
 __constant__ double c_cie_x[IZPI_CIE_N] = IZPI_CIE_X_INIT;
 __constant__ double c_cie_y[IZPI_CIE_N] = IZPI_CIE_Y_INIT;
 __constant__ double c_cie_z[IZPI_CIE_N] = IZPI_CIE_Z_INIT;
+// Running sums of CIE y in SampleWavelength's own order (current += y from 0): entry i is
+// the loop's `current + y` at step i, so a bisection over it stops where the scan stops.
+struct CieCum { double v[IZPI_CIE_N]; };
+constexpr CieCum cie_y_running_sums() {
+  CieCum c{};
+  constexpr double y[IZPI_CIE_N] = IZPI_CIE_Y_INIT;
+  double cur = 0.0;
+  for (int i = 0; i < IZPI_CIE_N; i++) { c.v[i] = cur + y[i]; cur += y[i]; }
+  return c;
+}
+__constant__ CieCum c_cie_ycum = cie_y_running_sums();
 
 namespace izpi_bvh {  // bvh_build.hip
 int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, uint32_t method,
@@ -135,38 +146,41 @@ IZPI_DEV double spd_value(const double* wl, const double* vl, uint32_t n, double
   }
   return 0.0;
 }
-// spectral.SampleWavelength (spectral.go:184-224)
+// spectral.SampleWavelength (spectral.go:184-224): the scan stops at the first i whose
+// running sum reaches the target (y >= 0, so the sums never decrease): bisected.
 IZPI_DEV void sample_wavelength(double random, double& lambda, double& pdf) {
-  double target = random * IZPI_CIE_Y_INTEGRAL;
-  double current = 0.0;
-#pragma unroll 1
-  for (int i = 0; i < IZPI_CIE_N; i++) {
-    double y = c_cie_y[i];
-    if (current + y >= target) {
-      if (i > 0) {
-        double prev = current;
-        double t = (target - prev) / y;
-        lambda = c_cie_wl[i - 1] + t * (c_cie_wl[i] - c_cie_wl[i - 1]);
-        double iy = c_cie_y[i - 1] + t * (c_cie_y[i] - c_cie_y[i - 1]);
-        pdf = iy / IZPI_CIE_Y_INTEGRAL;
-        return;
-      }
-      lambda = c_cie_wl[i];
-      pdf = y / IZPI_CIE_Y_INTEGRAL;
-      return;
-    }
-    current += y;
+  const double target = random * IZPI_CIE_Y_INTEGRAL;
+  const double* cum = c_cie_ycum.v;
+  if (!(cum[IZPI_CIE_N - 1] >= target)) {  // the scan ran off the end
+    lambda = 750;
+    pdf = c_cie_y[IZPI_CIE_N - 1] / IZPI_CIE_Y_INTEGRAL;
+    return;
   }
-  lambda = 750;
-  pdf = c_cie_y[IZPI_CIE_N - 1] / IZPI_CIE_Y_INTEGRAL;
+  uint32_t lo = 0, hi = IZPI_CIE_N - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cum[mid] >= target) hi = mid; else lo = mid + 1;
+  }
+  const uint32_t i = lo;
+  const double y = c_cie_y[i];
+  if (i > 0) {
+    const double prev = cum[i - 1];
+    const double t = (target - prev) / y;
+    lambda = c_cie_wl[i - 1] + t * (c_cie_wl[i] - c_cie_wl[i - 1]);
+    const double iy = c_cie_y[i - 1] + t * (c_cie_y[i] - c_cie_y[i - 1]);
+    pdf = iy / IZPI_CIE_Y_INTEGRAL;
+    return;
+  }
+  lambda = c_cie_wl[i];
+  pdf = y / IZPI_CIE_Y_INTEGRAL;
 }
-// spectral.GetCIEValues (spectral.go:227-253)
+// spectral.GetCIEValues (spectral.go:227-253); the index scan over the ascending CIE
+// wavelengths is bisected (sorted_interval returns index - 1)
 IZPI_DEV void cie_values(double w, double& x, double& y, double& z) {
   if (w <= c_cie_wl[0]) { x = c_cie_x[0]; y = c_cie_y[0]; z = c_cie_z[0]; return; }
   if (w >= c_cie_wl[IZPI_CIE_N - 1]) { x = c_cie_x[IZPI_CIE_N - 1]; y = c_cie_y[IZPI_CIE_N - 1]; z = c_cie_z[IZPI_CIE_N - 1]; return; }
   int index = 0;
-#pragma unroll 1
-  for (int i = 0; i < IZPI_CIE_N; i++) if (c_cie_wl[i] >= w) { index = i; break; }
+  if (w == w) index = (int)sorted_interval(c_cie_wl, IZPI_CIE_N, w) + 1;
   double w1 = c_cie_wl[index - 1], w2 = c_cie_wl[index];
   double t = (w - w1) / (w2 - w1);
   x = c_cie_x[index - 1] + t * (c_cie_x[index] - c_cie_x[index - 1]);
@@ -1868,6 +1882,8 @@ __global__ void k_gomath(int op, const double* x, const double* y, uint32_t n, d
     case 8: r = gm::sqrt(a); break;
     case 9: r = a / b; break;
     case 10: r = gm::atan(a); break;
+    case 32: case 33: { double l, pdf; sample_wavelength(a, l, pdf); r = op == 32 ? l : pdf; break; }
+    case 34: case 35: case 36: { double cx, cy, cz; cie_values(a, cx, cy, cz); r = op == 34 ? cx : op == 35 ? cy : cz; break; }
     default: r = gm::nan();
   }
   out[i] = r;

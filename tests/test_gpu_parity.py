@@ -538,3 +538,41 @@ def test_spectral_table_lookups_bitwise(gpu, table):
     ref_img, ostats = oracle_canvas(s, 40, 40, 8, N.SAMPLER_SPECTRAL, bg=bg)
     assert_parity(img, ref_img, r.stats, ostats)
     r.close()
+
+
+def test_spectral_sampling_device_bitwise(gpu):
+    """SampleWavelength and GetCIEValues on the device (bisected over the CIE tables)
+    equal the oracle's linear scans, including randoms that land on the running sums'
+    entries and wavelengths on the table's grid points and ends."""
+    r = GPURenderer(configs.cornell_rgb(), 8, 8, 1)
+    L = N.lib()
+    rng = np.random.default_rng(11)
+    tabs = configs.spectral_tables()
+    wl = np.asarray(tabs["cie_wavelengths"], np.float64)
+    y = np.asarray(tabs["cie_y"], np.float64)
+    rand = [rng.random(20000), np.array([0.0, 0.5, np.nextafter(1.0, 0.0)])]
+    cum = np.cumsum(y)  # sequential float64 sums, the reference's running `current`
+    integ = float(tabs["cie_y_integral"])
+    rand.append(np.concatenate([cum / integ, np.nextafter(cum / integ, 0), np.nextafter(cum / integ, 2)]))
+    rand = np.ascontiguousarray(np.concatenate(rand).clip(0, np.nextafter(1.0, 0.0)))
+    lams = np.ascontiguousarray(np.concatenate([rng.uniform(370, 790, 20000), wl, np.nextafter(wl, 0),
+                                                np.nextafter(wl, 1e4), [379.0, 380.0, 780.0, 800.0]]))
+    def dev(op, x):
+        out = np.zeros_like(x)
+        assert L.izpi_gpu_gomath(r.ctx, op, O.dptr(x), None, len(x), O.dptr(out)) == 0
+        return out
+    lam, pdf = dev(32, rand), dev(33, rand)
+    l_ref, p_ref = np.zeros_like(rand), np.zeros_like(rand)
+    a, b = C.c_double(), C.c_double()
+    for k, v in enumerate(rand):
+        O.lib().oracle_sample_wavelength(float(v), C.byref(a), C.byref(b))
+        l_ref[k], p_ref[k] = a.value, b.value
+    assert lam.tobytes() == l_ref.tobytes() and pdf.tobytes() == p_ref.tobytes()
+    xyz = np.stack([dev(op, lams) for op in (34, 35, 36)], 1)
+    ref = np.zeros((len(lams), 3))
+    o3 = (C.c_double * 3)()
+    for k, v in enumerate(lams):
+        O.lib().oracle_cie_values(float(v), o3)
+        ref[k] = list(o3)
+    assert xyz.tobytes() == ref.tobytes()
+    r.close()
