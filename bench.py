@@ -5,23 +5,39 @@ Cornell box with the synthetic ~817k-triangle dragon, Colour sampler, maxDepth 5
 1024x1024 pixels x 512 spp = 536,870,912 samples per frame.
 
 One step = one full frame through the hot path (BVH4 traversal, shading, light pdfs,
-ordered per-pixel accumulation) with the scene already resident in HBM. With N GPUs
-(one process each, torchrun) the frame's 32x32 tiles are dealt round-robin to ranks
-and the packed tiles are gathered to rank 0 over RCCL inside the timed step
-(strong scaling: total work fixed). Timing: barrier + synchronize on both sides of
-the K timed steps, max over ranks.
+ordered per-pixel accumulation) with the scene already resident in HBM. Timing: barrier
++ synchronize on both sides of the K timed steps, max over ranks.
+
+GPUs (strong scaling: the frame is fixed, its 32x32 tiles are dealt tile % N):
+  * under torchrun (WORLD_SIZE set): one process per GPU, each renders its share and the
+    library's own RCCL communicator gathers the shares to rank 0 (izpi_gpu_render_rank);
+    gloo carries only the launcher's barrier, the communicator id and the max of times;
+  * `--gpus N` without torchrun: ONE process drives N GPUs through izpi_gpu_multi_render
+    (a host thread and stream per GPU, xGMI peer copies to GPU 0).
+  Both forms do the gather inside the timed step.
 
 The JSON line also carries
-  roofline:     achieved algorithmic GB/s of the dominant kernel (k_trace) — node,
-                triangle and sphere bytes of SURVEY.md §8(d) counted exactly by the
-                kernel (== oracle counts) over its HIP-event time — against 8 TB/s.
+  roofline:     the dominant kernel k_trace2 against HBM peak. `achieved` = HBM traffic
+                per frame, measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+                MI355X_MICROARCH.md's gfx950 correction) over a one-frame child run of this
+                same revision, divided by k_trace2's HIP-event time per frame in the timed
+                run. `achieved_algorithmic` is SURVEY.md §8(d)'s model (128 B per node
+                visit, 72 B per triangle test, 32 B per sphere test, counted exactly by the
+                kernel) over the same time: those bytes are mostly served by L2 and the
+                Infinity Cache, so it is not bounded by HBM peak. TCC hit rates come from a
+                third PMC pass.
   cpu_baseline: the CPU oracle (deterministic restatement of the Go hot path) on a
-                bounded sample of the same frame on this host's cores (rank 0, N=1).
+                bounded sample of the same frame on the CPUs this process may use (rank 0,
+                N=1), with the host's CPU model and core counts.
 """
 import argparse
+import csv
 import json
+import math
 import os
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -29,17 +45,23 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_PASSES = {"fetch": ["FETCH_SIZE"], "write": ["WRITE_SIZE"], "tcc": ["TCC_HIT_sum", "TCC_MISS_sum"]}
+KERNELS = {"k_trace2": "k_trace2<", "k_shade": "k_shade<"}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None, help="GPUs (default: WORLD_SIZE under torchrun, else 1)")
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="C3")
     p.add_argument("--spp", type=int, default=None, help="override spp (debug only; the metric uses 512)")
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes (roofline traffic)")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher plumbing only (rank setup, tile shares, barriers, max of times): no GPU work")
     p.add_argument("--scene", default=None, help="render a transport.Scene file (.pbtxt/.izpi) at the config's size")
     p.add_argument("--bvh", default="gpu", choices=["reference", "gpu"],
                    help="gpu (default): the GPU linear BVH4 builder, checked at N=1 against a frame on the "
@@ -49,79 +71,36 @@ def parse():
                    help="skip the reference-tree frame (timing and image comparison) of --bvh gpu")
     p.add_argument("--obj", default=None, help="C3 with this OBJ mesh (e.g. the Stanford dragon) instead of the "
                                                "synthetic one")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def pmc_traffic(config):
-    """HBM bytes per k_trace launch from the committed rocprofv3 PMC pass, if any
-    (keyed "<config>/<bvh>", e.g. "C3/gpu")."""
-    f = ROOT / "profiles" / "pmc_summary.json"
-    if not f.exists():
-        return None
+# ---------------------------------------------------------------- host facts
+def host_cpus():
+    """CPUs this process may use (affinity, capped by a cgroup CPU quota), and the host's."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
     try:
-        d = json.loads(f.read_text())
-        return d.get(config, {}).get("hbm_bytes_per_trace_launch")
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
     except Exception:
-        return None
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"usable": usable, "affinity": aff, "cgroup_cpus": quota, "host_threads": os.cpu_count(), "model": model}
 
 
-def cpu_baseline(cfg, scene, budget_s, spp):
-    """Oracle render of a bounded sample of the same frame (centre tiles, full spp when
-    it fits the budget), timed on this host's cores."""
-    import numpy as np
-    from izpi_amd import _native as N
-    from izpi_amd.renderer import common_tiles
-    from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
-    o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
-    tiles = common_tiles(cfg.width, cfg.height)
-    # calibrate on one tile at 2 spp, then size the sample for the budget
-    def run(ts, s):
-        req = N.RenderReq(width=cfg.width, height=cfg.height, spp=s, max_depth=cfg.max_depth, sampler=cfg.sampler,
-                          seed=12345)
-        t = np.ascontiguousarray(ts, np.uint32)
-        req.num_tiles = len(t)
-        req.tiles = t.ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_uint32))
-        _, st = o.render(req, threads=threads)
-        return st
-    st = run(tiles[:threads], 2)
-    rate = st["samples"] / max(st["seconds"], 1e-6)
-    px_per_tile = int((tiles[0, 2] - tiles[0, 0] + 1) * (tiles[0, 3] - tiles[0, 1] + 1))
-    want_samples = rate * budget_s
-    s = spp
-    ntiles = int(want_samples // (px_per_tile * s))
-    if ntiles < threads:
-        ntiles = threads
-        s = max(1, int(want_samples // (px_per_tile * ntiles)))
-    ntiles = min(ntiles, len(tiles))
-    stride = max(1, len(tiles) // ntiles)
-    st = run(tiles[::stride][:ntiles], s)  # tiles spread over the whole frame
-    o.close()
-    return {"value": st["samples"] / st["seconds"] / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%s: %d evenly spread tiles (%d px) x %d spp = %d samples, %.1f s on %d threads of the CPU oracle "
-                      "(C++ restatement of the Go hot path, per-sample RNG streams)"
-                      % (cfg.name, ntiles, ntiles * px_per_tile, s, st["samples"], st["seconds"], threads)}
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    from izpi_amd import build
-    build.build_gpu(verbose=False)
+# ---------------------------------------------------------------- scene/config
+def load_config(args):
     from izpi_amd import configs
-    from izpi_amd.renderer import GPURenderer
-
     cfg = configs.configs()[args.config]
-    spp = args.spp or cfg.spp
     t0 = time.time()
     scene = None if (args.scene or args.obj) else cfg.build()
     if args.scene:  # leader.go:43-112: file scene, SPECTRAL scenes use the spectral sampler
@@ -133,92 +112,358 @@ def main():
         scene = configs.cornell_obj(args.obj, cfg.width / cfg.height)
         cfg = configs.Config("%s (mesh %s)" % (cfg.name, Path(args.obj).name), cfg.width, cfg.height, cfg.spp,
                              cfg.sampler, None, cfg.max_depth)
-    scene_s = time.time() - t0
+    return cfg, scene, time.time() - t0
+
+
+STAT_KEYS = ("node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests", "rays", "kernel_ms",
+             "shade_ms", "total_ms", "launches", "samples", "node_steps", "prim_steps", "leaf_shortcuts", "tail_ms",
+             "tail_node_visits", "tail_tri_tests", "tail_sph_tests", "parks")
+
+
+def add_stats(agg, st):
+    for k in STAT_KEYS:
+        agg[k] += float(st[k]) if st else 0.0
+
+
+# ---------------------------------------------------------------- PMC passes
+def pmc_children(args, timeout=240):
+    """rocprofv3 --pmc passes over a one-frame child of this bench (same workload,
+    single GPU): per-kernel counter sums and dispatch counts."""
+    out = {}
+    base = [sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config, "--steps", "1",
+            "--warmup", "0", "--bvh", args.bvh]
+    if args.spp:
+        base += ["--spp", str(args.spp)]
+    if args.scene:
+        base += ["--scene", args.scene]
+    if args.obj:
+        base += ["--obj", args.obj]
+    if args.bvh_leaf_max:
+        base += ["--bvh-leaf-max", str(args.bvh_leaf_max)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for name, counters in PMC_PASSES.items():
+        d = tempfile.mkdtemp(prefix="izpi_pmc_", dir="/tmp")
+        cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run", "--", *base]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+        except Exception as e:  # missing profiler, timeout: report, no traffic figure
+            out["error"] = "%s pass: %s" % (name, e)
+            return out
+        if r.returncode != 0:
+            out["error"] = "%s pass: rc %d: %s" % (name, r.returncode, r.stderr[-400:])
+            return out
+        for f in Path(d).rglob("*counter_collection.csv"):
+            for row in csv.DictReader(open(f)):
+                for short, pat in KERNELS.items():
+                    if pat in row["Kernel_Name"]:
+                        e = out.setdefault(short, {"dispatches": set()})
+                        e[row["Counter_Name"]] = e.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                        e["dispatches"].add((name, row["Dispatch_Id"]))
+    for short in KERNELS:
+        if short in out:
+            out[short]["dispatches"] = len([x for x in out[short]["dispatches"] if x[0] == "fetch"])
+    return out
+
+
+def traffic_summary(pmc):
+    """Bytes per frame and TCC hit rates per kernel from the PMC passes. FETCH_SIZE and
+    WRITE_SIZE are in KB; gfx950 reports half of the bytes of wide reads, so FETCH_SIZE is
+    doubled (MI355X_MICROARCH.md, HBM section). Both count L2 memory-side requests
+    (Infinity-Cache hits included), an upper bound of the HBM bytes."""
+    out = {}
+    for short in KERNELS:
+        e = pmc.get(short)
+        if not e or "FETCH_SIZE" not in e or "WRITE_SIZE" not in e:
+            continue
+        fb = 2.0 * 1024.0 * e["FETCH_SIZE"]
+        wb = 1024.0 * e["WRITE_SIZE"]
+        hit, miss = e.get("TCC_HIT_sum"), e.get("TCC_MISS_sum")
+        out[short] = {"fetch_bytes_per_frame": fb, "write_bytes_per_frame": wb, "bytes_per_frame": fb + wb,
+                      "dispatches": e["dispatches"],
+                      "tcc_hit_rate": hit / (hit + miss) if hit is not None and miss and hit + miss > 0 else None}
+    return out
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_baseline(cfg, scene, budget_s, spp, bvh):
+    """Oracle render of a bounded sample of the same frame (tiles spread over the frame,
+    full spp when it fits the budget), timed on the CPUs this process may use."""
+    import ctypes as C
+    import numpy as np
     from izpi_amd import _native as N
+    from izpi_amd.renderer import common_tiles
+    from oracle import oracle as O
+    cpus = host_cpus()
+    threads = cpus["usable"]
+    o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
+    tiles = common_tiles(cfg.width, cfg.height)
+
+    def run(ts, s):
+        req = N.RenderReq(width=cfg.width, height=cfg.height, spp=s, max_depth=cfg.max_depth, sampler=cfg.sampler,
+                          seed=12345)
+        t = np.ascontiguousarray(ts, np.uint32)
+        req.num_tiles = len(t)
+        req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
+        _, st = o.render(req, threads=threads)
+        return st
+    # calibrate on one tile per thread at 2 spp, then size the sample for the budget
+    st = run(tiles[:threads], 2)
+    rate = st["samples"] / max(st["seconds"], 1e-6)
+    px_per_tile = int((tiles[0, 2] - tiles[0, 0] + 1) * (tiles[0, 3] - tiles[0, 1] + 1))
+    want_samples = rate * budget_s
+    s = spp
+    ntiles = int(want_samples // (px_per_tile * s))
+    if ntiles < threads:
+        ntiles = threads
+        s = max(1, int(want_samples // (px_per_tile * ntiles)))
+    ntiles = min(ntiles, len(tiles))
+    stride = max(1, len(tiles) // ntiles)
+    st = run(tiles[::stride][:ntiles], s)
+    o.close()
+    value = st["samples"] / st["seconds"] / 1e6
+    res = {"value": value, "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": "%s: %d evenly spread tiles (%d px) x %d spp = %d samples, %.1f s on %d threads of the CPU "
+                     "oracle (C++ restatement of the Go hot path, per-sample RNG streams, izpi's own BVH4 tree)"
+                     % (cfg.name, ntiles, ntiles * px_per_tile, s, st["samples"], st["seconds"], threads),
+           "cpu_model": cpus["model"], "host_threads": cpus["host_threads"], "affinity_cpus": cpus["affinity"],
+           "cgroup_cpus": cpus["cgroup_cpus"]}
+    if cpus["host_threads"] and cpus["host_threads"] > threads:
+        # the box gives this process `threads` CPUs of a larger host: linear extrapolation to
+        # every hardware thread of the host (an upper bound: SMT siblings add less than a core)
+        res["extrapolated_all_host_threads"] = value * cpus["host_threads"] / threads
+    return res
+
+
+# ---------------------------------------------------------------- launcher plumbing
+def dist_setup(world, rank):
+    """gloo group for the launcher's barrier / id broadcast / max of times (CPU only)."""
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def dry_run(args, world, rank, mode):
+    """The launcher without GPU work: share dealing over the frame (izpi_host_share_tiles),
+    barriers and the max of per-rank times; prints the JSON skeleton on rank 0."""
+    import numpy as np
+    from izpi_amd import configs, sharding
+    from izpi_amd.renderer import common_tiles
+    cfg = configs.configs()[args.config]
+    tiles = common_tiles(cfg.width, cfg.height)
+    n = world if mode == "ranks" else (args.gpus or 1)
+    dist = dist_setup(world, rank) if mode == "ranks" else None
+    mine = [sharding.shard_tiles(tiles, r, n) for r in range(n)] if mode != "ranks" else \
+        [sharding.shard_tiles(tiles, rank, n)]
+    t0 = time.perf_counter()
+    covered = sum(len(m) for m in mine)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        dist.barrier()
+        tc = torch.tensor([covered, elapsed], dtype=torch.float64)
+        dist.all_reduce(tc[:1], op=dist.ReduceOp.SUM)
+        e = tc[1:].clone()
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        covered, elapsed = int(tc[0].item()), float(e.item())
+    if rank == 0:
+        line = {"metric": "Msamples/sec (pixels x spp) at 1024x1024/512spp", "value": None, "unit": "Msamples/s",
+                "n_gpus": n, "steps": args.steps, "warmup": args.warmup, "dry_run": True, "mode": mode,
+                "config": {"workload": cfg.name, "parallelism": "tiles%d" % n},
+                "tiles": int(len(tiles)), "tiles_covered": covered,
+                "max_share_tiles": int(max(len(sharding.shard_tiles(tiles, r, n)) for r in range(n)))}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- main
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if env_world is not None and world > 1:
+        mode = "ranks"
+        if args.gpus is not None and args.gpus != world:
+            sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (one rank per GPU)" % (args.gpus, world))
+        n_gpus = world
+    else:
+        world, rank = 1, 0
+        n_gpus = args.gpus or 1
+        mode = "threads" if n_gpus > 1 else "single"
+    if args.dry_run:
+        return dry_run(args, world, rank, mode)
+
+    import numpy as np
+    import torch
+    from izpi_amd import build
+    build.build_gpu(verbose=False)
+    from izpi_amd import _native as N
+    from izpi_amd.renderer import GPURenderer, MultiGPURenderer
+
+    dist = dist_setup(world, rank) if mode == "ranks" else None
+    cfg, scene, scene_s = load_config(args)
+    spp = args.spp or cfg.spp
     post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
-    keys = ("node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests", "rays", "kernel_ms",
-            "shade_ms", "total_ms", "launches", "samples", "node_steps", "prim_steps", "leaf_shortcuts", "tail_ms",
-            "tail_node_visits", "tail_tri_tests", "tail_sph_tests")
+    if mode != "threads":
+        torch.cuda.set_device(local)
 
-    def timed(bvh):
-        """W untimed + K timed frames on tree `bvh`; returns (elapsed, stats sums, canvas, renderer info)."""
+    def sync_all():
+        if mode == "threads":
+            for d in range(n_gpus):
+                torch.cuda.synchronize(d)
+        else:
+            torch.cuda.synchronize()
+
+    def timed(bvh, steps, warmup):
+        """warmup untimed + `steps` timed frames; returns (elapsed, per-step stats sums of
+        this process's device(s), canvas, info)."""
         ts = time.time()
-        r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=local,
-                        bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
+        if mode == "threads":
+            r = MultiGPURenderer(scene, cfg.width, cfg.height, spp, list(range(n_gpus)), max_depth=cfg.max_depth,
+                                 sampler=cfg.sampler, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
+
+            def step():
+                r.render(post=post, to_host=False)
+                return r.stats
+        else:
+            r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler,
+                            device=local, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
+            if mode == "ranks":
+                cid = bytearray(N.COMM_ID_BYTES)
+                if rank == 0:
+                    import ctypes as C
+                    buf = (C.c_uint8 * N.COMM_ID_BYTES)()
+                    if N.lib().izpi_gpu_comm_id(buf) != 0:
+                        raise RuntimeError("izpi_gpu_comm_id failed")
+                    cid = bytearray(bytes(buf))
+                obj = [bytes(cid)]
+                dist.broadcast_object_list(obj, src=0)
+                r.comm_init(world, rank, obj[0])
+            canvas_holder = {}
+
+            def step():  # Render(): spectral configs include FireflyRejection + XYZToRGB (renderer.go:215-219)
+                canvas, st = r.render_distributed(rank, world, post=post)
+                canvas_holder["c"] = canvas
+                return [st]
         setup = time.time() - ts
-
-        def step():  # Render(): spectral configs include FireflyRejection + XYZToRGB (renderer.go:215-219)
-            return r.render_distributed(rank, world, post=post)
-
-        for _ in range(args.warmup):
+        first_ms = None
+        for i in range(warmup):
+            t = time.perf_counter()
             step()
-        if world > 1:
+            sync_all()
+            if i == 0:
+                first_ms = (time.perf_counter() - t) * 1e3
+        if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync_all()
         t1 = time.perf_counter()
-        agg = {k: 0.0 for k in keys}
-        canvas = None
-        for _ in range(args.steps):
-            canvas, st = step()
-            for k in agg:
-                agg[k] += float(st[k]) if st else 0.0
-        torch.cuda.synchronize()
-        if world > 1:
+        agg = {k: 0.0 for k in STAT_KEYS}
+        for _ in range(steps):
+            for st in step():
+                add_stats(agg, st)
+        sync_all()
+        if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t1
-        if world > 1:
-            e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        if dist is not None:
+            e = torch.tensor([elapsed], dtype=torch.float64)
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             elapsed = float(e.item())
+        last = r.stats[0] if mode == "threads" else r.stats
         info = {"triangles": int(r.host.desc.num_tris), "nodes": int(r.host.desc.num_nodes),
-                "build_ms": r.bvh_build_ms if bvh == "gpu" else r.host.build_ms, "setup_s": setup}
-        img = canvas.cpu().numpy() if canvas is not None else None
+                "build_ms": r.bvh_build_ms if bvh == "gpu" else r.host.build_ms, "setup_s": setup,
+                "first_frame_ms": first_ms, "workspace_gb": (last or {}).get("workspace_bytes", 0) / 1e9,
+                "scene_gb": (last or {}).get("scene_bytes", 0) / 1e9, "slots": (last or {}).get("slots"),
+                "rec_dense": (last or {}).get("rec_dense"), "pool_blocks": (last or {}).get("pool_blocks"),
+                "chunk_spp": (last or {}).get("chunk_spp")}
+        img = None
+        if mode == "threads":  # one more frame, to the host, for the image summary
+            img = r.render(post=post)
+        elif rank == 0:
+            img = canvas_holder["c"].cpu().numpy() if canvas_holder.get("c") is not None else None
         r.close()
         return elapsed, agg, img, info
 
-    elapsed, agg, img, info = timed(args.bvh)
-    setup_s = info["setup_s"]  # host scene (+ reference BVH) build and upload of the timed renderer
+    if args.pmc_child:  # one frame under rocprofv3 --pmc (the parent reads the counters)
+        elapsed, agg, img, info = timed(args.bvh, 1, 0)
+        print(json.dumps({"pmc_child": True, "ms": elapsed * 1e3}), flush=True)
+        return
+
+    elapsed, agg, img, info = timed(args.bvh, args.steps, args.warmup)
     samples_per_step = cfg.width * cfg.height * spp
     value = samples_per_step * args.steps / elapsed / 1e6
     ref_check = None
-    if world == 1 and args.bvh == "gpu" and not args.no_reference_check:
+    if mode == "single" and args.bvh == "gpu" and not args.no_reference_check:
         # The same frame on hitable.NewBVH4's own tree (rebuilt bit for bit on the host):
         # the GPU-built tree only counts if its image is the reference tree's image.
-        import numpy as np
-        r_elapsed, r_agg, r_img, r_info = timed("reference")
+        rsteps = min(args.steps, 3)
+        r_elapsed, r_agg, r_img, r_info = timed("reference", rsteps, 1)
         equal = img.tobytes() == r_img.tobytes()
         rmse = float(np.sqrt(np.mean((img - r_img) ** 2)))
-        ref_value = samples_per_step * args.steps / r_elapsed / 1e6
-        ref_check = {"value": round(ref_value, 3), "ms_per_step": round(r_elapsed / args.steps * 1e3, 3),
-                     "image_bitwise_equal": equal, "image_rmse": rmse,
+        ref_value = samples_per_step * rsteps / r_elapsed / 1e6
+        ref_check = {"value": round(ref_value, 3), "ms_per_step": round(r_elapsed / rsteps * 1e3, 3),
+                     "steps": rsteps, "image_bitwise_equal": equal, "image_rmse": rmse,
                      "node_visits_per_ray": r_agg["node_visits"] / max(r_agg["rays"], 1),
-                     "trace_ms_per_step": r_agg["kernel_ms"] / args.steps,
-                     "shade_ms_per_step": r_agg["shade_ms"] / args.steps, "bvh_build_ms": r_info["build_ms"]}
+                     "trace_ms_per_step": r_agg["kernel_ms"] / rsteps,
+                     "shade_ms_per_step": r_agg["shade_ms"] / rsteps, "bvh_build_ms": r_info["build_ms"]}
         if not rmse < 1e-6:  # north-star tolerance: fall back to the reference tree's numbers
             print("WARNING: GPU-built BVH image differs from the reference tree's (rmse %g); reporting the "
                   "reference tree" % rmse, file=sys.stderr)
-            elapsed, agg, img, info, value = r_elapsed, r_agg, r_img, r_info, ref_value
+            elapsed, agg, img, info = r_elapsed * args.steps / rsteps, r_agg, r_img, r_info
+            for k in agg:
+                agg[k] *= args.steps / rsteps
+            value = ref_value
             args.bvh = "reference"
 
-    # roofline of the dominant kernel on this rank: algorithmic bytes / k_trace2 time
-    # (the traversals k_tail runs at the end of the frame are counted apart)
+    # dominant kernel: k_trace2 (the traversals k_tail runs at the end of the frame are counted apart)
+    steps = args.steps
+    trace_ms_frame = agg["kernel_ms"] / steps / (n_gpus if mode == "threads" else 1)
     trace_bytes = (128.0 * (agg["node_visits"] - agg["tail_node_visits"]) + 72.0 * (agg["tri_tests"] - agg["tail_tri_tests"])
                    + 32.0 * (agg["sph_tests"] - agg["tail_sph_tests"]))
-    achieved = trace_bytes / (agg["kernel_ms"] * 1e-3) / 1e9 if agg["kernel_ms"] > 0 else 0.0
-    launches = max(agg["launches"], 1.0)
-    traffic = pmc_traffic("%s/%s" % (args.config, args.bvh))
+    alg_frame = trace_bytes / steps / (n_gpus if mode == "threads" else 1)
+    achieved_alg = alg_frame / (trace_ms_frame * 1e-3) / 1e9 if trace_ms_frame > 0 else 0.0
+    launches = max(agg["launches"] / steps, 1.0)
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        dist.destroy_process_group()
         return
+    pmc = traffic_summary(pmc_children(args)) if (mode == "single" and not args.no_pmc) else {}
+    roof = {"bound": "hbm", "kernel": "k_trace2", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "achieved": None, "frac": None, "traffic": None,
+            "achieved_algorithmic": round(achieved_alg, 2),
+            "algorithmic_bytes_per_launch": alg_frame / launches,
+            "avg_launch_ms": trace_ms_frame / launches, "launches_per_frame": launches,
+            "binding_limit": "latency/issue (VALU ~53% busy, 57% of wave cycles waiting on memory, DESIGN.md §3.1), "
+                             "not HBM bandwidth"}
+    if "k_trace2" in pmc:
+        t = pmc["k_trace2"]
+        roof["traffic"] = t["bytes_per_frame"] / max(t["dispatches"], 1)  # HBM bytes per launch
+        roof["achieved"] = round(t["bytes_per_frame"] / (trace_ms_frame * 1e-3) / 1e9, 2)
+        roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
+        roof["traffic_per_frame"] = t["bytes_per_frame"]
+        roof["tcc_hit_rate"] = t["tcc_hit_rate"]
+        roof["pmc_dispatches"] = t["dispatches"]
+        if "k_shade" in pmc:
+            s = pmc["k_shade"]
+            roof["k_shade"] = {"bytes_per_frame": s["bytes_per_frame"], "tcc_hit_rate": s["tcc_hit_rate"],
+                               "achieved": round(s["bytes_per_frame"] / (agg["shade_ms"] / steps * 1e-3) / 1e9, 2)}
+    elif pmc.get("error"):
+        roof["pmc_error"] = pmc["error"]
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, scene, args.cpu_seconds, spp)
+    if mode == "single" and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, scene, args.cpu_seconds, spp, args.bvh)
+        cpu["gpu_speedup"] = value / cpu["value"]
+        if ref_check:
+            cpu["gpu_speedup_reference_tree"] = ref_check["value"] / cpu["value"]
+        if cpu.get("extrapolated_all_host_threads"):
+            cpu["gpu_speedup_vs_extrapolated"] = value / cpu["extrapolated_all_host_threads"]
     line = {
         "metric": "Msamples/sec (pixels x spp) at 1024x1024/512spp",
         "value": round(value, 3),
         "unit": "Msamples/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -229,20 +474,23 @@ def main():
         "data": "synthetic (deterministic Cornell box + 817k-triangle displaced cube-sphere dragon)",
         "config": {"workload": cfg.name, "width": cfg.width, "height": cfg.height, "spp": spp,
                    "max_depth": cfg.max_depth, "triangles": info["triangles"],
-                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "parallelism": "tiles%d" % world,
+                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "parallelism": "tiles%d" % n_gpus, "mode": mode,
                    "samples_per_step": samples_per_step},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": traffic,
-                     "kernel": "k_trace2", "algorithmic_bytes_per_launch": trace_bytes / launches,
-                     "avg_launch_ms": agg["kernel_ms"] / launches, "launches": int(agg["launches"])},
+        "roofline": roof,
         "cpu_baseline": cpu,
         "detail": {
-            "rank0_trace_ms_per_step": agg["kernel_ms"] / args.steps,
-            "rank0_shade_ms_per_step": agg["shade_ms"] / args.steps,
-            "rank0_tail_ms_per_step": agg["tail_ms"] / args.steps,
-            "rank0_render_ms_per_step": agg["total_ms"] / args.steps,
-            "rank0_rays_per_step": agg["rays"] / args.steps,
+            "first_frame_ms": info["first_frame_ms"],
+            "setup_s": round(info["setup_s"], 3),
+            "hbm_workspace_gb": round(info["workspace_gb"], 2),
+            "hbm_scene_gb": round(info["scene_gb"], 3),
+            "slots": info["slots"], "rec_dense": info["rec_dense"], "pool_blocks": info["pool_blocks"],
+            "chunk_spp": info["chunk_spp"],
+            "rank0_trace_ms_per_step": agg["kernel_ms"] / steps,
+            "rank0_shade_ms_per_step": agg["shade_ms"] / steps,
+            "rank0_tail_ms_per_step": agg["tail_ms"] / steps,
+            "rank0_render_ms_per_step": agg["total_ms"] / steps,
+            "rank0_rays_per_step": agg["rays"] / steps,
+            "rank0_parks_per_step": agg["parks"] / steps,
             "rank0_node_visits_per_ray": agg["node_visits"] / max(agg["rays"], 1),
             "rank0_tri_tests_per_ray": agg["tri_tests"] / max(agg["rays"], 1),
             # k_trace2 SIMD efficiency: useful lane-steps / (64 x wave-level steps)
@@ -252,14 +500,13 @@ def main():
                                          max(64 * agg["prim_steps"], 1),
             "rank0_leaf_shortcut_frac": agg["leaf_shortcuts"] / max(agg["node_visits"], 1),
             "scene_gen_s": round(scene_s, 2),
-            "setup_s": round(setup_s, 2),
             "bvh_build_ms": info["build_ms"],
             "reference_tree": ref_check,
             "image_mean_rgb": [float(x) for x in img[1:, :, :3].mean(axis=(0, 1))] if img is not None else None,
         },
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist is not None:
         dist.destroy_process_group()
 
 

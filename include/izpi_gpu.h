@@ -132,6 +132,13 @@ typedef struct izpi_render_stats {
   double tail_ms;
   /* the part of node_visits / tri_tests / sph_tests done inside k_tail */
   uint64_t tail_node_visits, tail_tri_tests, tail_sph_tests;
+  /* shading passes deferred one pass for want of an overflow record block (diagnostic) */
+  uint64_t parks;
+  /* device memory of the context after the call: render workspace and uploaded scene */
+  uint64_t workspace_bytes, scene_bytes;
+  /* wavefront configuration of the call: paths in flight, unwinding records per path kept
+   * in the dense array, overflow record blocks, samples per pixel per chunk */
+  uint32_t slots, rec_dense, pool_blocks, chunk_spp;
 } izpi_render_stats;
 
 /* Hit record returned by izpi_gpu_trace: BVH4.Hit (bvh4.go:49-164) followed by
@@ -188,6 +195,40 @@ enum { IZPI_BVH_LBVH = 0, /* Karras radix tree over the Morton order */
        IZPI_BVH_PLOC = 1  /* locally-ordered clustering (Meister & Bittner 2018) over the Morton order */ };
 int izpi_gpu_build_bvh4(izpi_ctx* ctx, const double* boxes, uint32_t n, uint32_t leaf_max, uint32_t method,
                         izpi_bvh4_node* nodes, uint32_t max_nodes, uint32_t* num_nodes, uint32_t* order, double* build_ms);
+
+/* ---- Multi-GPU (SURVEY.md §8(b),(e)) ---------------------------------------------
+ * Render fans out over the GPUs of the node in ONE call, as RendererImpl.Render fans
+ * out over its workers (render/renderer.go:123-147): one host thread and stream per
+ * device instead of one goroutine per core. The frame's tiles (common.Tiles in
+ * grid.WalkGrid's spiral order, or req->tiles) are dealt tile % G == i; device i renders
+ * its share packed; the shares are gathered to device 0 (peer copies over xGMI), which
+ * scatters them into the W*H*4 canvas (row H - y, rgb.go:41) and applies req->post.
+ * Per pixel-sample RNG streams make the canvas bit-identical for every G. A device may
+ * appear twice in `devices` (two contexts on one GPU). */
+typedef struct izpi_multi izpi_multi;
+int izpi_gpu_multi_open(const int* devices, uint32_t num_devices, izpi_multi** out);
+int izpi_gpu_multi_close(izpi_multi* m);
+const char* izpi_gpu_multi_last_error(izpi_multi* m);
+uint32_t izpi_gpu_multi_size(izpi_multi* m);
+/* context of device i (e.g. for izpi_gpu_build_bvh4), owned by `m` */
+izpi_ctx* izpi_gpu_multi_context(izpi_multi* m, uint32_t i);
+/* the scene is replicated on every device */
+int izpi_gpu_multi_upload_scene(izpi_multi* m, const izpi_scene_desc* scene);
+/* out_host: the caller's W*H*4 canvas (read first: pixels of no tile keep their values),
+ * or NULL to leave the canvas in device 0's memory (timing). stats: [num_devices] or NULL. */
+int izpi_gpu_multi_render(izpi_multi* m, const izpi_render_req* req, double* out_host, izpi_render_stats* stats);
+
+/* One process per GPU (torchrun / MPI style launchers): the library's own RCCL
+ * communicator. Rank 0 makes the id with izpi_gpu_comm_id and the launcher broadcasts
+ * it; every rank calls izpi_gpu_comm_init on its context. */
+#define IZPI_COMM_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
+int izpi_gpu_comm_id(uint8_t* id /* [IZPI_COMM_ID_BYTES] */);
+int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint8_t* id /* [IZPI_COMM_ID_BYTES] */);
+/* Collective: every rank passes the same whole-frame request. Rank r renders the tiles
+ * t % nranks == r, ncclGather moves the packed shares to rank 0, which writes the canvas
+ * into out_dev (device memory on its GPU; ignored on other ranks) and applies req->post.
+ * stats: this rank's share. */
+int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);

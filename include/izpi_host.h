@@ -83,6 +83,12 @@ const char* izpi_host_last_error(void);
  * (grid/grid.go:27-130): writes up to max_tiles entries of x0,y0,x1,y1; returns count. */
 uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint32_t max_tiles);
 
+/* Multi-GPU share of a tile list (the rule izpi_gpu_multi_render / izpi_gpu_render_rank
+ * use): copies tiles t with t % num_shares == share, in order, into `out`; returns how
+ * many. The largest share has ceil(num_tiles / num_shares) tiles. */
+uint32_t izpi_host_share_tiles(const uint32_t* tiles, uint32_t num_tiles, uint32_t share, uint32_t num_shares,
+                               uint32_t* out);
+
 /* The Go-math routines of izpi_amd/csrc/gomath.h evaluated on the host (same op
  * codes as izpi_gpu_gomath); used by the parity tests. */
 double izpi_host_gomath(int op, double x, double y);

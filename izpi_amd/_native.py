@@ -15,6 +15,7 @@ c_uint32_p = C.POINTER(C.c_uint32)
 c_float_p = C.POINTER(C.c_float)
 
 # ---- include/izpi_types.h
+COMM_ID_BYTES = 128
 IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE = range(6)
 IZPI_ABI_VERSION = 1
 PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
@@ -93,7 +94,9 @@ class RenderStats(C.Structure):
                 ("total_ms", C.c_double), ("launches", C.c_uint32), ("pad", C.c_uint32),
                 ("node_steps", C.c_uint64), ("prim_steps", C.c_uint64), ("leaf_shortcuts", C.c_uint64),
                 ("tail_ms", C.c_double), ("tail_node_visits", C.c_uint64), ("tail_tri_tests", C.c_uint64),
-                ("tail_sph_tests", C.c_uint64)]
+                ("tail_sph_tests", C.c_uint64), ("parks", C.c_uint64), ("workspace_bytes", C.c_uint64),
+                ("scene_bytes", C.c_uint64), ("slots", C.c_uint32), ("rec_dense", C.c_uint32),
+                ("pool_blocks", C.c_uint32), ("chunk_spp", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
@@ -170,9 +173,11 @@ EXPORTS = [
     "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
     "izpi_gpu_render_device", "izpi_gpu_unpack_tiles", "izpi_gpu_output_bytes", "izpi_gpu_trace",
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
-    "izpi_gpu_build_bvh4", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
+    "izpi_gpu_build_bvh4", "izpi_gpu_multi_open", "izpi_gpu_multi_close", "izpi_gpu_multi_last_error",
+    "izpi_gpu_multi_size", "izpi_gpu_multi_context", "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render",
+    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
-    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
+    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_info", "izpi_scene_image_file",
     "izpi_scene_set_image", "izpi_scene_add_triangles", "izpi_scene_background", "izpi_scene_to_input",
     "izpi_scene_material_name", "izpi_scene_free", "izpi_light_source", "izpi_light_source_name",
@@ -214,6 +219,19 @@ def lib():
                                        C.c_uint32]
     L.izpi_gpu_build_bvh4.argtypes = [C.c_void_p, c_double_p, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(BVH4Node),
                                       C.c_uint32, c_uint32_p, c_uint32_p, c_double_p]
+    L.izpi_gpu_multi_open.argtypes = [C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_void_p)]
+    L.izpi_gpu_multi_close.argtypes = [C.c_void_p]
+    L.izpi_gpu_multi_last_error.argtypes = [C.c_void_p]
+    L.izpi_gpu_multi_last_error.restype = C.c_char_p
+    L.izpi_gpu_multi_size.argtypes = [C.c_void_p]
+    L.izpi_gpu_multi_size.restype = C.c_uint32
+    L.izpi_gpu_multi_context.argtypes = [C.c_void_p, C.c_uint32]
+    L.izpi_gpu_multi_context.restype = C.c_void_p
+    L.izpi_gpu_multi_upload_scene.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
+    L.izpi_gpu_multi_render.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
+    L.izpi_gpu_comm_id.argtypes = [C.POINTER(C.c_uint8)]
+    L.izpi_gpu_comm_init.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
+    L.izpi_gpu_render_rank.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
     L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]
     L.izpi_host_scene_prim_boxes.argtypes = [C.c_void_p, c_double_p]
     L.izpi_host_scene_set_bvh.argtypes = [C.c_void_p, C.POINTER(BVH4Node), C.c_uint32, c_uint32_p]
@@ -228,6 +246,8 @@ def lib():
     L.izpi_host_last_error.restype = C.c_char_p
     L.izpi_host_tiles.argtypes = [C.c_uint32, C.c_uint32, c_uint32_p, C.c_uint32]
     L.izpi_host_tiles.restype = C.c_uint32
+    L.izpi_host_share_tiles.argtypes = [c_uint32_p, C.c_uint32, C.c_uint32, C.c_uint32, c_uint32_p]
+    L.izpi_host_share_tiles.restype = C.c_uint32
     L.izpi_host_gomath.argtypes = [C.c_int, C.c_double, C.c_double]
     L.izpi_host_gomath.restype = C.c_double
     L.izpi_abi_struct_size.argtypes = [C.c_int]

@@ -560,6 +560,15 @@ uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint3
   return n < max_tiles ? n : max_tiles;
 }
 
+uint32_t izpi_host_share_tiles(const uint32_t* tiles, uint32_t num_tiles, uint32_t share, uint32_t num_shares,
+                               uint32_t* out) {
+  if (!tiles || !out || num_shares == 0) return 0;
+  uint32_t n = 0;
+  for (uint32_t t = share; t < num_tiles; t += num_shares, n++)
+    for (int k = 0; k < 4; k++) out[4 * n + k] = tiles[4 * (size_t)t + k];
+  return n;
+}
+
 /* sizeof() of every boundary struct, in the order of IZPI_ABI_STRUCTS (tests compare
  * them with the Python/ctypes and Go-side layouts). */
 uint32_t izpi_abi_struct_size(int which) {

@@ -26,6 +26,10 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
+#include <thread>
+
 #include "../../include/izpi_host.h"
 #include "izpi_dev.h"
 #include "cie_tables.h"
@@ -66,7 +70,7 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
        CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
-       CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
+       CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_PARK, CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 
 // ======================================================= textures / spectra
@@ -200,30 +204,38 @@ struct RayRec {               // register form
 };
 struct alignas(64) RayHot { double o[3], d[3]; double tmin, tmax; };
 struct alignas(16) RayAux { double time; uint32_t kind, pad; };
-// Closest hit of a slot's ray and its path state. In HBM each is split into a hot record
-// every pass reads and a cold one read only when needed (UV-textured / sphere hits;
-// spectral wavelength, dielectric point), so k_shade moves fewer 64-B sectors.
+// Closest hit of a slot's ray: ONE aligned 32-B record (t, primitive, barycentrics), so
+// k_trace2's per-ray result is a single 32-B store into one line (two 16-B records in
+// two arrays cost two partially written lines per ray). k_shade reads the first 16 B
+// on every pass and (u, v) only for UV-textured and sphere hits.
 struct HitOut {               // register form
   double t, u, v;             // triangle barycentrics, or u = sphere root
   int32_t prim;               // leaf-order primitive, -1 = miss
   uint32_t pad;
 };
-struct alignas(16) HitHot { double t; int32_t prim; uint32_t pad; };
-struct alignas(16) HitUV { double u, v; };
+struct alignas(32) HitSt { double t; int32_t prim; uint32_t pad; double u, v; };
+// Path state, split into a hot record every pass reads and a cold one read only when
+// needed (spectral wavelength, dielectric point).
 struct PathSt {               // register form
   double lambda, lpdf;        // wavelength and its pdf (spectral)
   double pend[3];             // dielectric hit point while its path-length ray is traced
-  uint32_t rng, depth, unit, pad;
+  uint32_t rng, depth, unit, blk;
 };
-struct alignas(16) PathHot { uint32_t rng, depth, unit, pad; };
+// blk: 1 + the overflow record block holding this path's unwinding records at depths
+// >= ShadeParams::rec_dense (0 = none yet); see pool_alloc.
+struct alignas(16) PathHot { uint32_t rng, depth, unit, blk; };
 struct alignas(16) PathCold { double lambda, lpdf; double pend[3]; double pad; };
 enum { RAY_MAIN = 0, RAY_PATHLEN = 1 };
 
+// Queue entries are slot indices. PARK_BIT marks a slot whose shading pass waits for an
+// overflow record block (pool_alloc): k_trace2 leaves it untraced and untouched, and the
+// next k_shade pass shades the same traced ray again (the pass reads only stored state,
+// so the retry computes exactly what the first attempt would have).
+constexpr uint32_t PARK_BIT = 0x80000000u;
 struct WaveParams {
   RayHot* rhot;
   RayAux* raux;
-  HitHot* hhot;
-  HitUV* huv;
+  HitSt* hit;
   PathHot* phot;
   PathCold* pcold;
   const uint32_t* q_in;       // slots to process this pass
@@ -231,141 +243,29 @@ struct WaveParams {
   uint32_t* q_out;            // slots whose next ray must be traced
   uint32_t* q_out_count;
   uint32_t* trace_next;       // dynamic-fetch cursor of k_trace
-  uint32_t* free_q;           // slots whose sample finished this pass (k_shade -> k_refill)
-  uint32_t* free_count;
+  unsigned long long* pool_ctr;  // overflow-record ring counters (k_trace2 publishes frees), or null
   uint32_t slots;
 };
 
-// ============================================================ traversal
-// BVH4.Hit (bvh4.go:49-164) as a persistent dynamic-fetch kernel: each lane owns one
-// ray; every loop iteration visits one node per lane; finished lanes are refilled from
-// the queue in wave-sized batches (__ballot + popcount prefix) so SIMD lanes stay busy
-// while traversal lengths differ. Visit order, leaf re-test (A10), equal-t acceptance
-// (A11) and the float32 box test (A15) follow the reference exactly.
-template <int STACK>
-__global__ void __launch_bounds__(256) k_trace(const DevScene sc, const WaveParams wp, unsigned long long* counters,
-                                               uint32_t* err) {
-  __shared__ int32_t lds_stack[STACK * 256];
-  int32_t* stk = lds_stack + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t n = *wp.q_in_count;
-  uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
-  bool busy = false, exhausted = false;
-  uint32_t slot = 0;
-  V3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-  double tmin = 0, tmax = 0, time = 0;
-  float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
-  int32_t cur = -1;
-  int sp = 0;
-  double bt = 0, bu = 0, bv = 0;
-  int32_t bprim = -1;
-  for (;;) {
-    const uint64_t idle = __ballot(!busy);
-    if (idle != 0) {
-      const uint32_t nidle = (uint32_t)__popcll(idle);
-      if (!exhausted && (nidle >= 16 || idle == ~0ull)) {
-        const uint32_t leader = (uint32_t)__ffsll((long long)idle) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(wp.trace_next, nidle);
-        base = __shfl(base, (int)leader);
-        if (base + nidle >= n) exhausted = true;
-        if (!busy) {
-          const uint32_t my = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
-          if (my < n) {
-            slot = wp.q_in[my];
-            const RayHot& r = wp.rhot[slot];
-            const RayAux& ra = wp.raux[slot];
-            o = mk(r.o[0], r.o[1], r.o[2]);
-            d = mk(r.d[0], r.d[1], r.d[2]);
-            tmin = r.tmin; tmax = r.tmax; time = ra.time;
-            if (ra.kind == RAY_MAIN) c_rays++;
-            ix = (float)(1.0 / d.x); iy = (float)(1.0 / d.y); iz = (float)(1.0 / d.z);
-            ox = (float)o.x; oy = (float)o.y; oz = (float)o.z;
-            cur = sc.root;
-            sp = 0;
-            bprim = -1;
-            busy = cur != -1;
-            if (!busy) { wp.hhot[slot].prim = -1; }
-          }
-        }
-      } else if (exhausted && idle == ~0ull) {
-        break;
-      }
-    }
-    if (!busy) continue;
-    // ---- one node visit
-    c_nodes++;
-    const float tm = (float)tmax;
-    int32_t next = -1;
-    if (ref_is_leaf(cur)) {
-      const float4* lp = reinterpret_cast<const float4*>(sc.leaves + leaf_start(cur));
-      const float4 a = lp[0], b = lp[1];
-      if (slab(a.x, a.y, a.z, a.w, b.x, b.y, ox, oy, oz, ix, iy, iz, tm)) {
-        const int32_t start = __float_as_int(b.z), count = __float_as_int(b.w);
-        for (int32_t k = start; k < start + count; k++) {
-          const double2* pp = reinterpret_cast<const double2*>(sc.prims + k);
-          const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
-          const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
-          const uint32_t kind = (uint32_t)__double2loint(p4.y);
-          if (kind == IZPI_PRIM_TRIANGLE) {
-            c_tri++;
-            double t, u, v;
-            if (tri_intersect(pa, o, d, tmin, tmax, t, u, v)) { tmax = t; bt = t; bu = u; bv = v; bprim = k; }
-          } else {
-            c_sph++;
-            double t; int root;
-            if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) { tmax = t; bt = t; bu = (double)root; bv = 0; bprim = k; }
-          }
-        }
-      }
-    } else {
-      const float4* np = reinterpret_cast<const float4*>(sc.inner + cur);
-      const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
-      const int4 ch = *reinterpret_cast<const int4*>(np + 6);
-      const float amnx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, amny[4] = {mny.x, mny.y, mny.z, mny.w},
-                  amnz[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, amxx[4] = {mxx.x, mxx.y, mxx.z, mxx.w},
-                  amxy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, amxz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
-      const int32_t ach[4] = {ch.x, ch.y, ch.z, ch.w};
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        if (ach[i] == -1) continue;
-        if (!slab(amnx[i], amny[i], amnz[i], amxx[i], amxy[i], amxz[i], ox, oy, oz, ix, iy, iz, tm)) continue;
-        if (next == -1) {
-          next = ach[i];
-        } else if (sp < STACK) {
-          stk[sp * 256] = ach[i];
-          sp++;
-        } else {
-          atomicOr(err, 1u);  // unreachable: STACK >= host-computed bound
-        }
-      }
-    }
-    if (next != -1) {
-      cur = next;
-    } else if (sp > 0) {
-      sp--;
-      cur = stk[sp * 256];
-    } else {
-      HitHot h;
-      h.t = bt; h.prim = bprim; h.pad = 0;
-      wp.hhot[slot] = h;
-      wp.huv[slot] = HitUV{bu, bv};
-      busy = false;
-    }
-  }
-  unsigned long long vals[4] = {c_rays, c_nodes, c_tri, c_sph};
-  const int idx[4] = {CNT_RAYS, CNT_NODES, CNT_TRI, CNT_SPH};
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    unsigned long long s = vals[i];
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
-    if (lane == 0 && s) atomicAdd(counters + idx[i], s);
+// Overflow record blocks (see pool_alloc) come in POOL_SHARDS independent rings, each
+// with its own counters on its own 128-B line: [0] allocation head, [1] free tail,
+// [2] published free tail (one counter word serialises its atomics, ~88/us chip-wide).
+constexpr uint32_t POOL_SHARDS = 256, POOL_CTR_STRIDE = 16;
+// Make the frees of the last shading pass available to allocations (thread t of the
+// calling block handles rings t, t + blockDim, ...); failed allocations overshot the
+// head, so clamp it first.
+IZPI_DEV void pool_publish(unsigned long long* ctr) {
+  for (uint32_t r = threadIdx.x; r < POOL_SHARDS; r += blockDim.x) {
+    unsigned long long* c = ctr + (size_t)r * POOL_CTR_STRIDE;
+    const unsigned long long head = c[0], pub = c[2];
+    c[0] = head < pub ? head : pub;
+    c[2] = c[1];
   }
 }
 
-// BVH4.Hit (bvh4.go:49-164) of one slot's ray by one lane, from the root to the end,
-// in the reference's visit order (leaf re-test A10, equal-t acceptance A11, f32 box test
-// A15): the per-lane form k_tail uses. Writes the slot's hit record like k_trace2.
+// ============================================================ traversal
+// BVH4.Hit (bvh4.go:49-164) for one ray in one lane, LDS stack: k_tail's traversal
+// (the wavefront passes use k_trace2 below). Same visit order and counters.
 template <int STACK>
 IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot, int32_t* stk, uint32_t& c_rays,
                         uint32_t& c_nodes, uint32_t& c_tri, uint32_t& c_sph, uint32_t* err) {
@@ -436,8 +336,7 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot,
       cur = -1;
     }
   }
-  wp.hhot[slot] = HitHot{bprim >= 0 ? tmax : 0.0, bprim, 0u};
-  wp.huv[slot] = HitUV{bu, bv};
+  wp.hit[slot] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, bu, bv};
 }
 
 // BVH4.Hit, step-scheduled variant. Each lane is in one of two modes: NODE (visit
@@ -469,7 +368,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // (+4: an owner reads its four entries unconditionally, past the wave's last batch entry)
   __shared__ uint32_t dist_owner[DIST ? 260 : 1];
   __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST ? 260 : 1], dist_v[DIST ? 260 : 1];
-  // (u, v) of the lane's accepted hit so far: HitUV is stored once, when the ray finishes
+  // (u, v) of the lane's accepted hit so far: the hit record is stored once, when the ray finishes
   // (a global store per accepted hit would hold up the wave's next load wait, since
   // vmcnt counts stores and loads in one queue)
   __shared__ double2 lds_uv[256];
@@ -478,6 +377,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = *wp.q_in_count;
+  if (wp.pool_ctr && blockIdx.x == 0) pool_publish(wp.pool_ctr);
   // Small queues (the wavefront's tail passes): chunks shrink so the rays spread over
   // more waves, and waves past the last chunk exit at once instead of each paying a
   // dequeue atomic on the one counter word (~88/us chip-wide).
@@ -542,7 +442,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           pslot = k < 64 ? s0 : s1;
         }
         if (!busy) {
-          if (rank < take) {
+          // a parked slot (PARK_BIT) is not traced: its hit record stays for the retry
+          if (rank < take && !((PREQ ? pslot : wp.q_in[my]) & PARK_BIT)) {
             slot = PREQ ? pslot : wp.q_in[my];
             const RayHot& r = wp.rhot[slot];
             tmax = r.tmax;
@@ -556,7 +457,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             in_prim = false;
             bprim = -1;
             busy = cur != -1;
-            if (!busy) { wp.hhot[slot] = HitHot{0.0, -1, 0u}; wp.huv[slot] = HitUV{0.0, 0.0}; }
+            if (!busy) wp.hit[slot] = HitSt{0.0, -1, 0u, 0.0, 0.0};
           }
         }
         c_rays += (uint64_t)__popcll(__ballot(main_ray));
@@ -821,9 +722,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       pend = lf ? leaf_start(top) + leaf_count(top) : pend;
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
-        wp.hhot[slot] = HitHot{bprim >= 0 ? tmax : 0.0, bprim, 0u};
         const double2 uv = bprim >= 0 ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        wp.huv[slot] = HitUV{uv.x, uv.y};
+        wp.hit[slot] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
         busy = false;
       }
     }
@@ -859,8 +759,8 @@ struct HitRec {
   V3 p, n;
   uint32_t mat;
 };
-// `uvp` holds the hit's (u, v): read only for UV-textured triangles and for spheres.
-IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitUV* uvp, const GShade& gs, V3 o, V3 d, double time,
+// `uvp` is the hit record, whose (u, v): read only for UV-textured triangles and for spheres.
+IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, const GShade& gs, V3 o, V3 d, double time,
                          bool want_uv, HitRec& h) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
@@ -870,8 +770,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitUV* uvp, 
     V3 n = mk(gs.n[0], gs.n[1], gs.n[2]);
     if (want_uv) {  // (u,v) are read only by image textures and normal maps
       const double eps = 1e-8;
-      const HitUV huv = *uvp;
-      double u = huv.u, v = huv.v;
+      double u = uvp->u, v = uvp->v;
       double w = 1.0 - u - v;
       double sum = u + v + w;
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
@@ -1004,7 +903,9 @@ struct ShadeParams {
   uint32_t width, height, max_depth;
   uint32_t chunk_spp, s0, tile_w, tile_h, total_units;
   uint32_t num_bg_spd, slots;
-  uint32_t rec_depth;          // records per slot (max(1, max_depth))
+  uint32_t rec_dense;          // unwinding records per slot in the dense array (depths 0..rec_dense-1)
+  uint32_t rec_pool;           // records per overflow block (depths rec_dense..max_depth-1); 0 = no pool
+  uint32_t pool_shift;         // log2(overflow blocks per ring); ring r holds blocks [r << shift, (r + 1) << shift)
   uint32_t unit_base;          // k_start: slot i of this lane starts unit unit_base + i
   uint32_t bg_sorted;          // background SPD wavelengths non-decreasing (binary-search lookups)
   const uint32_t* tiles;
@@ -1013,7 +914,10 @@ struct ShadeParams {
   double background[3];
   uint64_t seed;
   double* out;                 // [total_units][3] per-sample result
-  double* recs;                // [max_depth][6][slots] unwinding records
+  double* recs;                // [slots][rec_dense][D] unwinding records
+  double* pool;                // [blocks][rec_pool][D] overflow unwinding records
+  uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
+  unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
   unsigned long long* counters;
   uint32_t* error;
@@ -1023,18 +927,25 @@ struct ShadeParams {
 // reads its records as one contiguous run (48 B per level for Colour: flag, att xyz, s, p;
 // 32 B for Spectral: flag, att, s, p). A [depth][field][slot] layout made every field
 // of every level a separate scattered 64-B sector read (measured: 44% of C5 shading).
+// Only the first rec_dense levels are stored per slot. Few paths go deeper (C3: ~3% of
+// the paths in flight at depth >= 8), so the deeper levels live in overflow blocks of
+// rec_pool levels, taken by a path when it reaches depth rec_dense and returned when it
+// finishes: the state of 40M slots at maxDepth 50 takes ~20 GB instead of ~100 GB.
 template <int SAMPLER>
 struct RecLayout {
   static constexpr uint32_t D = SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 4;  // doubles per record
   static constexpr uint32_t S = D - 2;                                   // index of s (p follows)
 };
 template <int SAMPLER>
-IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t slot, uint32_t depth) {
-  return sp.recs + ((size_t)slot * sp.rec_depth + depth) * RecLayout<SAMPLER>::D;
+IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t slot, uint32_t blk, uint32_t depth) {
+  constexpr uint32_t D = RecLayout<SAMPLER>::D;
+  if (depth < sp.rec_dense) return sp.recs + ((size_t)slot * sp.rec_dense + depth) * D;
+  return sp.pool + ((size_t)(blk - 1) * sp.rec_pool + (depth - sp.rec_dense)) * D;
 }
 template <int SAMPLER>
-IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t depth, bool spec, V3 att, double s, double p) {
-  double2* r = reinterpret_cast<double2*>(rec_ptr<SAMPLER>(sp, slot, depth));
+IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t blk, uint32_t depth, bool spec, V3 att, double s,
+                        double p) {
+  double2* r = reinterpret_cast<double2*>(rec_ptr<SAMPLER>(sp, slot, blk, depth));
   r[0] = make_double2(spec ? 1.0 : 0.0, att.x);
   if (SAMPLER == IZPI_SAMPLER_COLOUR) r[1] = make_double2(att.y, att.z);
   if (!spec) r[RecLayout<SAMPLER>::S / 2] = make_double2(s, p);
@@ -1066,7 +977,7 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
 #pragma unroll
     for (int j = 0; j < RB; j++) {
       if (dd - j >= 0) {
-        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER>(sp, slot, (uint32_t)(dd - j)));
+        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER>(sp, slot, P.blk, (uint32_t)(dd - j)));
 #pragma unroll
         for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
       }
@@ -1137,6 +1048,7 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slo
   cam.s = (uint32_t)splitmix64(sp.seed ^ key ^ IZPI_CAMERA_STREAM_SALT);
   P.unit = unit;
   P.depth = 0;
+  P.blk = 0;
   P.lambda = 0;
   P.lpdf = 1;
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) {
@@ -1282,9 +1194,6 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
   if (push) wp.q_out[pos] = slot;
 }
 
-#ifndef IZPI_SPLIT_REFILL
-#define IZPI_SPLIT_REFILL 0  // 1: refill in its own kernel (k_refill; k_shade -35 VGPRs, but measured 2x slower shading)
-#endif
 // Give `slot` (when `want`) new work units until one yields a ray to trace (block-uniform
 // loop, block-wide unit reservations). Sets `push` when the slot has a ray.
 template <int SAMPLER>
@@ -1310,23 +1219,6 @@ IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const Wave
   }
 }
 
-// Refill the slots k_shade freed in this pass (its free list), then queue them.
-template <int SAMPLER>
-__global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
-  uint32_t parity = 0;  // block_reserve LDS buffer set
-  const uint32_t n = *wp.free_count;  // written by the previous kernel: the same value for every thread
-  const uint32_t stride = gridDim.x * 256;
-  for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
-    const uint32_t i = base + threadIdx.x;
-    const bool valid = i < n;
-    const uint32_t slot = valid ? wp.free_q[i] : 0u;
-    bool push = false;
-    refill_block<SAMPLER>(sc, sp, wp, slot, valid, push, parity);
-    const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
-    if (push) wp.q_out[pos] = slot;
-  }
-}
-
 // Partial stores of the per-slot records: only the fields a pass changes are written,
 // so k_shade does not keep the untouched ones (ray time, wavelength, ...) in registers.
 // `aux`: also store kind/pad. Only MATSET_FULL turns a slot's ray into a path-length ray
@@ -1340,9 +1232,7 @@ IZPI_DEV void store_ray(const WaveParams& wp, uint32_t slot, V3 o, V3 d, double 
   p[3] = make_double2(tmin, tmax);
   if (aux) *reinterpret_cast<uint2*>(&wp.raux[slot].kind) = make_uint2(kind, pad);  // the ray time is left as is
 }
-IZPI_DEV void store_path_rng_depth(PathHot* ps, uint32_t rng, uint32_t depth) {
-  *reinterpret_cast<uint2*>(&ps->rng) = make_uint2(rng, depth);
-}
+IZPI_DEV void store_path_hot(PathHot* ps, uint32_t rng, const PathSt& P) { *ps = PathHot{rng, P.depth, P.unit, P.blk}; }
 
 // MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
 // DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
@@ -1353,14 +1243,16 @@ enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
 // One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
 // one bounce deep (colour.go:33-94, sampler/spectral.go:47-80). Sets `push` when the slot
 // has a ray to trace next and `done` when its sample finished.
+// `ph` is the slot's PathHot as read by the caller, with blk set to the path's overflow
+// block when it needs one (P.depth >= rec_dense). `fblk` returns the block to free when
+// the sample finished.
 template <int SAMPLER, int MATSET>
-IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, bool& push,
-                         bool& done, uint32_t& c_lt, uint32_t& c_ls) {
+IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, const PathHot& ph,
+                         bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt, uint32_t& c_ls) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   PathSt P;
   {
-    const PathHot ph = wp.phot[slot];
-    P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.pad = 0;
+    P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.blk = ph.blk;
     P.lambda = 0; P.lpdf = 1;
     if (!COLOUR) { const PathCold& pc = wp.pcold[slot]; P.lambda = pc.lambda; P.lpdf = pc.lpdf; }
   }
@@ -1375,8 +1267,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
   }
   HitOut H;
   {
-    const HitHot hh = wp.hhot[slot];
-    H.t = hh.t; H.prim = hh.prim; H.pad = 0; H.u = 0; H.v = 0;
+    const double2 hh = *reinterpret_cast<const double2*>(wp.hit + slot);  // t, prim (u, v read on demand)
+    H.t = hh.x; H.prim = (int32_t)__double2loint(hh.y); H.pad = 0; H.u = 0; H.v = 0;
   }
   Lcg rng;
   rng.s = P.rng;
@@ -1413,7 +1305,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
     const GShade gs = sc.shade[H.prim];
     HitRec h;
     const double rtime = IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_SPHERE ? wp.raux[slot].time : 0.0;
-    hit_record(sc, H, wp.huv + slot, gs, ro, rd, rtime, (gs.cflags & 2u) != 0, h);
+    hit_record(sc, H, wp.hit + slot, gs, ro, rd, rtime, (gs.cflags & 2u) != 0, h);
     hit_n = h.n;
     next_o = h.p;
     // the shade record carries the material kind and, for a constant RGB texture, its
@@ -1450,7 +1342,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
           // the extra World.Hit of calculatePathLength: trace it, finish next pass
           PathCold* pcw = wp.pcold + slot;
           pcw->pend[0] = h.p.x; pcw->pend[1] = h.p.y; pcw->pend[2] = h.p.z;
-          store_path_rng_depth(wp.phot + slot, rng.s, P.depth);
+          store_path_hot(wp.phot + slot, rng.s, P);
           store_ray(wp, slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
           push = true;
           break;
@@ -1523,6 +1415,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
     if (terminal) {
       finish<SAMPLER, MATSET == MATSET_BASIC>(sp, slot, P, L);
       done = true;
+      fblk = P.blk;
     } else {
       if (have_pdf) {
         // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:85-90, mixture.go:17-33)
@@ -1536,25 +1429,78 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
         const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
         double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
         if (sc_cos < 0) sc_cos = 0;
-        rec_store<SAMPLER>(sp, slot, P.depth, false, att, sc_cos / 3.141592653589793, 0);
+        rec_store<SAMPLER>(sp, slot, P.blk, P.depth, false, att, sc_cos / 3.141592653589793, 0);
         const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
-        rec_ptr<SAMPLER>(sp, slot, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
+        rec_ptr<SAMPLER>(sp, slot, P.blk, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
         next_d = dir;
       } else {
-        rec_store<SAMPLER>(sp, slot, P.depth, true, att, 0, 0);
+        rec_store<SAMPLER>(sp, slot, P.blk, P.depth, true, att, 0, 0);
       }
       P.depth++;
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
         finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
         done = true;
+        fblk = P.blk;
       } else {
-        store_path_rng_depth(wp.phot + slot, P.rng, P.depth);
+        store_path_hot(wp.phot + slot, P.rng, P);
         store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0, MATSET == MATSET_FULL);
         push = true;
       }
     }
   }
+}
+
+// ---- overflow record blocks
+// POOL_SHARDS rings of free block ids. A ring holds its own blocks only: block b belongs
+// to ring b >> pool_shift, and a freed block goes back to its ring, so no ring ever holds
+// more than its 1 << pool_shift entries. Each ring is a FIFO between an allocation head
+// and a free tail (64-bit counters, index = counter & (ring size - 1)). Allocations take
+// from the head but only below the PUBLISHED tail, which k_trace2 advances once per pass
+// (kernel boundaries order the frees' ring writes before the next pass's reads). A wave
+// allocates from its own ring; an allocation that finds no published block there parks
+// its slot for one pass (PARK_BIT). Paths that hold a block never wait, so parked slots
+// always get one back.
+IZPI_DEV unsigned long long* pool_ring_ctr(const ShadeParams& sp, uint32_t r) {
+  return sp.pool_ctr + (size_t)r * POOL_CTR_STRIDE;
+}
+// Wave-aggregated allocation for the lanes with `need`: returns 1 + block, or 0 (`need`
+// lanes with 0 are parked).
+IZPI_DEV uint32_t pool_alloc(const ShadeParams& sp, bool need) {
+  const uint64_t m = __ballot(need);
+  if (m == 0) return 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t ring = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (POOL_SHARDS - 1);
+  unsigned long long* c = pool_ring_ctr(sp, ring);
+  const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+  unsigned long long base = 0, pub = 0;
+  if (lane == leader) {
+    base = atomicAdd(c, (unsigned long long)__popcll(m));
+    pub = __atomic_load_n(c + 2, __ATOMIC_RELAXED);
+  }
+  base = __shfl(base, (int)leader);
+  pub = __shfl(pub, (int)leader);
+  const unsigned long long idx = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1));
+  const uint32_t size_mask = (1u << sp.pool_shift) - 1u;
+  return (need && idx < pub) ? sp.pool_ring[((size_t)ring << sp.pool_shift) + (idx & size_mask)] + 1u : 0u;
+}
+// Return a lane's block (1 + block, 0 = none) to its ring.
+IZPI_DEV void pool_free_one(const ShadeParams& sp, uint32_t fblk) {
+  const uint32_t b = fblk - 1u, ring = b >> sp.pool_shift, size_mask = (1u << sp.pool_shift) - 1u;
+  const unsigned long long pos = atomicAdd(pool_ring_ctr(sp, ring) + 1, 1ull);
+  sp.pool_ring[((size_t)ring << sp.pool_shift) + (pos & size_mask)] = b;
+}
+// Single-lane allocation that tries every ring (k_tail: cannot park), or 0.
+IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
+  const uint32_t size_mask = (1u << sp.pool_shift) - 1u;
+  for (uint32_t k = 0; k < POOL_SHARDS; k++) {
+    const uint32_t ring = (first + k) & (POOL_SHARDS - 1);
+    unsigned long long* c = pool_ring_ctr(sp, ring);
+    if (__atomic_load_n(c, __ATOMIC_RELAXED) >= __atomic_load_n(c + 2, __ATOMIC_RELAXED)) continue;  // exhausted
+    const unsigned long long idx = atomicAdd(c, 1ull);
+    if (idx < __atomic_load_n(c + 2, __ATOMIC_RELAXED)) return sp.pool_ring[((size_t)ring << sp.pool_shift) + (idx & size_mask)] + 1u;
+  }
+  return 0u;
 }
 
 // One shading pass over the slots traced in the previous k_trace.
@@ -1573,7 +1519,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve LDS buffer set
   const uint32_t n = *wp.q_in_count;
-  uint32_t c_lt = 0, c_ls = 0;
+  uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * 256;
 #ifdef IZPI_SHADE_CLOCKS
   uint64_t k_item = 0, k_ref = 0, k_push = 0;
@@ -1588,32 +1534,37 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     uint32_t slot = next_slot;
     next_slot = IZPI_SHADE_PREQ && i + stride < n ? wp.q_in[i + stride] : 0u;
     if (!IZPI_SHADE_PREQ) slot = valid ? wp.q_in[i] : 0;
+    slot &= ~PARK_BIT;      // a parked slot retries its pass (its traced ray is unchanged)
     bool push = false;      // slot has a ray to trace next
     bool done = false;      // slot's sample finished: grab a new unit
+    bool parked = false;
+    uint32_t fblk = 0;
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t0 = __builtin_readcyclecounter();
 #endif
-    if (valid) shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, push, done, c_lt, c_ls);
+    PathHot ph = valid ? wp.phot[slot] : PathHot{0u, 0u, 0u, 0u};
+    if (sp.rec_pool) {  // a path at depth >= rec_dense writes its records to an overflow block
+      const bool need = valid && ph.depth >= sp.rec_dense && ph.blk == 0;
+      const uint32_t b = pool_alloc(sp, need);
+      ph.blk = need ? b : ph.blk;
+      parked = need && b == 0;
+      c_park += parked ? 1u : 0u;
+    }
+    if (valid && !parked) shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, ph, push, done, fblk, c_lt, c_ls);
+    if (sp.rec_pool && fblk) pool_free_one(sp, fblk);
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t1 = __builtin_readcyclecounter();
     k_item += t1 - t0;
     t0 = t1;
 #endif
-#if IZPI_SPLIT_REFILL
-    {  // finished slots go to the free list; k_refill gives them new units
-      const uint32_t fpos = block_reserve(wp.free_count, done, parity);
-      if (done) wp.free_q[fpos] = slot;
-    }
-#else
     refill_block<SAMPLER>(sc, sp, wp, slot, done, push, parity);
-#endif
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
     k_ref += t1 - t0;
     t0 = t1;
 #endif
-    const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
-    if (push) wp.q_out[pos] = slot;
+    const uint32_t pos = block_reserve(wp.q_out_count, push || parked, parity);
+    if (push || parked) wp.q_out[pos] = parked ? (slot | PARK_BIT) : slot;
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
     k_push += t1 - t0;
@@ -1627,9 +1578,9 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     atomicAdd(sp.counters + CNT_SCLK_PUSH, (unsigned long long)k_push);
   }
 #endif
-  unsigned long long vals[2] = {c_lt, c_ls};
-  const int idx[2] = {CNT_LTRI, CNT_LSPH};
-  for (int k = 0; k < 2; k++) {
+  unsigned long long vals[3] = {c_lt, c_ls, c_park};
+  const int idx[3] = {CNT_LTRI, CNT_LSPH, CNT_PARK};
+  for (int k = 0; k < 3; k++) {
     unsigned long long s = vals[k];
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
     if (lane == 0 && s) atomicAdd(sp.counters + idx[k], s);
@@ -1648,11 +1599,23 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
   const uint32_t n = *wp.q_in_count;
   uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_lt = 0, c_ls = 0;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint32_t slot = wp.q_in[i];
+    const uint32_t entry = wp.q_in[i];
+    const uint32_t slot = entry & ~PARK_BIT;
+    bool traced = (entry & PARK_BIT) != 0;  // a parked slot's ray is already traced
     for (;;) {
-      trace_one<STACK>(sc, wp, slot, stk, c_rays, c_nodes, c_tri, c_sph, sp.error);
+      if (!traced) trace_one<STACK>(sc, wp, slot, stk, c_rays, c_nodes, c_tri, c_sph, sp.error);
+      traced = false;
+      PathHot ph = wp.phot[slot];
+      if (sp.rec_pool && ph.depth >= sp.rec_dense && ph.blk == 0) {
+        // The host launches k_tail with at most pool blocks paths, all of the free
+        // blocks published, so this cannot fail (guarded anyway: no spin on a bug).
+        ph.blk = pool_alloc_any(sp, blockIdx.x * 4u + (threadIdx.x >> 6));
+        if (ph.blk == 0) { atomicOr(sp.error, 4u); break; }
+      }
       bool push = false, done = false;
-      shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, push, done, c_lt, c_ls);
+      uint32_t fblk = 0;
+      shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, ph, push, done, fblk, c_lt, c_ls);
+      if (fblk) pool_free_one(sp, fblk);
       if (!push) break;
     }
   }
@@ -1664,6 +1627,19 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
     unsigned long long v = vals[k];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
     if (lane == 0 && v) atomicAdd(sp.counters + idx[k], v);
+  }
+}
+
+// Publish the frees of the last shading pass (k_trace2 does it at its start; k_tail and
+// the host's pool checks need it on their own).
+__global__ void k_pool_publish(unsigned long long* ctr) { pool_publish(ctr); }
+// Every ring holds all of its blocks at the start of a render.
+__global__ void k_pool_init(uint32_t* ring, uint32_t n, uint32_t per_ring, unsigned long long* ctr) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) ring[i] = i;
+  if (i < POOL_SHARDS) {
+    unsigned long long* c = ctr + (size_t)i * POOL_CTR_STRIDE;
+    c[0] = 0; c[1] = per_ring; c[2] = per_ring;
   }
 }
 
@@ -1832,7 +1808,7 @@ __global__ void k_trace_setup(const double* rays, uint32_t n, RayHot* rh, RayAux
   ra[i] = RayAux{R.time, R.kind, R.pad};
   q[i] = i;
 }
-__global__ void k_trace_records(const DevScene sc, const RayHot* rr, const HitHot* hhot, const HitUV* huv, uint32_t n,
+__global__ void k_trace_records(const DevScene sc, const RayHot* rr, const HitSt* hit, uint32_t n,
                                 izpi_hit* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
@@ -1840,12 +1816,12 @@ __global__ void k_trace_records(const DevScene sc, const RayHot* rr, const HitHo
   memset(&h, 0, sizeof(h));
   h.prim_ref = 0xFFFFFFFFu;
   HitOut c;
-  c.t = hhot[i].t; c.prim = hhot[i].prim; c.u = huv[i].u; c.v = huv[i].v; c.pad = 0;
+  c.t = hit[i].t; c.prim = hit[i].prim; c.u = hit[i].u; c.v = hit[i].v; c.pad = 0;
   if (c.prim >= 0) {
     const RayHot R = rr[i];
     HitRec hr;
     const GShade gs = sc.shade[c.prim];
-    hit_record(sc, c, huv + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
+    hit_record(sc, c, hit + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
     const GPrim& p = sc.prims[c.prim];
     h.hit = 1; h.t = hr.t; h.u = hr.u; h.v = hr.v;
     h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
@@ -1902,35 +1878,36 @@ struct izpi_ctx {
   uint32_t stack_needed = 0;
   uint32_t num_prims = 0;
   std::vector<void*> scene_allocs;
+  size_t scene_bytes = 0;
   // render workspace (grown on demand)
   double* d_samples = nullptr; size_t samples_cap = 0;
   double* d_recs = nullptr; size_t recs_cap = 0;
+  double* d_pool = nullptr; size_t pool_cap = 0;       // overflow unwinding records
+  uint32_t* d_ring = nullptr; size_t ring_cap = 0;     // free ring of overflow blocks
+  unsigned long long* d_pool_ctr = nullptr;            // ring counters, [POOL_SHARDS][POOL_CTR_STRIDE]
   double* d_running = nullptr; size_t running_cap = 0;
   double* d_out = nullptr; size_t out_cap = 0;
   uint32_t* d_tiles = nullptr; size_t tiles_cap = 0;
+  uint32_t* d_utiles = nullptr; size_t utiles_cap = 0;  // tile lists of k_unpack (multi-GPU root)
   double* d_bg = nullptr; size_t bg_cap = 0;
-  uint32_t* d_misc = nullptr;              // [0] head, [1] error, [2] trace cursor, [3..4] queue counts, [5] free count, [5] free count
+  uint32_t* d_misc = nullptr;              // [0] unit head, [1] error, [2] trace cursor, [3..4] queue counts
   unsigned long long* d_counters = nullptr;
   RayHot* d_rhot = nullptr; size_t rhot_cap = 0;
   RayAux* d_raux = nullptr; size_t raux_cap = 0;
-  HitHot* d_hhot = nullptr; size_t hhot_cap = 0;
-  HitUV* d_huv = nullptr; size_t huv_cap = 0;
+  HitSt* d_hit = nullptr; size_t hit_cap = 0;
   PathHot* d_phot = nullptr; size_t phot_cap = 0;
   PathCold* d_pcold = nullptr; size_t pcold_cap = 0;
   uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
+  double* d_share = nullptr; size_t share_cap = 0;    // multi-GPU: this device's packed tiles
+  double* d_gather = nullptr; size_t gather_cap = 0;  // multi-GPU root: every device's packed tiles
   uint32_t* h_count = nullptr;                        // pinned readback of d_misc (unit head, queue lengths)
   hipEvent_t ev3 = nullptr;
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
-  // second wavefront lane (run_chunks with two lanes): its own stream, counters, events
-  // and traversal spill area; the slots, queues and records are split between the lanes
-  hipStream_t stream2 = nullptr;
-  uint32_t* d_misc2 = nullptr;
-  uint32_t* h_count2 = nullptr;
-  hipEvent_t evb2[3 * IZPI_PASS_BATCH] = {};
-  hipEvent_t evj = nullptr;
-  int32_t* d_spill2 = nullptr; size_t spill2_cap = 0;
+  // RCCL communicator of a multi-process render (izpi_gpu_comm_init), or null
+  ncclComm_t comm = nullptr;
+  uint32_t comm_rank = 0, comm_size = 1;
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
@@ -1944,6 +1921,7 @@ int dev_upload(izpi_ctx* ctx, const T* host, size_t count, T** out) {
   if (count == 0) return IZPI_OK;
   HIP_TRY(hipMalloc((void**)out, count * sizeof(T)));
   ctx->scene_allocs.push_back(*out);
+  ctx->scene_bytes += count * sizeof(T);
   if (host) HIP_TRY(hipMemcpy(*out, host, count * sizeof(T), hipMemcpyHostToDevice));
   return IZPI_OK;
 }
@@ -1963,9 +1941,17 @@ int grow(izpi_ctx* ctx, void** p, size_t* cap, size_t bytes) {
   return IZPI_OK;
 }
 
+// Device bytes of the render workspace (the buffers `grow` manages).
+uint64_t workspace_bytes(const izpi_ctx* ctx) {
+  return (uint64_t)ctx->samples_cap + ctx->recs_cap + ctx->pool_cap + ctx->ring_cap + ctx->running_cap + ctx->out_cap +
+         ctx->tiles_cap + ctx->utiles_cap + ctx->bg_cap + ctx->rhot_cap + ctx->raux_cap + ctx->hit_cap + ctx->phot_cap +
+         ctx->pcold_cap + ctx->queue_cap + ctx->spill_cap + ctx->post_cap + ctx->share_cap + ctx->gather_cap;
+}
+
 void free_scene(izpi_ctx* ctx) {
   for (void* p : ctx->scene_allocs) (void)hipFree(p);
   ctx->scene_allocs.clear();
+  ctx->scene_bytes = 0;
   ctx->have_scene = false;
 }
 
@@ -1978,29 +1964,25 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
   return IZPI_OK;
 }
 
-// Traversal kernel selection. IZPI_TRACE=1 picks the one-visit-per-iteration kernel
-// (k_trace, LDS stack sized by the host bound); the default 2 picks the step-scheduled
-// k_trace2 with an LDS ring of IZPI_TRACE_RING entries (8/16/32, default 16) and global
-// spill; IZPI_PRIM_W (default 32) weighs primitive steps against node steps (x/16).
-// All variants give identical results and counters.
+// Traversal kernel selection: k_trace2 with a 16-entry LDS stack ring and global spill,
+// 5 waves/SIMD. Instances: DIST (leaf tests spread over the wave; off only when primitive
+// indices do not fit the 26-bit LDS packing, or IZPI_TRACE_DIST=0) x TRI (sphere code
+// compiled out for triangle-only scenes; IZPI_TRACE_NO_TRI forces the general one).
+// Runtime knobs: IZPI_PRIM_W (default 32) weighs primitive steps against node steps
+// (x/16); IZPI_TRACE_CHUNK queue entries per dequeue; IZPI_REFILL_MIN idle lanes per
+// refill. All settings give identical results and counters.
+constexpr int TRACE_RING = 16, TRACE_WPE = 5;
 struct Tracer {
-  int variant = 2, stack = 32, ring = 16, wpe = 5;
-  bool p2 = true;  // DIST: spread leaf tests over the wave
-  bool tri = false;  // sphere code compiled out (scene without spheres)
+  bool p2 = true;    // DIST
+  bool tri = false;  // TRI
   uint32_t prim_w = 32, tchunk = 128, refill_min = 16;
   int blocks = 0;
 };
 
-// k_trace2 instances: ring entries x minimum waves per SIMD (register budget).
-#define IZPI_T2_LIST(X) X(8, 4, false, false) X(8, 5, false, false) X(16, 4, false, false) X(16, 5, false, false) \
-  X(32, 4, false, false) X(16, 4, true, false) X(16, 5, true, false) X(8, 5, true, false) X(16, 5, true, true)   \
-  X(8, 5, true, true) X(16, 5, false, true)
+#define IZPI_T2_LIST(X) X(true, false) X(true, true) X(false, false) X(false, true)
 
 int make_tracer(izpi_ctx* ctx, Tracer* t) {
   *t = Tracer();
-  if (const char* e = getenv("IZPI_TRACE")) t->variant = atoi(e) == 1 ? 1 : 2;
-  if (const char* e = getenv("IZPI_TRACE_RING")) t->ring = atoi(e);
-  if (const char* e = getenv("IZPI_TRACE_WPE")) t->wpe = atoi(e);
   if (const char* e = getenv("IZPI_TRACE_DIST")) t->p2 = atoi(e) != 0;
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
@@ -2009,42 +1991,23 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   // DIST packs (primitive << 6 | lane) into one LDS word
   if (ctx->num_prims >= (1u << 26)) t->p2 = false;
   t->tri = ctx->sc.tri_only != 0 && !getenv("IZPI_TRACE_NO_TRI");
-  t->stack = ctx->stack_needed <= 32 ? 32 : 64;
   int rc = IZPI_ERR_INVALID;
-  if (t->variant == 1) {
-    rc = t->stack == 32 ? resident_blocks(ctx, k_trace<32>, &t->blocks) : resident_blocks(ctx, k_trace<64>, &t->blocks);
-    return rc;
-  }
-#define IZPI_T2_OCC(R, W, P, T) \
-  if (t->ring == R && t->wpe == W && t->p2 == P && t->tri == T) rc = resident_blocks(ctx, k_trace2<R, W, P, T>, &t->blocks);
+#define IZPI_T2_OCC(P, T) \
+  if (t->p2 == P && t->tri == T) rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
-  if (rc == IZPI_ERR_INVALID && t->tri) {  // no triangle-only instance for this ring/wpe
-    t->tri = false;
-    IZPI_T2_LIST(IZPI_T2_OCC)
-  }
-  if (rc == IZPI_ERR_INVALID && t->p2) {  // no distributed instance for this ring/wpe: sequential leaf tests
-    t->p2 = false;
-    IZPI_T2_LIST(IZPI_T2_OCC)
-  }
 #undef IZPI_T2_OCC
-  if (rc == IZPI_ERR_INVALID) { ctx->err = "no k_trace2 instance for IZPI_TRACE_RING/IZPI_TRACE_WPE"; return rc; }
   if (rc) return rc;
   return grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, (size_t)t->blocks * 256 * 64 * sizeof(int32_t));
 }
 
 void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
   const dim3 g(t.blocks), b(256);
-  if (t.variant == 1) {
-    if (t.stack == 32) hipLaunchKernelGGL(k_trace<32>, g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
-    else hipLaunchKernelGGL(k_trace<64>, g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1);
-    return;
-  }
   const uint32_t stride = (uint32_t)t.blocks * 256;
-#define IZPI_T2_LAUNCH(R, W, P, T)                                                                            \
-  if (t.ring == R && t.wpe == W && t.p2 == P && t.tri == T) {                                                \
-    hipLaunchKernelGGL((k_trace2<R, W, P, T>), g, b, 0, st, ctx->sc, wp, ctx->d_counters, ctx->d_misc + 1, spill, \
-                       stride, t.prim_w, t.tchunk, t.refill_min);                                            \
-    return;                                                                                                  \
+#define IZPI_T2_LAUNCH(P, T)                                                                                   \
+  if (t.p2 == P && t.tri == T) {                                                                               \
+    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T>), g, b, 0, st, ctx->sc, wp, ctx->d_counters,     \
+                       ctx->d_misc + 1, spill, stride, t.prim_w, t.tchunk, t.refill_min);                      \
+    return;                                                                                                    \
   }
   IZPI_T2_LIST(IZPI_T2_LAUNCH)
 #undef IZPI_T2_LAUNCH
@@ -2062,20 +2025,20 @@ uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint3
   return n;
 }
 
-// One chunk loop of the wavefront scheme: k_start fills the slots, then k_trace /
-// k_shade alternate until no slot has a ray left; k_accumulate folds the chunk's
-// per-sample radiance into the pixels in sample order.
+// One chunk loop of the wavefront scheme: k_start fills the slots, then k_trace2 /
+// k_shade alternate until no slot has a ray left (the last few paths run to their end
+// in k_tail); k_accumulate folds the chunk's per-sample radiance into the pixels in
+// sample order.
 template <int SAMPLER, int MATSET>
 int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveParams& wp, AccumParams& ap,
-               uint32_t num_pixels, uint32_t chunk, float* trace_ms, float* shade_ms, float* tail_ms, uint32_t* launches) {
+               uint32_t num_pixels, uint32_t chunk, uint32_t pool_blocks, float* trace_ms, float* shade_ms, float* tail_ms,
+               uint32_t* launches) {
   hipStream_t st = ctx->stream;
   int shade_res = 0;
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
   if ((rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res))) return rc;
-  int refill_res = 0;
-  if ((rc = resident_blocks(ctx, k_refill<SAMPLER>, &refill_res))) return rc;
   // tail kernel: used once every unit has started and at most `tail_max` paths remain
   const bool tail_deep = ctx->stack_needed > 32;
   int tail_res = 0;
@@ -2083,158 +2046,117 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
                       : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
   uint64_t tail_max = (uint64_t)tail_res * 256;
   if (const char* e = getenv("IZPI_TAIL")) tail_max = strtoull(e, nullptr, 10);
-  // Wavefront lanes. With two lanes the slots, queues and records are split in halves and
-  // each lane alternates k_trace2 / k_shade on its own stream: the drain at the end of one
-  // lane's pass (few waves left, ~0.5 ms of k_trace2 per pass on C3) is filled by the other
-  // lane's kernels. Lanes share the unit head, so the work and the results are the same.
-  // Measured on C3: 411.8 ms per frame with two lanes against 407.6-443.9 with one (the
-  // spread is host turnaround between pass batches, which the second lane covers), so
-  // one lane stays the default and IZPI_LANES=2 selects two.
-  int lanes = 1;
-  if (const char* e = getenv("IZPI_LANES")) lanes = atoi(e) == 2 && sp.slots >= 2 ? 2 : 1;
-  struct Lane {
-    hipStream_t st;
-    uint32_t* misc;      // [2] trace cursor, [3..4] queue counts, [5] free count (lane 0: ctx->d_misc)
-    uint32_t* hc;        // pinned readback
-    hipEvent_t* ev;
-    int32_t* spill;
-    uint32_t off, slots;
-    uint32_t* q[2];
-    uint32_t* qn[2];
-    WaveParams wp;
-    ShadeParams sp;
-    int cur;
-    uint32_t n;
-  } L[2];
-  if (lanes == 2 && (rc = grow(ctx, (void**)&ctx->d_spill2, &ctx->spill2_cap, ctx->spill_cap))) return rc;
-  const uint32_t half = lanes == 2 ? sp.slots / 2 : sp.slots;
-  for (int l = 0; l < lanes; l++) {
-    Lane& a = L[l];
-    a.st = l ? ctx->stream2 : st;
-    a.misc = l ? ctx->d_misc2 : ctx->d_misc;
-    a.hc = l ? ctx->h_count2 : ctx->h_count;
-    a.ev = l ? ctx->evb2 : ctx->evb;
-    a.spill = l ? ctx->d_spill2 : ctx->d_spill;
-    a.off = l ? half : 0;
-    a.slots = l ? sp.slots - half : half;
-    a.q[0] = ctx->d_queue + a.off;
-    a.q[1] = ctx->d_queue + sp.slots + a.off;
-    a.qn[0] = a.misc + 3;
-    a.qn[1] = a.misc + 4;
-    a.wp = wp;
-    a.wp.rhot = wp.rhot + a.off; a.wp.raux = wp.raux + a.off; a.wp.hhot = wp.hhot + a.off; a.wp.huv = wp.huv + a.off;
-    a.wp.phot = wp.phot + a.off; a.wp.pcold = wp.pcold + a.off;
-    a.wp.trace_next = a.misc + 2;
-    a.wp.slots = a.slots;
-    a.wp.free_q = ctx->d_queue + 2 * (size_t)sp.slots + a.off;
-    a.wp.free_count = a.misc + 5;
-    a.sp = sp;
-    a.sp.slots = a.slots;
-    a.sp.recs = sp.recs + (size_t)a.off * sp.rec_depth * RecLayout<SAMPLER>::D;
-    a.sp.unit_base = a.off;
-    a.cur = 0;
-    a.n = 0;
-  }
-  const uint64_t lane_tail_max = tail_max / (uint64_t)lanes;
+  // k_tail's allocations cannot park: every tail path must find a published block
+  if (sp.rec_pool) tail_max = std::min<uint64_t>(tail_max, pool_blocks);
+  uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
+  uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
+  if (sp.rec_pool)
+    hipLaunchKernelGGL(k_pool_init, dim3((pool_blocks + 255) / 256), dim3(256), 0, st, sp.pool_ring, pool_blocks,
+                       pool_blocks / POOL_SHARDS, sp.pool_ctr);
+  HIP_TRY(hipGetLastError());
   for (uint32_t s0 = 0; s0 < req->spp; s0 += chunk) {
     const uint32_t cs = std::min(chunk, req->spp - s0);
     sp.chunk_spp = cs; sp.s0 = s0; sp.total_units = num_pixels * cs;
-    const uint32_t start_slots = std::min<uint32_t>(sp.slots, sp.total_units);
-    HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)start_slots, 1, st));  // head: k_start gives slot i unit i
-    if (lanes == 2) {
-      HIP_TRY(hipEventRecord(ctx->evj, st));
-      HIP_TRY(hipStreamWaitEvent(ctx->stream2, ctx->evj, 0));  // lane 1 after the head reset and the setup copies
-    }
-    for (int l = 0; l < lanes; l++) {
-      Lane& a = L[l];
-      a.sp.chunk_spp = cs; a.sp.s0 = s0; a.sp.total_units = sp.total_units;
-      HIP_TRY(hipMemsetAsync(a.misc + 3, 0, 2 * sizeof(uint32_t), a.st));  // queue counts
-      a.wp.q_out = a.q[0]; a.wp.q_out_count = a.qn[0];
-      const uint32_t fill = std::min<uint32_t>(a.slots, sp.total_units > a.off ? sp.total_units - a.off : 0u);
-      if (fill)
-        hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(a.hc, a.qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, a.st));
-    }
-    for (int l = 0; l < lanes; l++) {
-      HIP_TRY(hipStreamSynchronize(L[l].st));
-      L[l].n = L[l].hc[0];
-      L[l].cur = 0;
-    }
+    const uint32_t fill = std::min<uint32_t>(sp.slots, sp.total_units);
+    HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)fill, 1, st));  // unit head: k_start gives slot i unit i
+    HIP_TRY(hipMemsetAsync(ctx->d_misc + 3, 0, 2 * sizeof(uint32_t), st));  // queue counts
+    wp.q_out = q[0]; wp.q_out_count = qn[0];
+    hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, ctx->sc, sp, wp);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint32_t n = ctx->h_count[0];
+    int cur = 0;
     // Launch passes in batches without a host round-trip per pass: both kernels read
     // their queue length from device memory and exit at once when it is zero, so the
     // host only polls the queue length once per batch (overshoot costs a few empty
     // launches of ~5 us).
     const int B = IZPI_PASS_BATCH;
-    for (;;) {
-      bool any = false;
-      for (int l = 0; l < lanes; l++) {
-        Lane& a = L[l];
-        if (a.n == 0) continue;
-        any = true;
-        for (int b = 0; b < B; b++) {
-          a.wp.q_in = a.q[a.cur]; a.wp.q_in_count = a.qn[a.cur];
-          a.wp.q_out = a.q[1 - a.cur]; a.wp.q_out_count = a.qn[1 - a.cur];
-          HIP_TRY(hipMemsetAsync(a.misc + 2, 0, sizeof(uint32_t), a.st));
-          HIP_TRY(hipMemsetAsync(a.qn[1 - a.cur], 0, sizeof(uint32_t), a.st));
-          if (IZPI_SPLIT_REFILL) HIP_TRY(hipMemsetAsync(a.wp.free_count, 0, sizeof(uint32_t), a.st));
-          HIP_TRY(hipEventRecord(a.ev[3 * b], a.st));
-          launch_trace(ctx, tr, a.wp, a.st, a.spill);
-          HIP_TRY(hipGetLastError());
-          HIP_TRY(hipEventRecord(a.ev[3 * b + 1], a.st));
-          hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
-          HIP_TRY(hipGetLastError());
-          if (IZPI_SPLIT_REFILL) {
-            hipLaunchKernelGGL(k_refill<SAMPLER>, dim3(refill_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
-            HIP_TRY(hipGetLastError());
-          }
-          HIP_TRY(hipEventRecord(a.ev[3 * b + 2], a.st));
-          a.cur = 1 - a.cur;
-        }
-        HIP_TRY(hipMemcpyAsync(a.hc, a.misc, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, a.st));
+    while (n > 0) {
+      for (int b = 0; b < B; b++) {
+        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
+        wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
+        HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
+        HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
+        HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
+        launch_trace(ctx, tr, wp, st, ctx->d_spill);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
+        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
+        cur = 1 - cur;
       }
-      if (!any) break;
-      for (int l = 0; l < lanes; l++) {
-        Lane& a = L[l];
-        if (a.n == 0) continue;
-        HIP_TRY(hipStreamSynchronize(a.st));
-        for (int b = 0; b < B; b++) {
-          float t_ms = 0, s_ms = 0;
-          HIP_TRY(hipEventElapsedTime(&t_ms, a.ev[3 * b], a.ev[3 * b + 1]));
-          HIP_TRY(hipEventElapsedTime(&s_ms, a.ev[3 * b + 1], a.ev[3 * b + 2]));
-          *trace_ms += t_ms;
-          *shade_ms += s_ms;
-          (*launches)++;
-        }
-        a.n = a.hc[3 + a.cur];
+      HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->d_misc, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      for (int b = 0; b < B; b++) {
+        float t_ms = 0, s_ms = 0;
+        HIP_TRY(hipEventElapsedTime(&t_ms, ctx->evb[3 * b], ctx->evb[3 * b + 1]));
+        HIP_TRY(hipEventElapsedTime(&s_ms, ctx->evb[3 * b + 1], ctx->evb[3 * b + 2]));
+        *trace_ms += t_ms;
+        *shade_ms += s_ms;
+        (*launches)++;
       }
-      // every unit has started: finish each lane's remaining paths in one k_tail launch
-      // (the unit head is read from lane 0's copy, refreshed this round)
-      const uint32_t head = ctx->h_count[0];
-      for (int l = 0; l < lanes; l++) {
-        Lane& a = L[l];
-        if (a.n > 0 && a.n <= lane_tail_max && head >= sp.total_units) {
-          a.wp.q_in = a.q[a.cur]; a.wp.q_in_count = a.qn[a.cur];
-          HIP_TRY(hipEventRecord(a.ev[0], a.st));
-          if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
-          else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, a.st, ctx->sc, a.sp, a.wp);
-          HIP_TRY(hipGetLastError());
-          HIP_TRY(hipEventRecord(a.ev[1], a.st));
-          HIP_TRY(hipEventSynchronize(a.ev[1]));
-          float t_ms = 0;
-          HIP_TRY(hipEventElapsedTime(&t_ms, a.ev[0], a.ev[1]));
-          *tail_ms += t_ms;
-          a.n = 0;
-        }
+      n = ctx->h_count[3 + cur];
+      // every unit has started: finish the remaining paths in one k_tail launch
+      if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
+        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
+        HIP_TRY(hipEventRecord(ctx->ev2, st));
+        if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
+        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev3, st));
+        HIP_TRY(hipEventSynchronize(ctx->ev3));
+        float t_ms = 0;
+        HIP_TRY(hipEventElapsedTime(&t_ms, ctx->ev2, ctx->ev3));
+        *tail_ms += t_ms;
+        n = 0;
       }
-    }
-    if (lanes == 2) {  // k_accumulate (stream 0) after lane 1's last pass
-      HIP_TRY(hipEventRecord(ctx->evj, ctx->stream2));
-      HIP_TRY(hipStreamWaitEvent(st, ctx->evj, 0));
     }
     ap.chunk_spp = cs;
     ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
     hipLaunchKernelGGL(k_accumulate, dim3((num_pixels + 255) / 256), dim3(256), 0, st, ap);
+    HIP_TRY(hipGetLastError());
+  }
+  return IZPI_OK;
+}
+
+// The request's tiles: its own list, or the whole frame in common.Tiles steps and
+// grid.WalkGrid's spiral order (tiles.go:6-24, renderer.go:172-188).
+int request_tiles(izpi_ctx* ctx, const izpi_render_req* req, std::vector<uint32_t>& tiles) {
+  if (req->num_tiles) {
+    if (!req->tiles) { ctx->err = "num_tiles without tiles"; return IZPI_ERR_INVALID; }
+    tiles.assign(req->tiles, req->tiles + 4 * (size_t)req->num_tiles);
+    return IZPI_OK;
+  }
+  tiles.resize(4 * ((size_t)req->width * req->height / 16 + 16));
+  const uint32_t nt = izpi_host_tiles(req->width, req->height, tiles.data(), (uint32_t)(tiles.size() / 4));
+  if (nt == 0) { ctx->err = "image size not divisible by any common.Tiles step"; return IZPI_ERR_INVALID; }
+  tiles.resize(4 * (size_t)nt);
+  return IZPI_OK;
+}
+
+// Render's post-processing of a whole-frame canvas on the context's stream: the Spectral
+// sampler's FireflyRejection + XYZToRGB (renderer.go:215-219), then the leader's "png"
+// pipeline, Gamma and Clamp(1.0) (leader.go:179-182).
+int apply_post(izpi_ctx* ctx, const izpi_render_req* req, double* canvas_dev) {
+  hipStream_t st = ctx->stream;
+  int rc;
+  if (req->post & IZPI_POST_SPECTRAL) {
+    if ((rc = grow(ctx, (void**)&ctx->d_post, &ctx->post_cap, (size_t)req->width * req->height * 4 * sizeof(double)))) return rc;
+    dim3 g((req->width + 15) / 16, (req->height + 15) / 16);
+    hipLaunchKernelGGL(k_spectral_post, g, dim3(256), 0, st, canvas_dev, ctx->d_post, req->width, req->height, req->exposure);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(canvas_dev, ctx->d_post, (size_t)req->width * req->height * 4 * sizeof(double),
+                           hipMemcpyDeviceToDevice, st));
+  }
+  if (req->post & IZPI_POST_GAMMA_CLAMP) {
+    PostFilters pf;
+    memset(&pf, 0, sizeof pf);
+    pf.n = 2; pf.kind[0] = IZPI_FILTER_GAMMA; pf.kind[1] = IZPI_FILTER_CLAMP; pf.param[1] = 1.0;
+    const uint64_t np = (uint64_t)req->width * req->height;
+    hipLaunchKernelGGL(k_postprocess, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, canvas_dev, np, pf);
     HIP_TRY(hipGetLastError());
   }
   return IZPI_OK;
@@ -2256,14 +2178,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   }
   if (ctx->sc.num_lights == 0) { ctx->err = "scene has no lights (HitableSlice.PDFValue divides by zero)"; return IZPI_ERR_INVALID; }
   std::vector<uint32_t> tiles;
-  if (req->num_tiles) {
-    tiles.assign(req->tiles, req->tiles + 4 * (size_t)req->num_tiles);
-  } else {
-    tiles.resize(4 * ((size_t)req->width * req->height / 16 + 16));
-    uint32_t nt = izpi_host_tiles(req->width, req->height, tiles.data(), (uint32_t)(tiles.size() / 4));
-    if (nt == 0) { ctx->err = "image size not divisible by any common.Tiles step"; return IZPI_ERR_INVALID; }
-    tiles.resize(4 * (size_t)nt);
-  }
+  int rc = request_tiles(ctx, req, tiles);
+  if (rc) return rc;
   uint32_t tw = 0, th = 0;
   const uint32_t ntiles = validate_tiles(req, tiles.data(), (uint32_t)(tiles.size() / 4), &tw, &th);
   if (ntiles == 0) { ctx->err = "tiles must be non-empty, in bounds and equal-sized"; return IZPI_ERR_INVALID; }
@@ -2271,40 +2187,61 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (num_pixels64 > (1ull << 30)) { ctx->err = "too many pixels in one request"; return IZPI_ERR_INVALID; }
   const uint32_t num_pixels = (uint32_t)num_pixels64;
   if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
-  // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
-  // sample order. One chunk per request when it fits in 1/4 of the free HBM (C3: 12.9 GB
-  // of 288 GB), so the wavefront drains once per frame instead of once per chunk.
+  // Sizing against the HBM this context may use: what is free plus its own workspace
+  // (which a later frame reuses), so that every frame of a renderer sizes alike.
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-  uint64_t max_units = std::max<uint64_t>(64ull << 20, (uint64_t)(free_b / 4) / (3 * sizeof(double)));
+  const uint64_t avail = free_b ? (uint64_t)free_b + workspace_bytes(ctx) : 0;
+  // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
+  // sample order. One chunk per request when it fits in 1/4 of the HBM (C3: 12.9 GB of
+  // 288 GB), so the wavefront drains once per frame instead of once per chunk.
+  uint64_t max_units = std::max<uint64_t>(64ull << 20, (avail / 4) / (3 * sizeof(double)));
   if (const char* e = getenv("IZPI_CHUNK_UNITS")) max_units = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
+  // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
+  // blocks (ShadeParams::rec_pool). Colour records are 48 B, spectral 32 B, and spectral
+  // glass paths run deeper, hence the larger dense part there.
+  const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
+  const uint32_t D = spectral ? RecLayout<IZPI_SAMPLER_SPECTRAL>::D : RecLayout<IZPI_SAMPLER_COLOUR>::D;
+  const uint32_t max_depth = std::max(1u, req->max_depth);
+  uint32_t rec_dense = spectral ? 16u : 8u;
+  if (const char* e = getenv("IZPI_REC_DENSE")) rec_dense = (uint32_t)std::max(1, atoi(e));
+  rec_dense = std::min(rec_dense, max_depth);
+  const uint32_t rec_pool = max_depth - rec_dense;
+  // PathCold (wavelength, dielectric point) is read only by the spectral sampler and glass
+  const bool need_cold = spectral || !ctx->sc.no_pathlen;
   // Paths in flight per wavefront pass. Larger = fewer k_trace/k_shade launches and
-  // a smaller share of launch tails; costs HBM for the per-slot state (~176 B +
-  // 48 B per depth level of unwinding records).
+  // a smaller share of launch tails.
   uint64_t slot_cap = 40ull << 20;  // C3: 16M -> 435 ms/frame, 24M -> 414, 40M -> 407 (fewer passes, fewer pass tails)
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
-  {  // keep the wavefront state within half of the free HBM (the per-sample results take at most a quarter)
-    if (free_b > 0) {
-      const uint64_t per_slot = sizeof(RayHot) + sizeof(RayAux) + sizeof(HitHot) + sizeof(HitUV) + sizeof(PathHot) + sizeof(PathCold) + 12 +
-                                (uint64_t)std::max(1u, req->max_depth) * 6 * sizeof(double);
-      slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (free_b / 2) / per_slot));
-    }
-  }
+  const uint64_t per_slot = sizeof(RayHot) + sizeof(RayAux) + sizeof(HitSt) + sizeof(PathHot) +
+                            (need_cold ? sizeof(PathCold) : 0) + 3 * sizeof(uint32_t) + (uint64_t)rec_dense * D * sizeof(double);
+  // overflow blocks per 16 slots (C3: ~3% of the paths in flight are deeper than 8)
+  uint32_t pool_div = 16;
+  if (const char* e = getenv("IZPI_POOL_DIV")) pool_div = (uint32_t)std::max(1, atoi(e));
+  const uint64_t per_block = (uint64_t)rec_pool * D * sizeof(double) + sizeof(uint32_t);
+  if (avail > 0)  // the wavefront state within half of the HBM
+    slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (avail / 2) / (per_slot + per_block / pool_div + 1)));
   const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);
-  const uint32_t depth_cap = std::max(1u, req->max_depth);
-  int rc;
+  uint32_t pool_blocks = 0;
+  if (rec_pool) {  // POOL_SHARDS rings of a power of two each, at least 16 blocks per ring
+    pool_blocks = POOL_SHARDS * 16;
+    while (pool_blocks < slots / pool_div && pool_blocks < (1u << 30)) pool_blocks <<= 1;
+  }
   if ((rc = grow(ctx, (void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * 3 * sizeof(double)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_recs, &ctx->recs_cap, (size_t)depth_cap * 6 * slots * sizeof(double)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_recs, &ctx->recs_cap, (size_t)rec_dense * D * slots * sizeof(double)))) return rc;
+  if (rec_pool) {
+    if ((rc = grow(ctx, (void**)&ctx->d_pool, &ctx->pool_cap, (size_t)pool_blocks * rec_pool * D * sizeof(double)))) return rc;
+    if ((rc = grow(ctx, (void**)&ctx->d_ring, &ctx->ring_cap, (size_t)pool_blocks * sizeof(uint32_t)))) return rc;
+  }
   if ((rc = grow(ctx, (void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_rhot, &ctx->rhot_cap, (size_t)slots * sizeof(RayHot)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_raux, &ctx->raux_cap, (size_t)slots * sizeof(RayAux)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_hhot, &ctx->hhot_cap, (size_t)slots * sizeof(HitHot)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_huv, &ctx->huv_cap, (size_t)slots * sizeof(HitUV)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_hit, &ctx->hit_cap, (size_t)slots * sizeof(HitSt)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_phot, &ctx->phot_cap, (size_t)slots * sizeof(PathHot)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_pcold, &ctx->pcold_cap, (size_t)slots * sizeof(PathCold)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)3 * slots * sizeof(uint32_t)))) return rc;
+  if (need_cold && (rc = grow(ctx, (void**)&ctx->d_pcold, &ctx->pcold_cap, (size_t)slots * sizeof(PathCold)))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)2 * slots * sizeof(uint32_t)))) return rc;
   const size_t nbg = req->num_bg_spd;
   if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
   hipStream_t st = ctx->stream;
@@ -2315,7 +2252,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   }
   HIP_TRY(hipMemsetAsync(ctx->d_running, 0, (size_t)num_pixels * 3 * sizeof(double), st));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), st));
-  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 6 * sizeof(uint32_t), st));
+  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), st));
 
   ShadeParams sp{};
   sp.width = req->width; sp.height = req->height; sp.max_depth = req->max_depth;
@@ -2325,11 +2262,17 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
     if (!(req->bg_spd_wavelengths[i - 1] <= req->bg_spd_wavelengths[i])) sp.bg_sorted = 0;
   sp.tiles = ctx->d_tiles; sp.bg_wl = ctx->d_bg; sp.bg_val = ctx->d_bg + nbg;
   sp.background[0] = req->background[0]; sp.background[1] = req->background[1]; sp.background[2] = req->background[2];
-  sp.rec_depth = depth_cap;
+  sp.rec_dense = rec_dense; sp.rec_pool = rec_pool;
+  sp.pool_shift = 0;
+  while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.head = ctx->d_misc;
+  sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
+  sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
   WaveParams wp{};
-  wp.rhot = ctx->d_rhot; wp.raux = ctx->d_raux; wp.hhot = ctx->d_hhot; wp.huv = ctx->d_huv; wp.phot = ctx->d_phot; wp.pcold = ctx->d_pcold; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  wp.rhot = ctx->d_rhot; wp.raux = ctx->d_raux; wp.hit = ctx->d_hit; wp.phot = ctx->d_phot;
+  wp.pcold = need_cold ? ctx->d_pcold : nullptr; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  wp.pool_ctr = sp.pool_ctr;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
   ap.tile_w = tw; ap.tile_h = th; ap.sampler = req->sampler; ap.out_layout = req->out_layout;
@@ -2338,7 +2281,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   float trace_ms = 0, shade_ms = 0, tail_ms = 0;
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
-#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, &trace_ms, &shade_ms, &tail_ms, &launches)
+#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches)
   const bool basic = ctx->basic_materials;
   if (req->sampler == IZPI_SAMPLER_COLOUR)
     rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
@@ -2347,22 +2290,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
 #undef IZPI_RUN
   if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, st));
-  if (req->post & IZPI_POST_SPECTRAL) {  // renderer.go:215-219, outside the timed render like the reference
-    if ((rc = grow(ctx, (void**)&ctx->d_post, &ctx->post_cap, (size_t)req->width * req->height * 4 * sizeof(double)))) return rc;
-    dim3 g((req->width + 15) / 16, (req->height + 15) / 16);
-    hipLaunchKernelGGL(k_spectral_post, g, dim3(256), 0, st, out_dev, ctx->d_post, req->width, req->height, req->exposure);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(out_dev, ctx->d_post, (size_t)req->width * req->height * 4 * sizeof(double),
-                           hipMemcpyDeviceToDevice, st));
-  }
-  if (req->post & IZPI_POST_GAMMA_CLAMP) {  // leader.go:179-182 ("png" output mode): Gamma, then Clamp(1.0)
-    PostFilters pf;
-    memset(&pf, 0, sizeof pf);
-    pf.n = 2; pf.kind[0] = IZPI_FILTER_GAMMA; pf.kind[1] = IZPI_FILTER_CLAMP; pf.param[1] = 1.0;
-    const uint64_t np = (uint64_t)req->width * req->height;
-    hipLaunchKernelGGL(k_postprocess, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, out_dev, np, pf);
-    HIP_TRY(hipGetLastError());
-  }
+  if ((rc = apply_post(ctx, req, out_dev))) return rc;
   HIP_TRY(hipEventSynchronize(ctx->ev1));
   float total_ms = 0;
   HIP_TRY(hipEventElapsedTime(&total_ms, ctx->ev0, ctx->ev1));
@@ -2378,6 +2306,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.kernel_ms = trace_ms; s.shade_ms = shade_ms; s.total_ms = total_ms; s.launches = launches; s.tail_ms = tail_ms;
   s.node_steps = cnt[CNT_NSTEP]; s.prim_steps = cnt[CNT_PSTEP]; s.leaf_shortcuts = cnt[CNT_SHORT];
   s.tail_node_visits = cnt[CNT_TAIL_NODES]; s.tail_tri_tests = cnt[CNT_TAIL_TRI]; s.tail_sph_tests = cnt[CNT_TAIL_SPH];
+  s.parks = cnt[CNT_PARK];
+  s.workspace_bytes = workspace_bytes(ctx);
+  s.scene_bytes = ctx->scene_bytes;
+  s.slots = slots; s.rec_dense = rec_dense; s.pool_blocks = pool_blocks; s.chunk_spp = chunk;
 #ifdef IZPI_SHADE_CLOCKS
   fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu (wave cycles)\n", cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL],
           cnt[CNT_SCLK_PUSH]);
@@ -2387,45 +2319,117 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
           cnt[CNT_CLK_NODE], cnt[CNT_CLK_PRIM], cnt[CNT_CLK_ADV]);
 #endif
   if (misc[1]) {
-    ctx->err = misc[1] & 1u ? "device guard: traversal stack overflow" : "device guard: unknown material kind";
+    ctx->err = misc[1] & 1u   ? "device guard: traversal stack overflow"
+               : misc[1] & 2u ? "device guard: unknown material kind"
+                              : "device guard: no overflow record block in k_tail";
     return IZPI_ERR_DEVICE;
   }
   return IZPI_OK;
 }
 
+// ------------------------------------------------------------------ multi-GPU
+// The frame is split into G shares: tile t (in common.Tiles' spiral order) goes to share
+// t % G, so the costly centre tiles spread over all devices. Share r is rendered packed
+// (IZPI_OUT_PACKED) into d_share, padded to the largest share's size so that one gather
+// moves equal blocks; the root scatters share r's tiles from block r into the canvas.
+struct Shares {
+  std::vector<uint32_t> all;  // the frame's tiles, [n][4]
+  uint32_t n = 1;             // shares
+  size_t block = 0;           // doubles per (padded) share
+  std::vector<uint32_t> mine(uint32_t r) const {
+    std::vector<uint32_t> t(all.size());
+    t.resize(4 * (size_t)izpi_host_share_tiles(all.data(), (uint32_t)(all.size() / 4), r, n, t.data()));
+    return t;
+  }
+};
+
+int make_shares(izpi_ctx* ctx, const izpi_render_req* req, uint32_t n, Shares& sh) {
+  if (!req || req->width == 0 || req->height == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
+  if (req->out_layout != IZPI_OUT_CANVAS) { ctx->err = "multi-GPU renders produce a canvas (IZPI_OUT_CANVAS)"; return IZPI_ERR_INVALID; }
+  int rc = request_tiles(ctx, req, sh.all);
+  if (rc) return rc;
+  uint32_t tw = 0, th = 0;
+  if (!validate_tiles(req, sh.all.data(), (uint32_t)(sh.all.size() / 4), &tw, &th)) {
+    ctx->err = "tiles must be non-empty, in bounds and equal-sized";
+    return IZPI_ERR_INVALID;
+  }
+  sh.n = n;
+  const size_t ntiles = sh.all.size() / 4;
+  sh.block = ((ntiles + n - 1) / n) * (size_t)tw * th * 4;
+  return IZPI_OK;
+}
+
+// Render share r of the frame into ctx->d_share (stats in ctx->last).
+int render_share(izpi_ctx* ctx, const izpi_render_req* req, const Shares& sh, uint32_t r) {
+  int rc = grow(ctx, (void**)&ctx->d_share, &ctx->share_cap, sh.block * sizeof(double));
+  if (rc) return rc;
+  const std::vector<uint32_t> mine = sh.mine(r);
+  memset(&ctx->last, 0, sizeof(ctx->last));
+  if (mine.empty()) return IZPI_OK;  // more shares than tiles: an empty block joins the gather
+  izpi_render_req q = *req;
+  q.num_tiles = (uint32_t)(mine.size() / 4);
+  q.tiles = mine.data();
+  q.out_layout = IZPI_OUT_PACKED;
+  q.post = IZPI_POST_NONE;
+  return render_impl(ctx, &q, ctx->d_share);
+}
+
+// Root: scatter every share's packed tiles from d_gather into the canvas (row H - y,
+// rgb.go:41), then Render's post-processing of the assembled frame.
+int assemble(izpi_ctx* ctx, const izpi_render_req* req, const Shares& sh, double* canvas_dev) {
+  izpi_ctx* root = ctx;  // (HIP_TRY reports into ctx)
+  hipStream_t st = root->stream;
+  for (uint32_t r = 0; r < sh.n; r++) {
+    const std::vector<uint32_t> t = sh.mine(r);
+    if (t.empty()) continue;
+    const uint32_t nt = (uint32_t)(t.size() / 4), tw = t[2] - t[0] + 1, th = t[3] - t[1] + 1;
+    int rc = grow(root, (void**)&root->d_utiles, &root->utiles_cap, sh.all.size() * sizeof(uint32_t));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(root->d_utiles, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    const uint32_t np = nt * tw * th;
+    hipLaunchKernelGGL(k_unpack, dim3((np + 255) / 256), dim3(256), 0, st, root->d_utiles, np, tw, th, req->width,
+                       req->height, root->d_gather + (size_t)r * sh.block, canvas_dev);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));  // d_utiles is reused by the next share
+  }
+  int rc = apply_post(root, req, canvas_dev);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  return IZPI_OK;
+}
+
 }  // namespace
+
+// One context per device of a single-process multi-GPU render (izpi_gpu_multi_*).
+struct izpi_multi {
+  std::vector<izpi_ctx*> ctx;
+  std::string err;
+};
 
 extern "C" {
 
 int izpi_gpu_open(int device, izpi_ctx** out) {
+  if (!out) return IZPI_ERR_INVALID;
   *out = nullptr;
-  izpi_ctx* ctx = new izpi_ctx();
-  ctx->device = device;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n == 0 || device < 0 || device >= n) {
-    delete ctx;
-    return IZPI_ERR_HIP;
-  }
-  if (hipSetDevice(device) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
+  if (e != hipSuccess || n == 0 || device < 0 || device >= n) return IZPI_ERR_HIP;
+  if (hipSetDevice(device) != hipSuccess) return IZPI_ERR_HIP;
+  izpi_ctx* ctx = new izpi_ctx();
+  ctx->device = device;
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
-  ctx->num_cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
-      hipEventCreate(&ctx->ev2) != hipSuccess || hipEventCreate(&ctx->ev3) != hipSuccess ||
-      hipHostMalloc((void**)&ctx->h_count, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-      hipMalloc((void**)&ctx->d_misc, 8 * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) != hipSuccess) {
-    delete ctx;
-    return IZPI_ERR_HIP;
-  }
-  for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++)
-    if (hipEventCreate(&ctx->evb[i]) != hipSuccess || hipEventCreate(&ctx->evb2[i]) != hipSuccess) { delete ctx; return IZPI_ERR_HIP; }
-  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&ctx->evj) != hipSuccess ||
-      hipHostMalloc((void**)&ctx->h_count2, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-      hipMalloc((void**)&ctx->d_misc2, 8 * sizeof(uint32_t)) != hipSuccess) {
-    delete ctx;
+  bool ok = hipGetDeviceProperties(&prop, device) == hipSuccess;
+  ctx->num_cus = ok ? prop.multiProcessorCount : 0;
+  ok = ok && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
+       hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess &&
+       hipEventCreate(&ctx->ev2) == hipSuccess && hipEventCreate(&ctx->ev3) == hipSuccess &&
+       hipHostMalloc((void**)&ctx->h_count, 8 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+       hipMalloc((void**)&ctx->d_misc, 8 * sizeof(uint32_t)) == hipSuccess &&
+       hipMalloc((void**)&ctx->d_pool_ctr, POOL_SHARDS * POOL_CTR_STRIDE * sizeof(unsigned long long)) == hipSuccess &&
+       hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) == hipSuccess;
+  for (int i = 0; ok && i < 3 * IZPI_PASS_BATCH; i++) ok = hipEventCreate(&ctx->evb[i]) == hipSuccess;
+  if (!ok) {
+    izpi_gpu_close(ctx);
     return IZPI_ERR_HIP;
   }
   *out = ctx;
@@ -2435,22 +2439,18 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
 int izpi_gpu_close(izpi_ctx* ctx) {
   if (!ctx) return IZPI_OK;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   free_scene(ctx);
-  void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_running, ctx->d_out, ctx->d_tiles, ctx->d_bg, ctx->d_misc,
-                  ctx->d_counters, ctx->d_rhot, ctx->d_raux, ctx->d_hhot, ctx->d_huv, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post, ctx->d_misc2, ctx->d_spill2};
+  void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_pool, ctx->d_ring, ctx->d_pool_ctr, ctx->d_running, ctx->d_out,
+                  ctx->d_tiles, ctx->d_utiles, ctx->d_bg, ctx->d_misc, ctx->d_counters, ctx->d_rhot, ctx->d_raux,
+                  ctx->d_hit, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post, ctx->d_share,
+                  ctx->d_gather};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
-  if (ctx->h_count2) (void)hipHostFree(ctx->h_count2);
-  for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb2[i]) (void)hipEventDestroy(ctx->evb2[i]);
-  if (ctx->evj) (void)hipEventDestroy(ctx->evj);
-  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-  if (ctx->ev3) (void)hipEventDestroy(ctx->ev3);
   for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb[i]) (void)hipEventDestroy(ctx->evb[i]);
-  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
-  if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
+  hipEvent_t evs[] = {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3};
+  for (hipEvent_t ev : evs) if (ev) (void)hipEventDestroy(ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return IZPI_OK;
@@ -2807,30 +2807,29 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (!ctx->have_scene) { ctx->err = "no scene"; return IZPI_ERR_NO_SCENE; }
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
-  double* dr; izpi_hit* dh; RayHot* rr; RayAux* rx; HitHot* hh; HitUV* hu; uint32_t* q;
+  double* dr; izpi_hit* dh; RayHot* rr; RayAux* rx; HitSt* hh; uint32_t* q;
   HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 8 * sizeof(double)));
   HIP_TRY(hipMalloc((void**)&dh, (size_t)n * sizeof(izpi_hit)));
   HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayHot)));
   HIP_TRY(hipMalloc((void**)&rx, (size_t)n * sizeof(RayAux)));
-  HIP_TRY(hipMalloc((void**)&hh, (size_t)n * sizeof(HitHot)));
-  HIP_TRY(hipMalloc((void**)&hu, (size_t)n * sizeof(HitUV)));
+  HIP_TRY(hipMalloc((void**)&hh, (size_t)n * sizeof(HitSt)));
   HIP_TRY(hipMalloc((void**)&q, (size_t)n * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, rx, q, ctx->d_misc + 3);
   WaveParams wp{};
-  wp.rhot = rr; wp.raux = rx; wp.hhot = hh; wp.huv = hu; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
+  wp.rhot = rr; wp.raux = rx; wp.hit = hh; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
   launch_trace(ctx, tr, wp, ctx->stream, ctx->d_spill);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, hu, n, dh);
+  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, n, dh);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));
-  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(rx); (void)hipFree(hh); (void)hipFree(hu); (void)hipFree(q);
+  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(rx); (void)hipFree(hh); (void)hipFree(q);
   return IZPI_OK;
 }
 
@@ -2870,6 +2869,172 @@ int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uin
   HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
   (void)hipFree(dx); (void)hipFree(dout);
   if (dy) (void)hipFree(dy);
+  return IZPI_OK;
+}
+
+// ------------------------------------------------- multi-GPU, one process
+int izpi_gpu_multi_open(const int* devices, uint32_t num_devices, izpi_multi** out) {
+  if (!out) return IZPI_ERR_INVALID;
+  *out = nullptr;
+  if (!devices || num_devices == 0) return IZPI_ERR_INVALID;
+  izpi_multi* m = new izpi_multi();
+  for (uint32_t i = 0; i < num_devices; i++) {
+    izpi_ctx* c = nullptr;
+    const int rc = izpi_gpu_open(devices[i], &c);
+    if (rc) {
+      izpi_gpu_multi_close(m);
+      return rc;
+    }
+    m->ctx.push_back(c);
+  }
+  // device 0 receives every share: let it read/write peers directly over xGMI
+  for (uint32_t i = 1; i < num_devices; i++) {
+    if (devices[i] == devices[0]) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, devices[i], devices[0]) == hipSuccess && can) {
+      (void)hipSetDevice(devices[i]);
+      (void)hipDeviceEnablePeerAccess(devices[0], 0);  // "already enabled" is fine
+      (void)hipGetLastError();
+    }
+  }
+  *out = m;
+  return IZPI_OK;
+}
+
+int izpi_gpu_multi_close(izpi_multi* m) {
+  if (!m) return IZPI_OK;
+  for (izpi_ctx* c : m->ctx) izpi_gpu_close(c);
+  delete m;
+  return IZPI_OK;
+}
+
+const char* izpi_gpu_multi_last_error(izpi_multi* m) { return m ? m->err.c_str() : "null context"; }
+
+uint32_t izpi_gpu_multi_size(izpi_multi* m) { return m ? (uint32_t)m->ctx.size() : 0u; }
+
+izpi_ctx* izpi_gpu_multi_context(izpi_multi* m, uint32_t i) { return (m && i < m->ctx.size()) ? m->ctx[i] : nullptr; }
+
+int izpi_gpu_multi_upload_scene(izpi_multi* m, const izpi_scene_desc* scene) {
+  if (!m) return IZPI_ERR_INVALID;
+  for (size_t i = 0; i < m->ctx.size(); i++) {  // the scene is replicated per GPU
+    const int rc = izpi_gpu_upload_scene(m->ctx[i], scene);
+    if (rc) {
+      m->err = "device " + std::to_string(i) + ": " + m->ctx[i]->err;
+      return rc;
+    }
+  }
+  return IZPI_OK;
+}
+
+int izpi_gpu_multi_render(izpi_multi* m, const izpi_render_req* req, double* out_host, izpi_render_stats* stats) {
+  if (!m || m->ctx.empty()) return IZPI_ERR_INVALID;
+  const uint32_t G = (uint32_t)m->ctx.size();
+  izpi_ctx* root = m->ctx[0];
+  Shares sh;
+  int rc = make_shares(root, req, G, sh);
+  if (rc) { m->err = root->err; return rc; }
+  if (req->post != IZPI_POST_NONE && req->num_tiles != 0) {
+    m->err = "post-processing needs a whole-frame request";
+    return IZPI_ERR_INVALID;
+  }
+  const size_t canvas_bytes = (size_t)req->width * req->height * 4 * sizeof(double);
+  if (hipSetDevice(root->device) != hipSuccess) { m->err = "hipSetDevice"; return IZPI_ERR_HIP; }
+  if ((rc = grow(root, (void**)&root->d_gather, &root->gather_cap, (size_t)G * sh.block * sizeof(double))) ||
+      (rc = grow(root, (void**)&root->d_out, &root->out_cap, canvas_bytes))) {
+    m->err = root->err;
+    return rc;
+  }
+  // the caller's canvas is the starting point (pixels of no tile keep their values)
+  if (out_host) {
+    if (hipMemcpy(root->d_out, out_host, canvas_bytes, hipMemcpyHostToDevice) != hipSuccess) { m->err = "hipMemcpy"; return IZPI_ERR_HIP; }
+  } else if (hipMemset(root->d_out, 0, canvas_bytes) != hipSuccess) {
+    m->err = "hipMemset";
+    return IZPI_ERR_HIP;
+  }
+  // one host thread per device: render its share, then copy it into block i of the
+  // root's gather buffer (peer copy over xGMI; a plain device copy for the root)
+  std::vector<int> rcs(G, IZPI_OK);
+  std::vector<std::thread> th;
+  for (uint32_t i = 0; i < G; i++) {
+    th.emplace_back([&, i]() {
+      izpi_ctx* c = m->ctx[i];
+      if (hipSetDevice(c->device) != hipSuccess) { rcs[i] = IZPI_ERR_HIP; c->err = "hipSetDevice"; return; }
+      int r = render_share(c, req, sh, i);
+      if (!r) {
+        hipError_t e = hipMemcpyPeerAsync(root->d_gather + (size_t)i * sh.block, root->device, c->d_share, c->device,
+                                          sh.block * sizeof(double), c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) { c->err = std::string("gather copy: ") + hipGetErrorString(e); r = IZPI_ERR_HIP; }
+      }
+      rcs[i] = r;
+    });
+  }
+  for (std::thread& t : th) t.join();
+  for (uint32_t i = 0; i < G; i++) {
+    if (stats) stats[i] = m->ctx[i]->last;
+    if (rcs[i]) {
+      m->err = "device " + std::to_string(i) + ": " + m->ctx[i]->err;
+      return rcs[i];
+    }
+  }
+  if (hipSetDevice(root->device) != hipSuccess) { m->err = "hipSetDevice"; return IZPI_ERR_HIP; }
+  if ((rc = assemble(root, req, sh, root->d_out))) { m->err = root->err; return rc; }
+  if (out_host && hipMemcpy(out_host, root->d_out, canvas_bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+    m->err = "hipMemcpy";
+    return IZPI_ERR_HIP;
+  }
+  return IZPI_OK;
+}
+
+// ------------------------------------------ multi-GPU, one process per GPU
+int izpi_gpu_comm_id(uint8_t* id) {
+  if (!id) return IZPI_ERR_INVALID;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return IZPI_ERR_HIP;
+  memcpy(id, u.internal, IZPI_COMM_ID_BYTES);
+  return IZPI_OK;
+}
+
+int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint8_t* id) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  if (!id || nranks == 0 || rank >= nranks) { ctx->err = "comm_init: bad arguments"; return IZPI_ERR_INVALID; }
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+  ncclUniqueId u;
+  memcpy(u.internal, id, IZPI_COMM_ID_BYTES);
+  const ncclResult_t r = ncclCommInitRank(&ctx->comm, (int)nranks, u, (int)rank);
+  if (r != ncclSuccess) {
+    ctx->comm = nullptr;
+    ctx->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+    return IZPI_ERR_HIP;
+  }
+  ctx->comm_rank = rank;
+  ctx->comm_size = nranks;
+  return IZPI_OK;
+}
+
+int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  if (!ctx->comm) { ctx->err = "render_rank before izpi_gpu_comm_init"; return IZPI_ERR_INVALID; }
+  if (ctx->comm_rank == 0 && !out_dev) { ctx->err = "rank 0 needs an output canvas"; return IZPI_ERR_INVALID; }
+  if (req && req->post != IZPI_POST_NONE && req->num_tiles != 0) { ctx->err = "post-processing needs a whole-frame request"; return IZPI_ERR_INVALID; }
+  HIP_TRY(hipSetDevice(ctx->device));
+  Shares sh;
+  int rc = make_shares(ctx, req, ctx->comm_size, sh);
+  if (rc) return rc;
+  // a failed share still joins the gather (the other ranks wait in it), then reports
+  const int rrc = render_share(ctx, req, sh, ctx->comm_rank);
+  if (!ctx->d_share || ctx->share_cap < sh.block * sizeof(double)) return rrc ? rrc : IZPI_ERR_HIP;
+  if (stats) *stats = ctx->last;
+  if (ctx->comm_rank == 0 &&
+      (rc = grow(ctx, (void**)&ctx->d_gather, &ctx->gather_cap, (size_t)ctx->comm_size * sh.block * sizeof(double)))) return rc;
+  // ncclGather (rccl.h:745): block r of the root's buffer = rank r's packed share
+  const ncclResult_t r = ncclGather(ctx->d_share, ctx->comm_rank == 0 ? ctx->d_gather : nullptr, sh.block, ncclFloat64, 0,
+                                    ctx->comm, ctx->stream);
+  if (r != ncclSuccess) { ctx->err = std::string("ncclGather: ") + ncclGetErrorString(r); return IZPI_ERR_HIP; }
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (rrc) return rrc;
+  if (ctx->comm_rank == 0 && (rc = assemble(ctx, req, sh, out_dev))) return rc;
   return IZPI_OK;
 }
 

@@ -6,11 +6,16 @@ float64 NRGBA canvas (H, W, 4) the Go renderer fills — RGB for the Colour samp
 before post-processing for the Spectral sampler (``.render_spectral_rgb()`` applies
 FireflyRejection + XYZToRGB on the GPU like renderer.go:216-219).
 
-Multi-GPU (one process per GPU, torch.distributed over RCCL): tiles are dealt
-round-robin (tile_id % world == rank), each rank renders its tiles into a packed
-device buffer, and one ``gather`` moves them to rank 0, which scatters them into the
-canvas on its GPU (izpi_gpu_unpack_tiles). Per pixel-sample RNG streams make the image
-independent of the partition.
+Multi-GPU goes through the library (include/izpi_gpu.h): tiles are dealt round-robin
+(tile_id % G == i), each device renders its tiles into a packed buffer, and the shares
+are gathered to device 0, which scatters them into the canvas. Two forms:
+
+* ``MultiGPURenderer`` — one process drives every GPU (izpi_gpu_multi_*): one host
+  thread and stream per device, xGMI peer copies to device 0;
+* ``GPURenderer.render_rank`` — one process per GPU (torchrun): the library's own RCCL
+  communicator (izpi_gpu_comm_init) and one ncclGather to rank 0.
+
+Per pixel-sample RNG streams make the image independent of the partition.
 """
 import ctypes as C
 import os
@@ -30,6 +35,52 @@ def _check(rc, ctx, what):
     if rc != 0:
         msg = N.lib().izpi_gpu_last_error(ctx).decode() if ctx else ""
         raise RuntimeError("%s failed (status %d): %s" % (what, rc, msg))
+
+
+def build_bvh4(ctx, boxes, leaf_max=4, method=None):
+    """izpi_gpu_build_bvh4 on context `ctx` over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
+    if method is None:  # IZPI_BVH_METHOD=lbvh|ploc overrides the default (experiments)
+        method = {"lbvh": N.BVH_LBVH, "ploc": N.BVH_PLOC}.get(os.environ.get("IZPI_BVH_METHOD", ""), GPU_BVH_METHOD)
+    boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
+    n = len(boxes)
+    nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
+    order = np.zeros(max(1, n), np.uint32)
+    m = C.c_uint32()
+    ms = C.c_double()
+    _check(N.lib().izpi_gpu_build_bvh4(ctx, boxes.ctypes.data_as(N.c_double_p), n, leaf_max, method,
+                                        nodes.ctypes.data_as(C.POINTER(N.BVH4Node)), len(nodes), C.byref(m),
+                                        order.ctypes.data_as(N.c_uint32_p), C.byref(ms)),
+           ctx, "izpi_gpu_build_bvh4")
+    return nodes[:m.value].copy(), order[:n].copy(), ms.value
+
+
+def make_request(width, height, spp, max_depth, sampler, background, seed, exposure, bg_spd=None, tiles=None,
+                 layout=N.OUT_CANVAS, post=N.POST_NONE):
+    """izpi_render_req for Render (the arrays it points to are kept alive on `req._keep`)."""
+    req = N.RenderReq()
+    req.post = post
+    req.exposure = exposure
+    req.width, req.height = width, height
+    req.spp = spp
+    req.max_depth = max_depth
+    req.sampler = sampler
+    req.out_layout = layout
+    req.background[:] = background
+    req.seed = seed
+    keep = []
+    if tiles is not None:
+        t = np.ascontiguousarray(tiles, np.uint32).reshape(-1, 4)
+        keep.append(t)
+        req.num_tiles = len(t)
+        req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
+    if bg_spd is not None and len(bg_spd[0]):
+        wl, val = bg_spd
+        keep += [wl, val]
+        req.num_bg_spd = wl.size
+        req.bg_spd_wavelengths = wl.ctypes.data_as(C.POINTER(C.c_double))
+        req.bg_spd_values = val.ctypes.data_as(C.POINTER(C.c_double))
+    req._keep = keep
+    return req
 
 
 def common_tiles(width, height):
@@ -81,44 +132,13 @@ class GPURenderer:
 
     def build_bvh4(self, boxes, leaf_max=4, method=None):
         """izpi_gpu_build_bvh4 over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
-        if method is None:  # IZPI_BVH_METHOD=lbvh|ploc overrides the default (experiments)
-            method = {"lbvh": N.BVH_LBVH, "ploc": N.BVH_PLOC}.get(os.environ.get("IZPI_BVH_METHOD", ""), GPU_BVH_METHOD)
-        boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
-        n = len(boxes)
-        nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
-        order = np.zeros(max(1, n), np.uint32)
-        m = C.c_uint32()
-        ms = C.c_double()
-        _check(N.lib().izpi_gpu_build_bvh4(self.ctx, boxes.ctypes.data_as(N.c_double_p), n, leaf_max, method,
-                                            nodes.ctypes.data_as(C.POINTER(N.BVH4Node)), len(nodes), C.byref(m),
-                                            order.ctypes.data_as(N.c_uint32_p), C.byref(ms)),
-               self.ctx, "izpi_gpu_build_bvh4")
-        return nodes[:m.value].copy(), order[:n].copy(), ms.value
+        return build_bvh4(self.ctx, boxes, leaf_max, method)
 
     # -------------------------------------------------------------- request
     def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None, post=N.POST_NONE):
-        req = N.RenderReq()
-        req.post = post
-        req.exposure = self.exposure
-        req.width, req.height = self.width, self.height
-        req.spp = self.spp if spp is None else int(spp)
-        req.max_depth = self.max_depth
-        req.sampler = self.sampler
-        req.out_layout = layout
-        req.background[:] = self.background
-        req.seed = self.seed
-        keep = []
-        if tiles is not None:
-            t = np.ascontiguousarray(tiles, np.uint32).reshape(-1, 4)
-            keep.append(t)
-            req.num_tiles = len(t)
-            req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
-        if self._bg_wl.size:
-            req.num_bg_spd = self._bg_wl.size
-            req.bg_spd_wavelengths = self._bg_wl.ctypes.data_as(C.POINTER(C.c_double))
-            req.bg_spd_values = self._bg_val.ctypes.data_as(C.POINTER(C.c_double))
-        req._keep = keep
-        return req
+        return make_request(self.width, self.height, self.spp if spp is None else int(spp), self.max_depth,
+                            self.sampler, self.background, self.seed, self.exposure, (self._bg_wl, self._bg_val),
+                            tiles, layout, post)
 
     # --------------------------------------------------------------- render
     @property
@@ -159,9 +179,9 @@ class GPURenderer:
                                             k.ctypes.data_as(N.c_uint32_p), p.ctypes.data_as(N.c_double_p), len(k)),
                self.ctx, "izpi_gpu_postprocess")
 
-    def render_device(self, out_ptr, tiles=None, layout=N.OUT_CANVAS, spp=None):
+    def render_device(self, out_ptr, tiles=None, layout=N.OUT_CANVAS, spp=None, post=N.POST_NONE):
         """Render into device memory at `out_ptr` (e.g. torch tensor .data_ptr())."""
-        req = self.request(tiles, layout, spp)
+        req = self.request(tiles, layout, spp, post)
         st = N.RenderStats()
         rc = N.lib().izpi_gpu_render_device(self.ctx, C.byref(req), C.c_void_p(out_ptr), C.byref(st))
         _check(rc, self.ctx, "izpi_gpu_render_device")
@@ -178,41 +198,111 @@ class GPURenderer:
                self.ctx, "izpi_gpu_unpack_tiles")
 
     # ------------------------------------------------------------ multi-GPU
-    def render_distributed(self, rank, world, group=None, tiles=None, post=N.POST_NONE):
-        """Tile-sharded render over `world` ranks; returns the canvas as a torch tensor
-        on rank 0 (None elsewhere) and this rank's stats. One RCCL gather. With
-        post=POST_SPECTRAL rank 0 applies FireflyRejection + XYZToRGB after the gather."""
+    def comm_init(self, world, rank, comm_id):
+        """Join the library's RCCL communicator (one process per GPU); comm_id is rank 0's
+        izpi_gpu_comm_id bytes, broadcast by the launcher."""
+        cid = (C.c_uint8 * N.COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
+        _check(N.lib().izpi_gpu_comm_init(self.ctx, world, rank, cid), self.ctx, "izpi_gpu_comm_init")
+
+    def render_rank(self, out_ptr=None, post=N.POST_NONE, tiles=None):
+        """Collective Render over the communicator: this rank's share of the frame, one
+        ncclGather, and on rank 0 the assembled canvas written to device memory at
+        `out_ptr` (post-processed). Returns this rank's stats."""
+        req = self.request(tiles, N.OUT_CANVAS, None, post)
+        st = N.RenderStats()
+        rc = N.lib().izpi_gpu_render_rank(self.ctx, C.byref(req), C.c_void_p(out_ptr or 0), C.byref(st))
+        _check(rc, self.ctx, "izpi_gpu_render_rank")
+        self.stats = st.as_dict()
+        return self.stats
+
+    def render_distributed(self, rank, world, post=N.POST_NONE):
+        """render_rank into a torch canvas on rank 0 (None elsewhere); the communicator
+        must be set up (comm_init) when world > 1. Returns (canvas, stats)."""
         import torch
-        from . import sharding
-        all_tiles = common_tiles(self.width, self.height) if tiles is None else np.asarray(tiles, np.uint32)
-        mine = sharding.shard_tiles(all_tiles, rank, world)
         dev = torch.device("cuda", self.device)
-        packed = torch.zeros(sharding.packed_len(all_tiles, world), dtype=torch.float64, device=dev)
-        self.stats = None
-        if len(mine):
-            self.render_device(packed.data_ptr(), tiles=mine, layout=N.OUT_PACKED)
-        torch.cuda.synchronize(dev)
-        gathered = sharding.gather_packed(packed, rank, world, group)
-        if rank != 0:
-            return None, self.stats
-        canvas = torch.zeros((self.height, self.width, 4), dtype=torch.float64, device=dev)
-        for r in range(world):
-            rt = sharding.shard_tiles(all_tiles, r, world)
-            if len(rt):
-                self.unpack(rt, gathered[r].data_ptr(), canvas.data_ptr())
-        if post & N.POST_SPECTRAL:
-            rgb = torch.empty_like(canvas)
-            self.spectral_post(canvas.data_ptr(), rgb.data_ptr())
-            canvas = rgb
-        if post & N.POST_GAMMA_CLAMP:  # leader.go:179-182
-            self.postprocess(canvas.data_ptr(), [(N.FILTER_GAMMA, 0.0), (N.FILTER_CLAMP, 1.0)])
-        torch.cuda.synchronize(dev)
-        return canvas, self.stats
+        canvas = torch.zeros((self.height, self.width, 4), dtype=torch.float64, device=dev) if rank == 0 else None
+        if world == 1:
+            st = self.render_device(canvas.data_ptr(), post=post)
+        else:
+            st = self.render_rank(canvas.data_ptr() if canvas is not None else None, post)
+        return canvas, st
 
     def close(self):
         if getattr(self, "ctx", None):
             N.lib().izpi_gpu_close(self.ctx)
             self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiGPURenderer:
+    """Render over several GPUs from one process (izpi_gpu_multi_*): the scene is
+    replicated on every device, the frame's tiles are dealt tile % G, device 0 gathers
+    and assembles the canvas. Same arguments as GPURenderer plus ``devices``."""
+
+    def __init__(self, scene, width, height, spp, devices, max_depth=50, sampler=N.SAMPLER_COLOUR,
+                 background=(0.0, 0.0, 0.0), spectral_background=None, seed=12345, bvh_seed=12345, bvh="gpu",
+                 bvh_leaf_max=None):
+        if bvh not in ("reference", "gpu"):
+            raise ValueError("bvh must be 'reference' or 'gpu'")
+        self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
+        self.sampler = int(sampler)
+        self.background = tuple(float(b) for b in background)
+        self.seed = int(seed)
+        self.devices = [int(d) for d in devices]
+        if spectral_background is None:
+            self._bg = (np.zeros(0), np.zeros(0))
+        else:
+            self._bg = tuple(np.ascontiguousarray(x, np.float64) for x in spectral_background)
+        self.host = HostScene(scene, aspect_override=float(width) / float(height), bvh_seed=bvh_seed,
+                              skip_bvh=bvh == "gpu")
+        L = N.lib()
+        m = C.c_void_p()
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        rc = L.izpi_gpu_multi_open(devs, len(self.devices), C.byref(m))
+        if rc != 0:
+            raise RuntimeError("izpi_gpu_multi_open(%s) failed (status %d)" % (self.devices, rc))
+        self.m = m
+        self.bvh_build_ms = None
+        if bvh == "gpu":
+            nodes, order, self.bvh_build_ms = build_bvh4(L.izpi_gpu_multi_context(m, 0), self.host.prim_boxes(),
+                                                         bvh_leaf_max or GPU_BVH_LEAF_MAX)
+            self.host.set_bvh(nodes, order)
+        self._check(L.izpi_gpu_multi_upload_scene(m, C.byref(self.host.desc)), "izpi_gpu_multi_upload_scene")
+        self.stats = None
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = N.lib().izpi_gpu_multi_last_error(self.m).decode()
+            raise RuntimeError("%s failed (status %d): %s" % (what, rc, msg))
+
+    @property
+    def exposure(self):
+        return float(self.host.desc.camera.exposure)
+
+    def render(self, canvas=None, post=N.POST_NONE, to_host=True):
+        """Render.Render over all devices. Returns the (H, W, 4) canvas (host), or None with
+        to_host=False (the canvas stays on device 0: the timing form). self.stats is the
+        list of per-device stats."""
+        req = make_request(self.width, self.height, self.spp, self.max_depth, self.sampler, self.background,
+                           self.seed, self.exposure, self._bg, None, N.OUT_CANVAS, post)
+        G = len(self.devices)
+        st = (N.RenderStats * G)()
+        if to_host and canvas is None:
+            canvas = np.zeros((self.height, self.width, 4), np.float64)
+        ptr = canvas.ctypes.data_as(C.c_void_p) if to_host else None
+        self._check(N.lib().izpi_gpu_multi_render(self.m, C.byref(req), ptr, st), "izpi_gpu_multi_render")
+        self.stats = [st[i].as_dict() for i in range(G)]
+        return canvas if to_host else None
+
+    def close(self):
+        if getattr(self, "m", None):
+            N.lib().izpi_gpu_multi_close(self.m)
+            self.m = None
 
     def __del__(self):
         try:

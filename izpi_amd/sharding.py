@@ -15,7 +15,16 @@ import numpy as np
 
 
 def shard_tiles(all_tiles, rank, world):
-    return np.ascontiguousarray(np.asarray(all_tiles, np.uint32)[rank::world])
+    """Tiles of share `rank` of `world`: the library's own rule (izpi_host_share_tiles),
+    the one izpi_gpu_multi_render and izpi_gpu_render_rank deal the frame with."""
+    import ctypes as C
+    from . import _native as N
+    t = np.ascontiguousarray(np.asarray(all_tiles, np.uint32).reshape(-1, 4))
+    out = np.zeros_like(t)
+    n = N.lib().izpi_host_share_tiles(t.ctypes.data_as(N.c_uint32_p), len(t), rank, world,
+                                      out.ctypes.data_as(N.c_uint32_p))
+    assert n == len(range(rank, len(t), world))
+    return np.ascontiguousarray(out[:n])
 
 
 def tile_pixels(tiles):

@@ -200,24 +200,44 @@ def test_tiles_packed_and_unpack(gpu):
     r.close()
 
 
-@pytest.mark.parametrize("env", [{"IZPI_TRACE": "1"}, {"IZPI_TRACE_RING": "8", "IZPI_TRACE_WPE": "4"},
-                                 {"IZPI_TRACE_RING": "32", "IZPI_TRACE_WPE": "4"}, {"IZPI_PRIM_W": "1"},
+@pytest.mark.parametrize("env", [{"IZPI_PRIM_W": "1"},
                                  {"IZPI_PRIM_W": "100000"}, {"IZPI_SLOTS": "3000", "IZPI_CHUNK_UNITS": "5000"},
                                  {"IZPI_NO_LEAF_SHORTCUT": "1"}, {"IZPI_TRACE_CHUNK": "1", "IZPI_REFILL_MIN": "1"},
-                                 {"IZPI_TRACE_RING": "8", "IZPI_TRACE_WPE": "5"},
-                                 {"IZPI_TRACE_DIST": "0"}, {"IZPI_TRACE_DIST": "1", "IZPI_TRACE_WPE": "4"},
+                                 {"IZPI_TRACE_DIST": "0"},
                                  {"IZPI_TAIL": "0"}, {"IZPI_TAIL": "0", "IZPI_SLOTS": "3000"},
-                                 {"IZPI_TRACE_NO_TRI": "1"}])
+                                 {"IZPI_TRACE_NO_TRI": "1"},
+                                 {"IZPI_REC_DENSE": "1", "IZPI_POOL_DIV": "100000"},
+                                 {"IZPI_REC_DENSE": "2", "IZPI_POOL_DIV": "100000", "IZPI_TAIL": "0"},
+                                 {"IZPI_REC_DENSE": "50"}])
 def test_kernel_variants_bitwise(gpu, env, monkeypatch):
-    """Traversal kernel variants, the LDS-ring spill path, step weights, tiny
-    slot/chunk counts, the sphere-capable instance and the pass loop without the k_tail
-    finish are launch knobs only: results and counters must not move."""
+    """Traversal step weights, tiny slot/chunk counts, the sequential-leaf and
+    sphere-capable instances, the pass loop without the k_tail finish, and the unwinding
+    records' split (dense levels + overflow blocks: a 4096-block pool far below the demand
+    parks slots, all-dense needs no pool) are launch knobs only: results and counters
+    must not move."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     scene = configs.cornell_dragon(1.0, n=60)
     r = GPURenderer(scene, 64, 64, 4)
     img = r.render()
     ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    if env.get("IZPI_POOL_DIV") == "100000":
+        assert r.stats["pool_blocks"] == 4096 and r.stats["parks"] > 0, r.stats  # the park path ran
+    r.close()
+
+
+@pytest.mark.parametrize("env", [{"IZPI_REC_DENSE": "1", "IZPI_POOL_DIV": "100000"},
+                                 {"IZPI_REC_DENSE": "3", "IZPI_POOL_DIV": "100000", "IZPI_TAIL": "0"}])
+def test_record_pool_spectral_glass_bitwise(gpu, env, monkeypatch):
+    """Overflow records under the spectral sampler with dielectrics: path-length rays,
+    parked slots and 32-B records."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scene = configs.cornell_glass_spectral()
+    r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_SPECTRAL)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
 
@@ -454,15 +474,53 @@ def test_render_on_gpu_built_bvh_bitwise(gpu, which):
     r.close()
 
 
-def test_two_wavefront_lanes_bitwise(gpu, monkeypatch):
-    """IZPI_LANES=2: slots, queues and records split in two lanes on two streams sharing
-    the unit head; the image and counters are the same."""
-    monkeypatch.setenv("IZPI_LANES", "2")
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_gpu_render_bitwise(gpu, devices):
+    """izpi_gpu_multi_render (one call, one context per device, shares gathered to device
+    0) == the oracle, for 1-3 contexts (several contexts on this box's one GPU exercise
+    the share dealing, the padded gather and the assembly)."""
+    from izpi_amd.renderer import MultiGPURenderer
     scene = configs.cornell_dragon(1.0, n=40)
-    r = GPURenderer(scene, 64, 64, 16)
+    r = MultiGPURenderer(scene, 64, 64, 4, devices, bvh="reference")
     img = r.render()
-    ref, ostats = oracle_canvas(scene, 64, 64, 16, N.SAMPLER_COLOUR)
-    assert_parity(img, ref, r.stats, ostats)
+    ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(img, ref)
+    for k in ("rays", "node_visits", "tri_tests", "light_tri_tests", "samples"):
+        assert sum(st[k] for st in r.stats) == ostats[k], k
+    assert len(r.stats) == len(devices)
+    r.close()
+
+
+def test_multi_gpu_spectral_post_bitwise(gpu):
+    """Render's spectral post (FireflyRejection + XYZToRGB) runs on the ASSEMBLED frame:
+    two shares must give the single-device canvas, including the firefly halo across
+    share boundaries."""
+    from izpi_amd.renderer import MultiGPURenderer
+    scene = configs.cornell_glass_spectral()
+    one = GPURenderer(scene, 64, 64, 4, sampler=N.SAMPLER_SPECTRAL, bvh="gpu")
+    want = one.render(post=N.POST_SPECTRAL | N.POST_GAMMA_CLAMP)
+    one.close()
+    r = MultiGPURenderer(scene, 64, 64, 4, [0, 0], sampler=N.SAMPLER_SPECTRAL, bvh="gpu")
+    got = r.render(post=N.POST_SPECTRAL | N.POST_GAMMA_CLAMP)
+    r.close()
+    assert got.tobytes() == want.tobytes()
+
+
+def test_render_rank_rccl_world1_bitwise(gpu):
+    """The one-process-per-GPU form through the library's RCCL communicator (comm id,
+    ncclCommInitRank, ncclGather to rank 0) at world size 1 == the oracle."""
+    import ctypes as C
+    import torch
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 64, 64, 4)
+    cid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    assert N.lib().izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    canvas = torch.zeros((64, 64, 4), dtype=torch.float64, device="cuda:0")
+    r.render_rank(canvas.data_ptr())
+    torch.cuda.synchronize()
+    ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(canvas.cpu().numpy(), ref, r.stats, ostats)
     r.close()
 
 
