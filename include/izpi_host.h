@@ -128,6 +128,11 @@ typedef struct izpi_proto_info {
 
 int izpi_scene_parse_text(const char* text, uint64_t len, izpi_proto_scene** out);
 int izpi_scene_parse_binary(const void* buf, uint64_t len, izpi_proto_scene** out);
+/* The parsed scene as transport.Scene wire bytes, as proto.Marshal writes them (fields in
+ * number order, repeated scalars packed, proto3 zero scalars omitted): the .izpi form of
+ * a .pbtxt. Writes min(cap, size) bytes to buf (may be NULL with cap 0) and the size to
+ * *len. Streamed triangles (izpi_scene_add_triangles) are not part of the message. */
+int izpi_scene_serialize(const izpi_proto_scene* s, void* buf, uint64_t cap, uint64_t* len);
 int izpi_scene_info(const izpi_proto_scene* s, izpi_proto_info* out);
 /* Filenames of Scene.image_textures, which the host decodes (leader.go:84-98)... */
 const char* izpi_scene_image_file(const izpi_proto_scene* s, uint32_t i);

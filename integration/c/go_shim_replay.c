@@ -1,0 +1,124 @@
+/* go_shim_replay.c — the C call sequence of integration/go/render/gpu/renderer_gpu.go,
+ * step for step, so that it runs (and is tested) where no Go toolchain exists.
+ *
+ *   gpu.New (renderer_gpu.go:90-213) and Renderer.Render (:216-235):
+ *   1. proto.Marshal(scene) -> izpi_scene_parse_binary   (here: a .izpi file = those bytes)
+ *   2. izpi_scene_set_image per loaded image texture      (here: none / a flat test texture)
+ *   3. izpi_scene_to_input(aspect = W/H, bvh seed 12345) -> izpi_host_build_scene_ex(SKIP_BVH)
+ *   4. izpi_gpu_open / izpi_gpu_multi_open (Options.Devices), izpi_host_scene_prim_boxes,
+ *      izpi_gpu_build_bvh4(leaf 3, PLOC) -> izpi_host_scene_set_bvh
+ *   5. izpi_gpu_upload_scene / izpi_gpu_multi_upload_scene, the whole-frame request:
+ *      sampler from the scene's colour representation, IZPI_POST_SPECTRAL for the
+ *      spectral sampler, IZPI_POST_GAMMA_CLAMP with --png-pipeline, exposure = camera's
+ *   6. Render: izpi_gpu_render / izpi_gpu_multi_render into a zeroed W*H*4 float64 canvas
+ *
+ *   usage: go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices 0,0,...]
+ * Exit status 0 on success; the canvas is written as raw little-endian float64.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "izpi_gpu.h"
+#include "izpi_host.h"
+
+static int fail(const char* what, const char* msg) {
+  fprintf(stderr, "%s: %s\n", what, msg ? msg : "");
+  return 1;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 6) return fail("usage", "go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices a,b,..]");
+  const uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]), spp = (uint32_t)atoi(argv[4]);
+  int png = 0, devices[16], ndev = 0;
+  for (int i = 6; i < argc; i++) {
+    if (!strcmp(argv[i], "--png-pipeline")) png = 1;
+    else if (!strcmp(argv[i], "--devices") && i + 1 < argc) {
+      for (char* t = strtok(argv[++i], ","); t && ndev < 16; t = strtok(NULL, ",")) devices[ndev++] = atoi(t);
+    }
+  }
+  /* 1. the marshalled transport.Scene */
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return fail("open", argv[1]);
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t* buf = (uint8_t*)malloc(n > 0 ? (size_t)n : 1);
+  if (fread(buf, 1, (size_t)n, f) != (size_t)n) return fail("read", argv[1]);
+  fclose(f);
+  izpi_proto_scene* ps = NULL;
+  if (izpi_scene_parse_binary(buf, (uint64_t)n, &ps)) return fail("izpi_scene_parse_binary", izpi_host_last_error());
+  free(buf);
+  izpi_proto_info info;
+  if (izpi_scene_info(ps, &info)) return fail("izpi_scene_info", izpi_host_last_error());
+  /* 2. image textures: a flat mid-grey 2x2 float64 NRGBA texture per referenced file */
+  for (uint32_t i = 0; i < info.num_image_textures; i++) {
+    const double texels[16] = {0.5, 0.5, 0.5, 1, 0.5, 0.5, 0.5, 1, 0.5, 0.5, 0.5, 1, 0.5, 0.5, 0.5, 1};
+    if (izpi_scene_set_image(ps, izpi_scene_image_file(ps, i), 2, 2, texels))
+      return fail("izpi_scene_set_image", izpi_host_last_error());
+  }
+  /* 3. transport.ToScene up to the BVH, leader-mode aspect override */
+  const izpi_scene_input* in = NULL;
+  if (izpi_scene_to_input(ps, (double)W / (double)H, 12345, &in)) return fail("izpi_scene_to_input", izpi_host_last_error());
+  izpi_host_scene* host = NULL;
+  if (izpi_host_build_scene_ex(in, IZPI_HOST_SKIP_BVH, &host)) return fail("izpi_host_build_scene_ex", izpi_host_last_error());
+  /* 4. device(s), GPU BVH4 */
+  izpi_ctx* ctx = NULL;
+  izpi_multi* m = NULL;
+  if (ndev > 1) {
+    if (izpi_gpu_multi_open(devices, (uint32_t)ndev, &m)) return fail("izpi_gpu_multi_open", "");
+    ctx = izpi_gpu_multi_context(m, 0);
+  } else if (izpi_gpu_open(ndev ? devices[0] : 0, &ctx)) {
+    return fail("izpi_gpu_open", "");
+  }
+  const izpi_scene_desc* desc = izpi_host_scene_desc(host);
+  const uint32_t np = desc->num_tris + desc->num_spheres;
+  if (np > 0) {
+    double* boxes = (double*)malloc(sizeof(double) * 6 * np);
+    izpi_bvh4_node* nodes = (izpi_bvh4_node*)malloc(sizeof(izpi_bvh4_node) * 2 * np);
+    uint32_t* order = (uint32_t*)malloc(sizeof(uint32_t) * np);
+    uint32_t num_nodes = 0;
+    double ms = 0;
+    if (izpi_host_scene_prim_boxes(host, boxes)) return fail("izpi_host_scene_prim_boxes", izpi_host_last_error());
+    if (izpi_gpu_build_bvh4(ctx, boxes, np, 3, IZPI_BVH_PLOC, nodes, 2 * np, &num_nodes, order, &ms))
+      return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
+    if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
+    free(boxes); free(nodes); free(order);
+  }
+  /* 5. upload and the request */
+  desc = izpi_host_scene_desc(host);
+  if (m ? izpi_gpu_multi_upload_scene(m, desc) : izpi_gpu_upload_scene(ctx, desc))
+    return fail("upload", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
+  izpi_render_req req;
+  memset(&req, 0, sizeof req);
+  req.width = W; req.height = H; req.spp = spp; req.max_depth = 50;
+  req.out_layout = IZPI_OUT_CANVAS;
+  req.seed = 12345;
+  req.exposure = desc->camera.exposure;
+  uint32_t post = IZPI_POST_NONE;
+  req.sampler = IZPI_SAMPLER_COLOUR;
+  if (info.colour_representation == IZPI_COLOUR_SPECTRAL) {  /* leader.go:77-81 */
+    req.sampler = IZPI_SAMPLER_SPECTRAL;
+    post |= IZPI_POST_SPECTRAL;
+  }
+  if (png) post |= IZPI_POST_GAMMA_CLAMP;
+  req.post = post;
+  /* 6. Render */
+  double* pix = (double*)calloc((size_t)W * H * 4, sizeof(double));
+  izpi_render_stats st;
+  if (m ? izpi_gpu_multi_render(m, &req, pix, NULL) : izpi_gpu_render(ctx, &req, pix, &st))
+    return fail("render", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
+  FILE* o = fopen(argv[5], "wb");
+  if (!o || fwrite(pix, sizeof(double), (size_t)W * H * 4, o) != (size_t)W * H * 4) return fail("write", argv[5]);
+  fclose(o);
+  free(pix);
+  /* Renderer.Close */
+  if (m) izpi_gpu_multi_close(m);
+  else izpi_gpu_close(ctx);
+  izpi_host_scene_free(host);
+  izpi_scene_free(ps);
+  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u}\n", req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour",
+         ndev > 1 ? ndev : 1, post);
+  return 0;
+}

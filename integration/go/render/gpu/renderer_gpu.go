@@ -61,6 +61,7 @@ type Options struct {
 	SpectralBackground                 []float64     // 75 values at the CIE wavelengths, nil = black
 	SamplerType                        sampler.SamplerType
 	Device                             int
+	Devices                            []int         // >1 entries: one Render fans out over these GPUs (izpi_gpu_multi_*)
 	Seed                               uint64        // master seed of the per-sample LCG streams
 	BVH                                BVH
 	PNGPipeline                        bool          // Gamma + Clamp(1.0) on the GPU (leader.go:179-182)
@@ -68,7 +69,8 @@ type Options struct {
 
 // Renderer renders one frame per Render call on one MI355X.
 type Renderer struct {
-	ctx   *C.izpi_ctx
+	ctx   *C.izpi_ctx   // single device, or device 0's context of m
+	m     *C.izpi_multi // multi-GPU form (Options.Devices), nil otherwise
 	ps    *C.izpi_proto_scene
 	host  *C.izpi_host_scene
 	req   C.izpi_render_req
@@ -81,6 +83,9 @@ type Renderer struct {
 func lastHostError() error { return errors.New(C.GoString(C.izpi_host_last_error())) }
 
 func (r *Renderer) deviceError(what string, rc C.int) error {
+	if r.m != nil && what != "izpi_gpu_build_bvh4" {
+		return fmt.Errorf("%s: status %d: %s", what, int(rc), C.GoString(C.izpi_gpu_multi_last_error(r.m)))
+	}
 	return fmt.Errorf("%s: status %d: %s", what, int(rc), C.GoString(C.izpi_gpu_last_error(r.ctx)))
 }
 
@@ -138,7 +143,17 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 	if rc := C.izpi_host_build_scene_ex(in, flags, &r.host); rc != 0 {
 		return nil, lastHostError()
 	}
-	if rc := C.izpi_gpu_open(C.int(opt.Device), &r.ctx); rc != 0 {
+	if len(opt.Devices) > 1 {
+		// renderer.go:123-147 starts a worker per core; here one host thread per GPU inside the library
+		devs := make([]C.int, len(opt.Devices))
+		for i, d := range opt.Devices {
+			devs[i] = C.int(d)
+		}
+		if rc := C.izpi_gpu_multi_open(&devs[0], C.uint32_t(len(devs)), &r.m); rc != 0 {
+			return nil, fmt.Errorf("izpi_gpu_multi_open(%v): status %d", opt.Devices, int(rc))
+		}
+		r.ctx = C.izpi_gpu_multi_context(r.m, 0) // owned by r.m
+	} else if rc := C.izpi_gpu_open(C.int(opt.Device), &r.ctx); rc != 0 {
 		return nil, fmt.Errorf("izpi_gpu_open(%d): status %d", opt.Device, int(rc))
 	}
 	// 4. optional GPU BVH4 build, then the upload
@@ -161,7 +176,11 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 			}
 		}
 	}
-	if rc := C.izpi_gpu_upload_scene(r.ctx, C.izpi_host_scene_desc(r.host)); rc != 0 {
+	if r.m != nil {
+		if rc := C.izpi_gpu_multi_upload_scene(r.m, C.izpi_host_scene_desc(r.host)); rc != 0 {
+			return nil, r.deviceError("izpi_gpu_multi_upload_scene", rc)
+		}
+	} else if rc := C.izpi_gpu_upload_scene(r.ctx, C.izpi_host_scene_desc(r.host)); rc != 0 {
 		return nil, r.deviceError("izpi_gpu_upload_scene", rc)
 	}
 	// 5. the request: whole frame, Render's post-processing (renderer.go:215-219)
@@ -205,6 +224,12 @@ func (r *Renderer) Render(ctx context.Context) image.Image {
 		req.bg_spd_wavelengths = (*C.double)(unsafe.Pointer(&r.bgWl[0]))
 		req.bg_spd_values = (*C.double)(unsafe.Pointer(&r.bgVal[0]))
 	}
+	if r.m != nil {
+		if rc := C.izpi_gpu_multi_render(r.m, &req, (*C.double)(unsafe.Pointer(&pix[0])), nil); rc != 0 {
+			panic(r.deviceError("izpi_gpu_multi_render", rc))
+		}
+		return floatimage.NewFloat64NRGBA(image.Rect(0, 0, r.sizeX, r.sizeY), pix)
+	}
 	var st C.izpi_render_stats
 	if rc := C.izpi_gpu_render(r.ctx, &req, (*C.double)(unsafe.Pointer(&pix[0])), &st); rc != 0 {
 		panic(r.deviceError("izpi_gpu_render", rc)) // the reference log.Fatals on render errors
@@ -214,6 +239,10 @@ func (r *Renderer) Render(ctx context.Context) image.Image {
 
 // Close releases the device context and the host-side scene.
 func (r *Renderer) Close() {
+	if r.m != nil {
+		C.izpi_gpu_multi_close(r.m) // closes device 0's context too
+		r.m, r.ctx = nil, nil
+	}
 	if r.ctx != nil {
 		C.izpi_gpu_close(r.ctx)
 		r.ctx = nil

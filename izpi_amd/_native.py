@@ -178,7 +178,7 @@ EXPORTS = [
     "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
-    "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_info", "izpi_scene_image_file",
+    "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_serialize", "izpi_scene_info", "izpi_scene_image_file",
     "izpi_scene_set_image", "izpi_scene_add_triangles", "izpi_scene_background", "izpi_scene_to_input",
     "izpi_scene_material_name", "izpi_scene_free", "izpi_light_source", "izpi_light_source_name",
     "izpi_obj_parse", "izpi_obj_info_get", "izpi_obj_copy_vertices", "izpi_obj_group_get", "izpi_obj_copy_faces",
@@ -257,6 +257,7 @@ def lib():
     L.izpi_scene_parse_text.argtypes = [C.c_char_p, C.c_uint64, vpp]
     L.izpi_scene_parse_binary.argtypes = [C.c_char_p, C.c_uint64, vpp]
     L.izpi_scene_info.argtypes = [vp, C.POINTER(ProtoInfo)]
+    L.izpi_scene_serialize.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]
     L.izpi_scene_image_file.argtypes = [vp, C.c_uint32]
     L.izpi_scene_image_file.restype = C.c_char_p
     L.izpi_scene_set_image.argtypes = [vp, C.c_char_p, C.c_uint32, C.c_uint32, c_double_p]

@@ -51,9 +51,26 @@ def build_cli(force=False, verbose=True):
 LINK = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]  # RCCL: multi-process framebuffer gather
 
 
+REPLAY = LIBDIR / "go_shim_replay"
+REPLAY_SRC = ROOT / "integration" / "c" / "go_shim_replay.c"
+
+
+def build_replay(force=False, verbose=True):
+    """go_shim_replay: the Go shim's C call sequence in C (integration/c), for the tests."""
+    if not force and not _stale(REPLAY, [REPLAY_SRC, LIB, ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h"]):
+        return REPLAY
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-std=c99", "-Wall", "-I" + str(ROOT / "include"), "-o", str(REPLAY),
+           str(REPLAY_SRC), "-L" + str(LIBDIR), "-lizpi_gpu", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return REPLAY
+
+
 def build_gpu(force=False, verbose=True):
     if not force and not _stale(LIB, DEPS):
         build_cli(force, verbose)
+        build_replay(force, verbose)
         return LIB
     LIBDIR.mkdir(parents=True, exist_ok=True)
     objdir = LIBDIR / "obj"
@@ -72,6 +89,7 @@ def build_gpu(force=False, verbose=True):
     run([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), *LINK])
     os.replace(tmp, LIB)
     build_cli(True, verbose)
+    build_replay(True, verbose)
     return LIB
 
 

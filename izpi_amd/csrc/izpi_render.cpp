@@ -4,7 +4,7 @@
 //
 //   izpi-render --scene cornell.pbtxt [--obj mesh.obj --obj-material White] [--x 1024 --y 1024]
 //               [--samples 512] [--depth 50] [--bvh gpu|reference] [--png-pipeline]
-//               [--out image.pfm] [--raw canvas.f64] [--device 0] [--seed 12345]
+//               [--out image.pfm] [--raw canvas.f64] [--device 0 | --gpus N] [--seed 12345]
 //
 // The scene file is read as leader.go:54-75 does (.pbtxt text, .izpi binary); a SPECTRAL
 // scene renders with the spectral sampler and Render's post-processing (leader.go:77-81,
@@ -52,7 +52,7 @@ constexpr double kMinus60Deg = -0x1.0c152382d7366p+0;  // == -ingest.go_radians(
 
 int main(int argc, char** argv) {
   std::string scene_path, obj_path, obj_material = "White", out_pfm, out_raw, bvh = "gpu";
-  uint32_t W = 1024, H = 1024, spp = 16, depth = 50, device = 0;
+  uint32_t W = 1024, H = 1024, spp = 16, depth = 50, device = 0, gpus = 1;
   uint64_t seed = 12345;
   bool png = false;
   for (int i = 1; i < argc; i++) {
@@ -70,6 +70,7 @@ int main(int argc, char** argv) {
     else if (a == "--out") out_pfm = val();
     else if (a == "--raw") out_raw = val();
     else if (a == "--device") device = (uint32_t)atoi(val().c_str());
+    else if (a == "--gpus") gpus = (uint32_t)atoi(val().c_str());
     else if (a == "--seed") seed = strtoull(val().c_str(), nullptr, 10);
     else die("unknown option " + a);
   }
@@ -115,8 +116,17 @@ int main(int argc, char** argv) {
   if (izpi_scene_to_input(ps, (double)W / H, 12345, &in)) die(izpi_host_last_error());
   izpi_host_scene* host = nullptr;
   if (izpi_host_build_scene_ex(in, bvh == "gpu" ? IZPI_HOST_SKIP_BVH : 0u, &host)) die(izpi_host_last_error());
+  // --gpus N: one Render fans out over GPUs 0..N-1 (izpi_gpu_multi_*, renderer.go:123-147)
   izpi_ctx* ctx = nullptr;
-  if (izpi_gpu_open((int)device, &ctx)) die("izpi_gpu_open failed (no HIP device?)");
+  izpi_multi* multi = nullptr;
+  if (gpus > 1) {
+    std::vector<int> devs(gpus);
+    for (uint32_t i = 0; i < gpus; i++) devs[i] = (int)i;
+    if (izpi_gpu_multi_open(devs.data(), gpus, &multi)) die("izpi_gpu_multi_open failed (fewer GPUs?)");
+    ctx = izpi_gpu_multi_context(multi, 0);
+  } else if (izpi_gpu_open((int)device, &ctx)) {
+    die("izpi_gpu_open failed (no HIP device?)");
+  }
   const izpi_scene_desc* desc = izpi_host_scene_desc(host);
   if (bvh == "gpu") {
     const uint32_t n = desc->num_tris + desc->num_spheres;
@@ -134,7 +144,8 @@ int main(int argc, char** argv) {
     }
     fprintf(stderr, "izpi-render: GPU BVH4 of %u primitives, %u nodes, %.1f ms\n", n, num_nodes, ms);
   }
-  if (izpi_gpu_upload_scene(ctx, izpi_host_scene_desc(host))) die(izpi_gpu_last_error(ctx));
+  if (multi ? izpi_gpu_multi_upload_scene(multi, izpi_host_scene_desc(host)) : izpi_gpu_upload_scene(ctx, izpi_host_scene_desc(host)))
+    die(multi ? izpi_gpu_multi_last_error(multi) : izpi_gpu_last_error(ctx));
   const double setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   // ---- Render (renderer.go:108-222)
   izpi_render_req req;
@@ -146,13 +157,19 @@ int main(int argc, char** argv) {
   req.exposure = izpi_host_scene_desc(host)->camera.exposure;
   req.post = (spectral ? IZPI_POST_SPECTRAL : IZPI_POST_NONE) | (png ? IZPI_POST_GAMMA_CLAMP : 0u);
   std::vector<double> canvas((size_t)W * H * 4);
-  izpi_render_stats st;
+  std::vector<izpi_render_stats> stv(gpus > 1 ? gpus : 1);
   auto t1 = std::chrono::steady_clock::now();
-  if (izpi_gpu_render(ctx, &req, canvas.data(), &st)) die(izpi_gpu_last_error(ctx));
+  if (multi) {
+    if (izpi_gpu_multi_render(multi, &req, canvas.data(), stv.data())) die(izpi_gpu_multi_last_error(multi));
+  } else if (izpi_gpu_render(ctx, &req, canvas.data(), stv.data())) {
+    die(izpi_gpu_last_error(ctx));
+  }
+  izpi_render_stats st = stv[0];
+  for (size_t i = 1; i < stv.size(); i++) { st.rays += stv[i].rays; st.node_visits += stv[i].node_visits; }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
-  printf("{\"scene\": \"%s\", \"width\": %u, \"height\": %u, \"spp\": %u, \"bvh\": \"%s\", \"sampler\": \"%s\", "
+  printf("{\"scene\": \"%s\", \"width\": %u, \"height\": %u, \"spp\": %u, \"bvh\": \"%s\", \"sampler\": \"%s\", \"gpus\": %u, "
          "\"setup_s\": %.3f, \"render_s\": %.4f, \"msamples_per_s\": %.2f, \"rays\": %llu, \"node_visits\": %llu}\n",
-         scene_path.c_str(), W, H, spp, bvh.c_str(), spectral ? "spectral" : "colour", setup_s, secs,
+         scene_path.c_str(), W, H, spp, bvh.c_str(), spectral ? "spectral" : "colour", gpus > 1 ? gpus : 1u, setup_s, secs,
          (double)W * H * spp / secs / 1e6, (unsigned long long)st.rays, (unsigned long long)st.node_visits);
   // ---- outputs
   if (!out_raw.empty()) {
@@ -172,7 +189,8 @@ int main(int argc, char** argv) {
     }
     fclose(f);
   }
-  izpi_gpu_close(ctx);
+  if (multi) izpi_gpu_multi_close(multi);
+  else izpi_gpu_close(ctx);
   izpi_host_scene_free(host);
   izpi_scene_free(ps);
   return 0;

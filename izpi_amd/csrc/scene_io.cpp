@@ -627,6 +627,72 @@ struct WireParser {
   }
 };
 
+// proto.Marshal of a field tree (google.golang.org/protobuf): fields in field-number
+// order, repeated scalars packed (proto3), repeated messages and map entries in
+// occurrence order, proto3 scalars at their zero value omitted unless they are a oneof
+// member (presence) or a map entry's key.
+struct WireWriter {
+  std::string out;
+  void varint(uint64_t v) {
+    do {
+      uint8_t b = v & 0x7F;
+      v >>= 7;
+      out.push_back((char)(b | (v ? 0x80 : 0)));
+    } while (v);
+  }
+  void key(int num, int wt) { varint((uint64_t)num << 3 | (uint64_t)wt); }
+  void f32(double x) { const float f = (float)x; uint32_t b; memcpy(&b, &f, 4); out.append((const char*)&b, 4); }
+  void f64(double x) { uint64_t b; memcpy(&b, &x, 8); out.append((const char*)&b, 8); }
+  static bool zero(const FieldDef& fd, const PVal& v) {
+    switch (fd.type) {
+      case T_FLOAT: { const float f = (float)v.num; uint32_t b; memcpy(&b, &f, 4); return b == 0; }  // -0 is kept
+      case T_DOUBLE: { uint64_t b; memcpy(&b, &v.num, 8); return b == 0; }
+      case T_STRING: return v.s.empty();
+      case T_MSG: return false;
+      default: return v.u == 0;
+    }
+  }
+  void scalar(const FieldDef& fd, const PVal& v) {
+    if (fd.type == T_FLOAT) f32(v.num);
+    else if (fd.type == T_DOUBLE) f64(v.num);
+    else varint(fd.type == T_ENUM ? (uint64_t)(int64_t)(int32_t)v.u : v.u);
+  }
+  void msg(const PMsg& m) {
+    std::vector<int> order(m.def->fields.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return m.def->fields[a].num < m.def->fields[b].num; });
+    const bool entry = strstr(m.def->name, "Entry") != nullptr;
+    for (int fi : order) {
+      const FieldDef& fd = m.def->fields[fi];
+      const std::vector<PVal>& vals = m.f[fi];
+      if (vals.empty()) continue;
+      if (fd.repeated && fd.type != T_MSG && fd.type != T_STRING) {  // packed
+        WireWriter w;
+        for (const PVal& v : vals) w.scalar(fd, v);
+        key(fd.num, 2);
+        varint(w.out.size());
+        out += w.out;
+        continue;
+      }
+      const size_t n = fd.repeated ? vals.size() : 1;
+      for (size_t k = 0; k < n; k++) {
+        const PVal& v = fd.repeated ? vals[k] : vals.back();
+        if (!fd.repeated && !fd.oneof && !entry && zero(fd, v)) continue;
+        if (fd.type == T_MSG || fd.type == T_STRING) {
+          std::string payload;
+          if (fd.type == T_MSG) { WireWriter w; w.msg(*v.m); payload.swap(w.out); } else payload = v.s;
+          key(fd.num, 2);
+          varint(payload.size());
+          out += payload;
+        } else {
+          key(fd.num, fd.type == T_FLOAT ? 5 : fd.type == T_DOUBLE ? 1 : 0);
+          scalar(fd, v);
+        }
+      }
+    }
+  }
+};
+
 // ================================================================ transport.ToScene
 struct LightSpd { std::vector<double> values; };
 
@@ -1189,6 +1255,17 @@ int izpi_scene_parse_binary(const void* buf, uint64_t len, izpi_proto_scene** ou
     WireParser wp{(const uint8_t*)buf, (const uint8_t*)buf + len};
     wp.parse(*root);
     return finish_parse(root, out);
+  });
+}
+
+int izpi_scene_serialize(const izpi_proto_scene* s, void* buf, uint64_t cap, uint64_t* len) {
+  return guarded([&] {
+    if (!s || !len || (!buf && cap)) invalid("null argument");
+    WireWriter w;
+    w.msg(*s->root);
+    *len = w.out.size();
+    if (buf) memcpy(buf, w.out.data(), std::min<uint64_t>(cap, w.out.size()));
+    return IZPI_OK;
   });
 }
 

@@ -67,6 +67,14 @@ class ProtoScene:
             return cls(path.read_bytes(), binary=True)
         raise ValueError("Unknown scene file extension: %s" % ext)
 
+    def to_wire(self):
+        """transport.Scene wire bytes (proto.Marshal's form, the .izpi file format)."""
+        n = C.c_uint64()
+        _err(N.lib().izpi_scene_serialize(self.handle, None, 0, C.byref(n)), "izpi_scene_serialize")
+        buf = C.create_string_buffer(max(1, n.value))
+        _err(N.lib().izpi_scene_serialize(self.handle, buf, n.value, C.byref(n)), "izpi_scene_serialize")
+        return buf.raw[:n.value]
+
     def info(self):
         i = N.ProtoInfo()
         _err(N.lib().izpi_scene_info(self.handle, C.byref(i)), "izpi_scene_info")

@@ -558,6 +558,11 @@ def test_cli_renders_like_the_python_host(gpu, tmp_path):
     img = r.render(post=N.POST_GAMMA_CLAMP)
     r.close()
     assert np.fromfile(raw, np.float64).tobytes() == img.tobytes()
+    import torch
+    if torch.cuda.device_count() >= 2:  # --gpus: the multi-GPU entry points (izpi_gpu_multi_*)
+        out = subprocess.run([str(cli), "--scene", str(example), "--x", "40", "--y", "40", "--samples", "4", "--gpus", "2",
+                              "--raw", str(raw)], capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
 
 
 @pytest.mark.parametrize("table", ["duplicates", "unsorted", "single"])
