@@ -5,10 +5,13 @@ their sizes against the compiled library's expectations. Loading fails loudly wh
 the native library is missing: there is no Python fallback for the hot path.
 """
 import ctypes as C
+import os
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 LIB_PATH = ROOT / "izpi_amd" / "_lib" / "libizpi_gpu.so"
+if os.environ.get("IZPI_LIB_PATH"):  # experiments only (tools/vrun.sh): a variant build of the same library
+    LIB_PATH = Path(os.environ["IZPI_LIB_PATH"])
 
 c_double_p = C.POINTER(C.c_double)
 c_uint32_p = C.POINTER(C.c_uint32)

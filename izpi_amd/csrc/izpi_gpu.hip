@@ -193,59 +193,75 @@ IZPI_DEV void cie_values(double w, double& x, double& y, double& z) {
 }
 
 // ============================================================ wavefront state
-// Per-slot records in HBM. The ray a slot wants traced next is kept as a 64-B-aligned
-// hot record (o, d, tmin, tmax: exactly one 64-B sector, read by every traversal refill
-// and primitive step) plus a 16-B aux record (time, kind, material of a path-length ray).
+// The paths in flight live in queue order: entry i of a pass's queue IS path i's state
+// (ray, hit, path), held in record arrays indexed by queue position and double-buffered
+// between passes (WaveBuf in / out). k_trace2 reads the rays of a chunk of consecutive
+// entries and writes their hits in place; k_shade reads entry i and writes a continuing
+// path to the position its block reserved on the output side, so every wave reads and
+// writes contiguous runs: no slot indirection, no scattered partial-line stores. Only a
+// path's unwinding records stay put, in its record slot (rslot), written once per bounce
+// and read back when the path finishes.
 struct RayRec {               // register form
   double o[3], d[3];
-  double tmin, tmax, time;
-  uint32_t kind;              // RAY_MAIN (counts as a Sampler call) / RAY_PATHLEN
-  uint32_t pad;
+  double time;
+  uint32_t kind;              // kind word (below)
 };
-struct alignas(64) RayHot { double o[3], d[3]; double tmin, tmax; };
-struct alignas(16) RayAux { double time; uint32_t kind, pad; };
-// Closest hit of a slot's ray: ONE aligned 32-B record (t, primitive, barycentrics), so
-// k_trace2's per-ray result is a single 32-B store into one line (two 16-B records in
-// two arrays cost two partially written lines per ray). k_shade reads the first 16 B
-// on every pass and (u, v) only for UV-textured and sphere hits.
+struct alignas(16) RayOD { double o[3], d[3]; };  // 48 B
+// kind word: bits 0-1 RAY_MAIN / RAY_PATHLEN, bit 2 RAY_PARKED, bit 3 RAY_DEAD, bits 4-31
+// the dielectric material of a path-length ray (<< KIND_MAT_SHIFT).
+// RAY_MAIN rays count as Sampler calls and run tMin 0.001 .. MaxFloat64 (colour.go:39);
+// RAY_PATHLEN rays are calculatePathLength's World.Hit, tMin 0 .. 1000 (dielectric.go:135).
+// RAY_PARKED: the entry's shading pass waits for an overflow record block (pool_alloc);
+// k_trace2 skips it and the next k_shade shades the same traced ray again (the pass reads
+// only stored state, so the retry computes exactly what the first attempt would have).
+// RAY_DEAD: an entry reserved for a new path whose sample completed without a ray
+// (spectral pdf 0, maxDepth 0); every kernel skips it.
+enum { RAY_MAIN = 0, RAY_PATHLEN = 1, RAY_PARKED = 4, RAY_DEAD = 8, KIND_MAT_SHIFT = 4 };
+IZPI_DEV uint32_t kind_of(uint32_t k) { return k & 3u; }
+// Closest hit of an entry's ray: ONE aligned 32-B record (t, primitive, barycentrics).
+// k_shade reads the first 16 B on every pass and (u, v) only for UV-textured and sphere hits.
 struct HitOut {               // register form
   double t, u, v;             // triangle barycentrics, or u = sphere root
   int32_t prim;               // leaf-order primitive, -1 = miss
   uint32_t pad;
 };
 struct alignas(32) HitSt { double t; int32_t prim; uint32_t pad; double u, v; };
-// Path state, split into a hot record every pass reads and a cold one read only when
-// needed (spectral wavelength, dielectric point).
 struct PathSt {               // register form
   double lambda, lpdf;        // wavelength and its pdf (spectral)
   double pend[3];             // dielectric hit point while its path-length ray is traced
-  uint32_t rng, depth, unit, blk;
+  uint32_t rng, depth, unit, rslot, blk;
 };
-// blk: 1 + the overflow record block holding this path's unwinding records at depths
-// >= ShadeParams::rec_dense (0 = none yet); see pool_alloc.
-struct alignas(16) PathHot { uint32_t rng, depth, unit, blk; };
+// rslot: the path's record slot; blk: 1 + the overflow record block holding its
+// unwinding records at depths >= ShadeParams::rec_dense (0 = none yet), see pool_alloc.
+struct alignas(16) PathHot { uint32_t rng, depth, unit, rslot; };
 struct alignas(16) PathCold { double lambda, lpdf; double pend[3]; double pad; };
-enum { RAY_MAIN = 0, RAY_PATHLEN = 1 };
 
-// Queue entries are slot indices. PARK_BIT marks a slot whose shading pass waits for an
-// overflow record block (pool_alloc): k_trace2 leaves it untraced and untouched, and the
-// next k_shade pass shades the same traced ray again (the pass reads only stored state,
-// so the retry computes exactly what the first attempt would have).
-constexpr uint32_t PARK_BIT = 0x80000000u;
-struct WaveParams {
-  RayHot* rhot;
-  RayAux* raux;
+// One side of the double-buffered state, indexed by queue position.
+struct WaveBuf {
+  RayOD* ray;
+  uint32_t* kind;     // kind word
+  double* time;       // ray time (scenes with spheres), else null
+  PathHot* path;
+  uint32_t* blk;      // overflow block + 1
+  PathCold* cold;     // spectral / dielectric scenes, else null
   HitSt* hit;
-  PathHot* phot;
-  PathCold* pcold;
-  const uint32_t* q_in;       // slots to process this pass
-  const uint32_t* q_in_count;
-  uint32_t* q_out;            // slots whose next ray must be traced
-  uint32_t* q_out_count;
-  uint32_t* trace_next;       // dynamic-fetch cursor of k_trace
+  const double2* tminmax;  // izpi_gpu_trace only: per-entry (tMin, tMax) instead of the kind's
+};
+struct WaveParams {
+  WaveBuf in, out;
+  const uint32_t* in_count;   // entries in `in` this pass
+  uint32_t* out_count;        // entries k_shade appends to `out`
+  uint32_t* trace_next;       // dynamic-fetch cursor of k_trace2
   unsigned long long* pool_ctr;  // overflow-record ring counters (k_trace2 publishes frees), or null
   uint32_t slots;
+  uint32_t read_kind;         // entries other than plain RAY_MAIN rays can occur (k_trace2 reads kind words)
 };
+IZPI_DEV double ray_tmin(const WaveBuf& b, uint32_t i, uint32_t kind) {
+  return b.tminmax ? b.tminmax[i].x : (kind_of(kind) == RAY_PATHLEN ? 0.0 : 0.001);
+}
+IZPI_DEV double ray_tmax(const WaveBuf& b, uint32_t i, uint32_t kind) {
+  return b.tminmax ? b.tminmax[i].y : (kind_of(kind) == RAY_PATHLEN ? 1000.0 : 1.7976931348623157e308);
+}
 
 // Overflow record blocks (see pool_alloc) come in POOL_SHARDS independent rings, each
 // with its own counters on its own 128-B line: [0] allocation head, [1] free tail,
@@ -267,14 +283,14 @@ IZPI_DEV void pool_publish(unsigned long long* ctr) {
 // BVH4.Hit (bvh4.go:49-164) for one ray in one lane, LDS stack: k_tail's traversal
 // (the wavefront passes use k_trace2 below). Same visit order and counters.
 template <int STACK>
-IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot, int32_t* stk, uint32_t& c_rays,
+IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32_t* stk, uint32_t& c_rays,
                         uint32_t& c_nodes, uint32_t& c_tri, uint32_t& c_sph, uint32_t* err) {
-  const RayHot& r = wp.rhot[slot];
-  const RayAux& ra = wp.raux[slot];
+  const RayOD& r = b.ray[qi];
+  const uint32_t kind = b.kind[qi];
   const V3 o = mk(r.o[0], r.o[1], r.o[2]), d = mk(r.d[0], r.d[1], r.d[2]);
-  const double tmin = r.tmin, time = ra.time;
-  double tmax = r.tmax;
-  if (ra.kind == RAY_MAIN) c_rays++;
+  const double tmin = ray_tmin(b, qi, kind), time = b.time ? b.time[qi] : 0.0;
+  double tmax = ray_tmax(b, qi, kind);
+  if (kind_of(kind) == RAY_MAIN) c_rays++;
   const float ix = (float)(1.0 / d.x), iy = (float)(1.0 / d.y), iz = (float)(1.0 / d.z);
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   int32_t cur = sc.root;
@@ -336,7 +352,7 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot,
       cur = -1;
     }
   }
-  wp.hit[slot] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, bu, bv};
+  b.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, bu, bv};
 }
 
 // BVH4.Hit, step-scheduled variant. Each lane is in one of two modes: NODE (visit
@@ -353,15 +369,11 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveParams& wp, uint32_t slot,
 // spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
 // are kept per wave in SGPRs (popcounts of ballots).
 // TRI: the scene holds no spheres (DevScene::tri_only), so the sphere code is compiled out.
-#ifndef IZPI_TRACE_PREQ
-#define IZPI_TRACE_PREQ 1  // prefetch a chunk's queue entries when the chunk is taken
-#endif
 template <int S, int WPE, bool DIST, bool TRI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
-  constexpr bool PREQ = IZPI_TRACE_PREQ != 0;  // chunks of <= 128 entries (make_tracer clamps)
   __shared__ int32_t lds_stack[S * 256];
   // DIST: one wave-wide batch of leaf tests: (primitive << 6 | owner lane), then the
   // test's result flags in the same word; distances and barycentrics
@@ -376,8 +388,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t* stk = lds_stack + threadIdx.x;
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t n = *wp.q_in_count;
+  const uint32_t n = *wp.in_count;
   if (wp.pool_ctr && blockIdx.x == 0) pool_publish(wp.pool_ctr);
+  // kind words other than RAY_MAIN exist only with dielectrics (path-length rays), an
+  // overflow record pool (parked entries), dead entries or explicit tMin / tMax
+  const bool read_kind = wp.read_kind != 0;
   // Small queues (the wavefront's tail passes): chunks shrink so the rays spread over
   // more waves, and waves past the last chunk exit at once instead of each paying a
   // dequeue atomic on the one counter word (~88/us chip-wide).
@@ -388,7 +403,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
   bool busy = false, in_prim = false;
   bool exhausted = false;
-  uint32_t slot = 0;
+  uint32_t qi = 0;        // the lane's queue entry (its ray, hit and path state index)
+  uint32_t lkind = RAY_MAIN;
   double tmax = 0;
   float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
   int32_t cur = -1, pk = 0, pend = 0;
@@ -397,10 +413,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
   uint32_t c_pos = 0, c_end = 0;  // wave-private range [c_pos, c_end) of the input queue
-  // the chunk's queue entries, loaded when the chunk is taken (lane i: entries c_beg + i and
-  // c_beg + 64 + i), so a refill reads its slot with a lane shuffle instead of a dependent
-  // load ahead of the ray load
-  uint32_t c_beg = 0, pre0 = 0, pre1 = 0;
 #ifdef IZPI_TRACE_CLOCKS
   uint64_t k_refill = 0, k_node = 0, k_prim = 0, k_adv = 0, k0 = 0, k1 = 0;
 #define IZPI_CLK(v) (v) = __builtin_readcyclecounter()
@@ -421,11 +433,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (b >= n) exhausted = true;
         c_pos = b;
         c_end = b + chunk < n ? b + chunk : n;
-        c_beg = b;
-        if (PREQ) {
-          pre0 = b + lane < c_end ? wp.q_in[b + lane] : 0u;
-          pre1 = b + 64 + lane < c_end ? wp.q_in[b + 64 + lane] : 0u;
-        }
       }
       if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos < c_end) {
         const uint32_t take = nidle < c_end - c_pos ? nidle : c_end - c_pos;
@@ -434,21 +441,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         bool main_ray = false;
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
         const uint32_t my = base + rank;
-        uint32_t pslot = 0;
-        if (PREQ) {  // all lanes shuffle (wave-uniform here), idle lanes keep the result
-          const uint32_t k = my - c_beg;
-          const uint32_t s0 = (uint32_t)__shfl((int)pre0, (int)(k & 63));
-          const uint32_t s1 = (uint32_t)__shfl((int)pre1, (int)(k & 63));
-          pslot = k < 64 ? s0 : s1;
-        }
-        if (!busy) {
-          // a parked slot (PARK_BIT) is not traced: its hit record stays for the retry
-          if (rank < take && !((PREQ ? pslot : wp.q_in[my]) & PARK_BIT)) {
-            slot = PREQ ? pslot : wp.q_in[my];
-            const RayHot& r = wp.rhot[slot];
-            tmax = r.tmax;
-            // ray kinds other than RAY_MAIN exist only with dielectrics (path-length rays)
-            main_ray = sc.no_pathlen || wp.raux[slot].kind == RAY_MAIN;
+        if (!busy && rank < take) {
+          const uint32_t k = read_kind ? wp.in.kind[my] : (uint32_t)RAY_MAIN;
+          // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
+          if (!(k & (RAY_PARKED | RAY_DEAD))) {
+            qi = my;
+            lkind = k;
+            const RayOD& r = wp.in.ray[my];
+            tmax = ray_tmax(wp.in, my, k);
+            main_ray = kind_of(k) == RAY_MAIN;
             ix = (float)(1.0 / r.d[0]); iy = (float)(1.0 / r.d[1]); iz = (float)(1.0 / r.d[2]);
             ox = (float)r.o[0]; oy = (float)r.o[1]; oz = (float)r.o[2];
             fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
@@ -457,7 +458,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             in_prim = false;
             bprim = -1;
             busy = cur != -1;
-            if (!busy) wp.hit[slot] = HitSt{0.0, -1, 0u, 0.0, 0.0};
+            if (!busy) wp.in.hit[my] = HitSt{0.0, -1, 0u, 0.0, 0.0};
           }
         }
         c_rays += (uint64_t)__popcll(__ballot(main_ray));
@@ -503,11 +504,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         __builtin_amdgcn_wave_barrier();
         const uint32_t ent = lane < total ? dist_owner[wbase + lane] : lane;
         const uint32_t ow = ent & 63u;
-        const uint32_t oslot = (uint32_t)__shfl((int)slot, (int)ow);
+        const uint32_t oqi = (uint32_t)__shfl((int)qi, (int)ow);
+        const uint32_t okind = (uint32_t)__shfl((int)lkind, (int)ow);
         if (lane < total) {
           const int32_t pi = (int32_t)(ent >> 6);
-          const double2* rp = reinterpret_cast<const double2*>(wp.rhot + oslot);
-          const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+          const double2* rp = reinterpret_cast<const double2*>(wp.in.ray + oqi);
+          const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+          const double otmin = ray_tmin(wp.in, oqi, okind);
           const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
           const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
           const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
@@ -515,14 +518,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
           uint32_t flags;
           if (TRI || (uint32_t)__double2loint(p4.y) == IZPI_PRIM_TRIANGLE) {
-            flags = tri_intersect_no_tmax(pa, o, d, r3.x, t, u, v) ? 1u : 0u;
+            flags = tri_intersect_no_tmax(pa, o, d, otmin, t, u, v) ? 1u : 0u;
           } else {
             // sphere: both roots now, their tMin tests as flags; tMax is applied in order
             // by the owner (sphere.go:72-92: root 0 if tMin < t0 < tMax, else root 1)
-            const double time = wp.raux[oslot].time;
+            const double time = wp.in.time ? wp.in.time[oqi] : 0.0;
             flags = 2u;
             if (sph_roots(sph_center(pa, time), pa[6], o, d, t, u))
-              flags |= 1u | (t > r3.x ? 4u : 0u) | (u > r3.x ? 8u : 0u);
+              flags |= 1u | (t > otmin ? 4u : 0u) | (u > otmin ? 8u : 0u);
           }
           dist_t[wbase + lane] = t; dist_u[wbase + lane] = u; dist_v[wbase + lane] = v;
           dist_owner[wbase + lane] = flags;
@@ -581,10 +584,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         // the f64 ray is re-read here (L2) instead of living in 14 VGPRs across node steps
         // (measured: keeping it in LDS instead makes k_shade's later read of the same
         // record miss and costs more than it saves)
-        const double2* rp = reinterpret_cast<const double2*>(wp.rhot + slot);
-        const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+        const double2* rp = reinterpret_cast<const double2*>(wp.in.ray + qi);
+        const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2];
         const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
-        const double tmin = r3.x;
+        const double tmin = ray_tmin(wp.in, qi, lkind);
         const double2* pp = reinterpret_cast<const double2*>(sc.prims + pk);
         const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
         const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
@@ -595,7 +598,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             tmax = t; bprim = pk; lds_uv[threadIdx.x] = make_double2(u, v); clean_from = sp;
           }
         } else if (!TRI) {
-          const double time = wp.raux[slot].time;  // only spheres read the ray time
+          const double time = wp.in.time ? wp.in.time[qi] : 0.0;  // only spheres read the ray time
           double t; int root;
           if (sph_intersect(pa, o, d, time, tmin, tmax, t, root)) {
             tmax = t; bprim = pk; lds_uv[threadIdx.x] = make_double2((double)root, 0.0); clean_from = sp;
@@ -723,7 +726,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
         const double2 uv = bprim >= 0 ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        wp.hit[slot] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
+        wp.in.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
         busy = false;
       }
     }
@@ -937,15 +940,15 @@ struct RecLayout {
   static constexpr uint32_t S = D - 2;                                   // index of s (p follows)
 };
 template <int SAMPLER>
-IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t slot, uint32_t blk, uint32_t depth) {
+IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth) {
   constexpr uint32_t D = RecLayout<SAMPLER>::D;
-  if (depth < sp.rec_dense) return sp.recs + ((size_t)slot * sp.rec_dense + depth) * D;
+  if (depth < sp.rec_dense) return sp.recs + ((size_t)rslot * sp.rec_dense + depth) * D;
   return sp.pool + ((size_t)(blk - 1) * sp.rec_pool + (depth - sp.rec_dense)) * D;
 }
 template <int SAMPLER>
-IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t slot, uint32_t blk, uint32_t depth, bool spec, V3 att, double s,
+IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth, bool spec, V3 att, double s,
                         double p) {
-  double2* r = reinterpret_cast<double2*>(rec_ptr<SAMPLER>(sp, slot, blk, depth));
+  double2* r = reinterpret_cast<double2*>(rec_ptr<SAMPLER>(sp, rslot, blk, depth));
   r[0] = make_double2(spec ? 1.0 : 0.0, att.x);
   if (SAMPLER == IZPI_SAMPLER_COLOUR) r[1] = make_double2(att.y, att.z);
   if (!spec) r[RecLayout<SAMPLER>::S / 2] = make_double2(s, p);
@@ -959,7 +962,7 @@ IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.ou
 // Write the finished path's radiance after unwinding the recursion of
 // colour.go:80-94 / sampler/spectral.go:161-174 from depth-1 down to 0.
 template <int SAMPLER, bool NO_SPEC = false>
-IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L) {
+IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
     // +0 radiance through only non-specular records: every level computes
     // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
@@ -977,7 +980,7 @@ IZPI_DEV void finish(const ShadeParams& sp, uint32_t slot, const PathSt& P, V3 L
 #pragma unroll
     for (int j = 0; j < RB; j++) {
       if (dd - j >= 0) {
-        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER>(sp, slot, P.blk, (uint32_t)(dd - j)));
+        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER>(sp, P.rslot, P.blk, (uint32_t)(dd - j)));
 #pragma unroll
         for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
       }
@@ -1030,11 +1033,12 @@ IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colo
   return colour ? mk(0, 0, 1.0) : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda, sp.bg_sorted != 0), 0, 0);
 }
 
-// Start the path of work unit `unit` in `slot`: per-sample LCG streams, wavelength
-// (spectral), jitter, Camera.GetRay (camera.go:61-89). Returns false when the sample
-// is already complete (spectral pdf == 0 or maxDepth == 0); its result is written.
+// Start the path of work unit `unit`: per-sample LCG streams, wavelength (spectral),
+// jitter, Camera.GetRay (camera.go:61-89). P.rslot (the record slot) is the caller's.
+// Returns false when the sample is already complete (spectral pdf == 0 or maxDepth ==
+// 0); its result is written.
 template <int SAMPLER>
-IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slot, uint32_t unit, PathSt& P, RayRec& R) {
+IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t unit, PathSt& P, RayRec& R) {
   const uint32_t pix_local = unit / sp.chunk_spp;
   const uint32_t s = sp.s0 + unit % sp.chunk_spp;
   const uint32_t tile_px = sp.tile_w * sp.tile_h;
@@ -1078,42 +1082,54 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t slo
   V3 rd = sub(sub(add(add(ld3(c.lower_left), smul(ld3(c.horizontal), u)), smul(ld3(c.vertical), v)), origin), offset);
   P.rng = rng.s;
   if (sp.max_depth == 0) {
-    finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));
+    finish<SAMPLER>(sp, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));
     return false;
   }
   R.o[0] = ro.x; R.o[1] = ro.y; R.o[2] = ro.z;
   R.d[0] = rd.x; R.d[1] = rd.y; R.d[2] = rd.z;
-  R.tmin = 0.001; R.tmax = 1.7976931348623157e308; R.time = time;
-  R.kind = RAY_MAIN; R.pad = 0;
+  R.time = time;
+  R.kind = RAY_MAIN;
   return true;
 }
 
+// A path's state into entry `pos` of buffer `b` (coalesced: the writing wave's entries
+// are consecutive). The cold record carries the wavelength (spectral) and, for a
+// path-length ray, the dielectric hit point.
 template <int SAMPLER>
-IZPI_DEV void store_path(const WaveParams& wp, uint32_t slot, const PathSt& P) {
-  wp.phot[slot] = PathHot{P.rng, P.depth, P.unit, 0u};
-  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { wp.pcold[slot].lambda = P.lambda; wp.pcold[slot].lpdf = P.lpdf; }
+IZPI_DEV void store_entry(const WaveBuf& b, uint32_t pos, const PathSt& P, const RayRec& R) {
+  double2* r = reinterpret_cast<double2*>(b.ray + pos);
+  r[0] = make_double2(R.o[0], R.o[1]);
+  r[1] = make_double2(R.o[2], R.d[0]);
+  r[2] = make_double2(R.d[1], R.d[2]);
+  b.kind[pos] = R.kind;
+  if (b.time) b.time[pos] = R.time;
+  b.path[pos] = PathHot{P.rng, P.depth, P.unit, P.rslot};
+  if (b.blk) b.blk[pos] = P.blk;
+  if (b.cold) {
+    double2* c = reinterpret_cast<double2*>(b.cold + pos);
+    if (SAMPLER == IZPI_SAMPLER_SPECTRAL) c[0] = make_double2(P.lambda, P.lpdf);
+    if (kind_of(R.kind) == RAY_PATHLEN) { c[1] = make_double2(P.pend[0], P.pend[1]); c[2] = make_double2(P.pend[2], 0.0); }
+  }
 }
-
-IZPI_DEV void store_ray_full(const WaveParams& wp, uint32_t slot, const RayRec& R) {
-  RayHot h;
-  for (int k = 0; k < 3; k++) { h.o[k] = R.o[k]; h.d[k] = R.d[k]; }
-  h.tmin = R.tmin; h.tmax = R.tmax;
-  wp.rhot[slot] = h;
-  wp.raux[slot] = RayAux{R.time, R.kind, R.pad};
+// A parked entry moves to the output unchanged (its hit record too), flagged RAY_PARKED.
+IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint32_t pos) {
+  out.ray[pos] = in.ray[i];
+  out.kind[pos] = in.kind[i] | RAY_PARKED;
+  if (in.time) out.time[pos] = in.time[i];
+  out.path[pos] = in.path[i];
+  if (in.blk) out.blk[pos] = in.blk[i];
+  if (in.cold) out.cold[pos] = in.cold[i];
+  out.hit[pos] = in.hit[i];
 }
-
-// Append `push` lanes' slots to the output queue: one atomic per wave.
-IZPI_DEV void queue_push(uint32_t* q, uint32_t* count, bool push, uint32_t slot) {
-  const uint64_t m = __ballot(push);
-  if (m == 0) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
-  base = __shfl(base, (int)leader);
-  if (push) q[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = slot;
+// The path state of entry i (the ray and hit are read by shade_item).
+template <int SAMPLER>
+IZPI_DEV void load_path(const WaveBuf& b, uint32_t i, PathSt& P) {
+  const PathHot ph = b.path[i];
+  P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.rslot = ph.rslot;
+  P.blk = b.blk ? b.blk[i] : 0u;
+  P.lambda = 0; P.lpdf = 1;
+  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { const double2 c = *reinterpret_cast<const double2*>(b.cold + i); P.lambda = c.x; P.lpdf = c.y; }
 }
-IZPI_DEV void queue_push(const WaveParams& wp, bool push, uint32_t slot) { queue_push(wp.q_out, wp.q_out_count, push, slot); }
 
 // Block-wide reservation: every lane with `want` gets a distinct index from `counter`,
 // with ONE atomic per 256-thread block (a single counter word saturates near 88
@@ -1153,20 +1169,24 @@ IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
   return (want && my < sp.total_units) ? my : 0xFFFFFFFFu;
 }
 
-// Fill empty slots (first pass of a chunk): slot i takes unit i (the host starts the unit
-// head at min(slots, units), so no atomic is needed: one counter word serialises ~88
-// atomics/us), then further units from the head while its path needs no tracing.
+// First fill of the queue (first pass of a chunk): record slot j takes unit j (the host
+// starts the unit head at min(slots, units), so no atomic is needed: one counter word
+// serialises ~88 atomics/us), then further units from the head while its path needs no
+// tracing. The traceable paths are appended to `out`, one reservation per block.
 template <int SAMPLER>
 __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
-  const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
-  bool want = slot < sp.slots;
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  bool want = j < sp.slots;
   bool push = false;
   bool first = true;
+  PathSt P;
+  RayRec R;
+  P.rslot = j;
   // a wave keeps grabbing while any of its lanes still lacks a traceable path
   for (;;) {
     uint32_t unit;
     if (first) {
-      unit = (want && slot + sp.unit_base < sp.total_units) ? slot + sp.unit_base : 0xFFFFFFFFu;
+      unit = (want && j < sp.total_units) ? j : 0xFFFFFFFFu;
       first = false;
     } else {
       unit = grab_unit(sp, want);
@@ -1175,64 +1195,75 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
     if (want) {
       if (unit == 0xFFFFFFFFu) {
         want = false;
-      } else {
-        PathSt P;
-        RayRec R;
-        if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
-          store_path<SAMPLER>(wp, slot, P);
-          store_ray_full(wp, slot, R);
-          want = false;
-          push = true;
-        }
-      }
-    }
-  }
-  // one queue reservation per block (a per-wave atomic on the one count word made this
-  // kernel atomic-bound: 16M slots = 262k serialised atomics)
-  uint32_t parity = 0;
-  const uint32_t pos = block_reserve(wp.q_out_count, push, parity);
-  if (push) wp.q_out[pos] = slot;
-}
-
-// Give `slot` (when `want`) new work units until one yields a ray to trace (block-uniform
-// loop, block-wide unit reservations). Sets `push` when the slot has a ray.
-template <int SAMPLER>
-IZPI_DEV void refill_block(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, bool want,
-                           bool& push, uint32_t& parity) {
-  while (__syncthreads_or(want)) {
-    const uint32_t u = block_reserve(sp.head, want, parity);
-    const uint32_t unit = u < sp.total_units ? u : 0xFFFFFFFFu;
-    if (want) {
-      if (unit == 0xFFFFFFFFu) {
+      } else if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
         want = false;
-      } else {
-        PathSt P;
-        RayRec R;
-        if (start_path<SAMPLER>(sc, sp, slot, unit, P, R)) {
-          store_path<SAMPLER>(wp, slot, P);
-          store_ray_full(wp, slot, R);
-          want = false;
-          push = true;
-        }
+        push = true;
       }
     }
   }
+  uint32_t parity = 0;
+  const uint32_t pos = block_reserve(wp.out_count, push, parity);
+  if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
 }
 
-// Partial stores of the per-slot records: only the fields a pass changes are written,
-// so k_shade does not keep the untouched ones (ray time, wavelength, ...) in registers.
-// `aux`: also store kind/pad. Only MATSET_FULL turns a slot's ray into a path-length ray
-// and back, so the other variants leave the aux record as the path start wrote it.
-IZPI_DEV void store_ray(const WaveParams& wp, uint32_t slot, V3 o, V3 d, double tmin, double tmax, uint32_t kind,
-                        uint32_t pad, bool aux = true) {
-  double2* p = reinterpret_cast<double2*>(wp.rhot + slot);
-  p[0] = make_double2(o.x, o.y);
-  p[1] = make_double2(o.z, d.x);
-  p[2] = make_double2(d.y, d.z);
-  p[3] = make_double2(tmin, tmax);
-  if (aux) *reinterpret_cast<uint2*>(&wp.raux[slot].kind) = make_uint2(kind, pad);  // the ray time is left as is
+// One block-wide reservation phase for a shading iteration (ONE pair of barriers, two
+// atomics by one thread): `unit_want` lanes get consecutive work units from the unit
+// head (the units past total_units are not granted); lanes with `put` and granted
+// `unit_want` lanes get consecutive output entries, `put` lanes first. A granted lane
+// whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
+IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
+                             uint32_t& pos, uint32_t& parity) {
+  __shared__ uint32_t s_p[2][4], s_u[2][4];
+  __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2];
+  const uint32_t b = parity;
+  parity ^= 1u;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  const uint64_t mp = __ballot(put), mu = __ballot(unit_want);
+  if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t np = s_p[b][0] + s_p[b][1] + s_p[b][2] + s_p[b][3];
+    const uint32_t nu = s_u[b][0] + s_u[b][1] + s_u[b][2] + s_u[b][3];
+    uint32_t u0 = 0, granted = 0;
+    if (nu) {
+      u0 = atomicAdd(sp.head, nu);
+      granted = u0 >= sp.total_units ? 0u : min(nu, sp.total_units - u0);
+    }
+    s_ubase[b] = u0;
+    s_granted[b] = granted;
+    s_nput[b] = np;
+    s_pbase[b] = (np + granted) ? atomicAdd(out_count, np + granted) : 0u;
+  }
+  __syncthreads();
+  uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
+  for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
+  unit = s_ubase[b] + ur;
+  const bool granted = unit_want && ur < s_granted[b];
+  if (!granted) unit = 0xFFFFFFFFu;
+  pos = put ? s_pbase[b] + pr : (granted ? s_pbase[b] + s_nput[b] + ur : 0xFFFFFFFFu);
 }
-IZPI_DEV void store_path_hot(PathHot* ps, uint32_t rng, const PathSt& P) { *ps = PathHot{rng, P.depth, P.unit, P.blk}; }
+
+// A lane whose path finished got `unit` and entry `pos` (block_reserve2): start the
+// unit's path in the finished path's record slot and store it; when its sample completes
+// without a ray, take further units one at a time (rare), and leave a dead entry when
+// none traces.
+template <int SAMPLER>
+IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBuf& out, uint32_t unit, uint32_t pos,
+                         PathSt& P) {
+  RayRec R;
+  for (;;) {
+    if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
+      store_entry<SAMPLER>(out, pos, P, R);
+      return;
+    }
+    unit = atomicAdd(sp.head, 1u);
+    if (unit >= sp.total_units) {
+      out.kind[pos] = RAY_DEAD;
+      return;
+    }
+  }
+}
 
 // MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
 // DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
@@ -1243,31 +1274,23 @@ enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
 // One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
 // one bounce deep (colour.go:33-94, sampler/spectral.go:47-80). Sets `push` when the slot
 // has a ray to trace next and `done` when its sample finished.
-// `ph` is the slot's PathHot as read by the caller, with blk set to the path's overflow
-// block when it needs one (P.depth >= rec_dense). `fblk` returns the block to free when
-// the sample finished.
+// Entry i of `in`: P is its path state (load_path), with blk set to the path's overflow
+// block when it needs one (P.depth >= rec_dense); `kind` its kind word. On return, P and
+// R hold the continuing path and its next ray (`push`), or `done` is set and `fblk` is
+// the block to free.
 template <int SAMPLER, int MATSET>
-IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveParams& wp, uint32_t slot, const PathHot& ph,
-                         bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt, uint32_t& c_ls) {
+IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
+                         PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt, uint32_t& c_ls) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
-  PathSt P;
   {
-    P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.blk = ph.blk;
-    P.lambda = 0; P.lpdf = 1;
-    if (!COLOUR) { const PathCold& pc = wp.pcold[slot]; P.lambda = pc.lambda; P.lpdf = pc.lpdf; }
-  }
-  RayRec R;
-  {
-    const RayHot rh = wp.rhot[slot];
+    const RayOD rh = in.ray[i];
     for (int k = 0; k < 3; k++) { R.o[k] = rh.o[k]; R.d[k] = rh.d[k]; }
-    R.tmin = rh.tmin; R.tmax = rh.tmax;
-    const RayAux& ra = wp.raux[slot];
-    R.kind = ra.kind; R.pad = ra.pad;
-    R.time = 0;  // read below only for sphere hits
+    R.kind = kind;
+    R.time = in.time ? in.time[i] : 0.0;  // NewRay(hr.P, dir, r.Time()): the next ray keeps the time
   }
   HitOut H;
   {
-    const double2 hh = *reinterpret_cast<const double2*>(wp.hit + slot);  // t, prim (u, v read on demand)
+    const double2 hh = *reinterpret_cast<const double2*>(in.hit + i);  // t, prim (u, v read on demand)
     H.t = hh.x; H.prim = (int32_t)__double2loint(hh.y); H.pad = 0; H.u = 0; H.v = 0;
   }
   Lcg rng;
@@ -1279,9 +1302,9 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
   V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
   V3 hit_n = mk(0, 0, 0);
   Onb cos_onb;
-  if (MATSET == MATSET_FULL && R.kind == RAY_PATHLEN) {
+  if (MATSET == MATSET_FULL && kind_of(R.kind) == RAY_PATHLEN) {
     // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
-    const PathCold& pc = wp.pcold[slot];
+    const PathCold& pc = in.cold[i];
     const V3 hp = mk(pc.pend[0], pc.pend[1], pc.pend[2]);
     double len = 10.0;
     if (H.prim >= 0) {
@@ -1290,7 +1313,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
       if (len < 0.1) len = 0.1;
       if (len > 100.0) len = 100.0;
     }
-    const uint32_t mat_id = (uint32_t)R.pad;  // dielectric material stashed by the glass bounce
+    const uint32_t mat_id = R.kind >> KIND_MAT_SHIFT;  // dielectric material stashed by the glass bounce
     const izpi_material& gm_ = sc.materials[mat_id];
     if (COLOUR) att = mk(gm::exp(-gm_.rgb[0] * len), gm::exp(-gm_.rgb[1] * len), gm::exp(-gm_.rgb[2] * len));
     else att.x = gm_.absorb_tex >= 0 ? gm::exp(-tex_spectral(sc, gm_.absorb_tex, P.lambda) * len) : 1.0;
@@ -1304,8 +1327,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    const double rtime = IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_SPHERE ? wp.raux[slot].time : 0.0;
-    hit_record(sc, H, wp.hit + slot, gs, ro, rd, rtime, (gs.cflags & 2u) != 0, h);
+    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs.cflags & 2u) != 0, h);
     hit_n = h.n;
     next_o = h.p;
     // the shade record carries the material kind and, for a constant RGB texture, its
@@ -1340,10 +1362,12 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
         const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
         if (!reflected && (!COLOUR || beer_rgb)) {
           // the extra World.Hit of calculatePathLength: trace it, finish next pass
-          PathCold* pcw = wp.pcold + slot;
-          pcw->pend[0] = h.p.x; pcw->pend[1] = h.p.y; pcw->pend[2] = h.p.z;
-          store_path_hot(wp.phot + slot, rng.s, P);
-          store_ray(wp, slot, add(h.p, smul(next_d, 0.001)), next_d, 0.0, 1000.0, RAY_PATHLEN, h.mat);
+          P.pend[0] = h.p.x; P.pend[1] = h.p.y; P.pend[2] = h.p.z;
+          P.rng = rng.s;
+          const V3 po = add(h.p, smul(next_d, 0.001));
+          R.o[0] = po.x; R.o[1] = po.y; R.o[2] = po.z;
+          R.d[0] = next_d.x; R.d[1] = next_d.y; R.d[2] = next_d.z;
+          R.kind = RAY_PATHLEN | (h.mat << KIND_MAT_SHIFT);
           push = true;
           break;
         }
@@ -1413,7 +1437,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
   }
   if (!push) {
     if (terminal) {
-      finish<SAMPLER, MATSET == MATSET_BASIC>(sp, slot, P, L);
+      finish<SAMPLER, MATSET == MATSET_BASIC>(sp, P, L);
       done = true;
       fblk = P.blk;
     } else {
@@ -1429,22 +1453,23 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WavePa
         const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
         double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
         if (sc_cos < 0) sc_cos = 0;
-        rec_store<SAMPLER>(sp, slot, P.blk, P.depth, false, att, sc_cos / 3.141592653589793, 0);
+        rec_store<SAMPLER>(sp, P.rslot, P.blk, P.depth, false, att, sc_cos / 3.141592653589793, 0);
         const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
-        rec_ptr<SAMPLER>(sp, slot, P.blk, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
+        rec_ptr<SAMPLER>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
         next_d = dir;
       } else {
-        rec_store<SAMPLER>(sp, slot, P.blk, P.depth, true, att, 0, 0);
+        rec_store<SAMPLER>(sp, P.rslot, P.blk, P.depth, true, att, 0, 0);
       }
       P.depth++;
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
-        finish<SAMPLER>(sp, slot, P, terminal_max_depth(sp, P, COLOUR));
+        finish<SAMPLER>(sp, P, terminal_max_depth(sp, P, COLOUR));
         done = true;
         fblk = P.blk;
       } else {
-        store_path_hot(wp.phot + slot, P.rng, P);
-        store_ray(wp, slot, next_o, next_d, 0.001, 1.7976931348623157e308, RAY_MAIN, 0, MATSET == MATSET_FULL);
+        R.o[0] = next_o.x; R.o[1] = next_o.y; R.o[2] = next_o.z;
+        R.d[0] = next_d.x; R.d[1] = next_d.y; R.d[2] = next_d.z;
+        R.kind = RAY_MAIN;
         push = true;
       }
     }
@@ -1505,7 +1530,7 @@ IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
 
 // One shading pass over the slots traced in the previous k_trace.
 #ifndef IZPI_SHADE_WPE
-#define IZPI_SHADE_WPE 4  // MATSET_BASIC colour register budget: 4 waves/SIMD (measured 4% faster than 3 despite ~26 spilled VGPRs; 5 is 20% slower)
+#define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (168 VGPRs, 6 spilled; 4 waves spill 47 VGPRs and measured 1% slower)
 #endif
 #ifndef IZPI_SHADE_PREQ
 #define IZPI_SHADE_PREQ 1
@@ -1518,56 +1543,60 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve LDS buffer set
-  const uint32_t n = *wp.q_in_count;
+  const uint32_t n = *wp.in_count;
+  const bool read_kind = wp.read_kind != 0;
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * 256;
 #ifdef IZPI_SHADE_CLOCKS
   uint64_t k_item = 0, k_ref = 0, k_push = 0;
 #endif
-  // Block-uniform trip count: the queue and unit reservations are block-wide.
-  // The next iteration's queue entry is loaded one iteration ahead (software pipelining:
-  // one dependent load less in front of the slot's records).
-  uint32_t next_slot = blockIdx.x * 256 + threadIdx.x < n ? wp.q_in[blockIdx.x * 256 + threadIdx.x] : 0u;
+  // Block-uniform trip count: the unit and queue reservations are block-wide.
   for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < n;
-    uint32_t slot = next_slot;
-    next_slot = IZPI_SHADE_PREQ && i + stride < n ? wp.q_in[i + stride] : 0u;
-    if (!IZPI_SHADE_PREQ) slot = valid ? wp.q_in[i] : 0;
-    slot &= ~PARK_BIT;      // a parked slot retries its pass (its traced ray is unchanged)
-    bool push = false;      // slot has a ray to trace next
-    bool done = false;      // slot's sample finished: grab a new unit
+    bool push = false;      // the path has a ray to trace next (P, R)
+    bool done = false;      // its sample finished: start a new unit in its record slot
     bool parked = false;
     uint32_t fblk = 0;
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t0 = __builtin_readcyclecounter();
 #endif
-    PathHot ph = valid ? wp.phot[slot] : PathHot{0u, 0u, 0u, 0u};
+    PathSt P;
+    RayRec R;
+    P.rslot = 0; P.blk = 0; P.depth = 0;
+    uint32_t kind = RAY_DEAD;
+    if (valid) kind = (read_kind ? wp.in.kind[i] : (uint32_t)RAY_MAIN) & ~(uint32_t)RAY_PARKED;  // a parked entry retries
+    const bool live = valid && !(kind & RAY_DEAD);
+    if (live) load_path<SAMPLER>(wp.in, i, P);
     if (sp.rec_pool) {  // a path at depth >= rec_dense writes its records to an overflow block
-      const bool need = valid && ph.depth >= sp.rec_dense && ph.blk == 0;
+      const bool need = live && P.depth >= sp.rec_dense && P.blk == 0;
       const uint32_t b = pool_alloc(sp, need);
-      ph.blk = need ? b : ph.blk;
+      P.blk = need ? b : P.blk;
       parked = need && b == 0;
       c_park += parked ? 1u : 0u;
     }
-    if (valid && !parked) shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, ph, push, done, fblk, c_lt, c_ls);
+    if (live && !parked) shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, P, R, push, done, fblk, c_lt, c_ls);
     if (sp.rec_pool && fblk) pool_free_one(sp, fblk);
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t1 = __builtin_readcyclecounter();
     k_item += t1 - t0;
     t0 = t1;
 #endif
-    refill_block<SAMPLER>(sc, sp, wp, slot, done, push, parity);
-#ifdef IZPI_SHADE_CLOCKS
-    t1 = __builtin_readcyclecounter();
-    k_ref += t1 - t0;
-    t0 = t1;
-#endif
-    const uint32_t pos = block_reserve(wp.q_out_count, push || parked, parity);
-    if (push || parked) wp.q_out[pos] = parked ? (slot | PARK_BIT) : slot;
+    // one reservation phase: output entries for continuing and parked paths, new units
+    // (and their entries) for finished ones
+    uint32_t unit, pos;
+    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity);
+    if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
+    if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
     k_push += t1 - t0;
+    t0 = t1;
+#endif
+    if (unit != 0xFFFFFFFFu) refill_one<SAMPLER>(sc, sp, wp.out, unit, pos, P);
+#ifdef IZPI_SHADE_CLOCKS
+    t1 = __builtin_readcyclecounter();
+    k_ref += t1 - t0;
 #endif
   }
   const uint32_t lane = threadIdx.x & 63;
@@ -1596,27 +1625,31 @@ template <int SAMPLER, int MATSET, int STACK>
 __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   __shared__ int32_t lds_stack[STACK * 256];
   int32_t* stk = lds_stack + threadIdx.x;
-  const uint32_t n = *wp.q_in_count;
+  const uint32_t n = *wp.in_count;
   uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_lt = 0, c_ls = 0;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint32_t entry = wp.q_in[i];
-    const uint32_t slot = entry & ~PARK_BIT;
-    bool traced = (entry & PARK_BIT) != 0;  // a parked slot's ray is already traced
+    // entry i runs to its end in this lane; its next ray goes back to entry i
+    if (wp.in.kind[i] & RAY_DEAD) continue;
+    bool traced = (wp.in.kind[i] & RAY_PARKED) != 0;  // a parked entry's ray is already traced
     for (;;) {
-      if (!traced) trace_one<STACK>(sc, wp, slot, stk, c_rays, c_nodes, c_tri, c_sph, sp.error);
+      if (!traced) trace_one<STACK>(sc, wp.in, i, stk, c_rays, c_nodes, c_tri, c_sph, sp.error);
       traced = false;
-      PathHot ph = wp.phot[slot];
-      if (sp.rec_pool && ph.depth >= sp.rec_dense && ph.blk == 0) {
+      PathSt P;
+      RayRec R;
+      load_path<SAMPLER>(wp.in, i, P);
+      const uint32_t kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;
+      if (sp.rec_pool && P.depth >= sp.rec_dense && P.blk == 0) {
         // The host launches k_tail with at most pool blocks paths, all of the free
         // blocks published, so this cannot fail (guarded anyway: no spin on a bug).
-        ph.blk = pool_alloc_any(sp, blockIdx.x * 4u + (threadIdx.x >> 6));
-        if (ph.blk == 0) { atomicOr(sp.error, 4u); break; }
+        P.blk = pool_alloc_any(sp, blockIdx.x * 4u + (threadIdx.x >> 6));
+        if (P.blk == 0) { atomicOr(sp.error, 4u); break; }
       }
       bool push = false, done = false;
       uint32_t fblk = 0;
-      shade_item<SAMPLER, MATSET>(sc, sp, wp, slot, ph, push, done, fblk, c_lt, c_ls);
+      shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, P, R, push, done, fblk, c_lt, c_ls);
       if (fblk) pool_free_one(sp, fblk);
       if (!push) break;
+      store_entry<SAMPLER>(wp.in, i, P, R);
     }
   }
   const uint32_t lane = threadIdx.x & 63;
@@ -1792,24 +1825,19 @@ __global__ void k_unpack(const uint32_t* tiles, uint32_t num_pixels, uint32_t ti
 }
 
 // ------------------------------------------------------- component kernels
-// izpi_gpu_trace: rays [n][8] -> RayRec, queue = identity
-__global__ void k_trace_setup(const double* rays, uint32_t n, RayHot* rh, RayAux* ra, uint32_t* q, uint32_t* qn) {
+// izpi_gpu_trace: rays [n][8] -> queue entries with explicit (tMin, tMax)
+__global__ void k_trace_setup(const double* rays, uint32_t n, RayOD* ray, uint32_t* kind, double2* tminmax, uint32_t* qn) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) *qn = n;
   if (i >= n) return;
   const double* r = rays + (size_t)i * 8;
-  RayRec R;
-  for (int k = 0; k < 3; k++) { R.o[k] = r[k]; R.d[k] = r[3 + k]; }
-  R.tmin = r[6]; R.tmax = r[7]; R.time = 0; R.kind = RAY_PATHLEN; R.pad = 0;
-  RayHot h;
-  for (int k = 0; k < 3; k++) { h.o[k] = R.o[k]; h.d[k] = R.d[k]; }
-  h.tmin = R.tmin; h.tmax = R.tmax;
-  rh[i] = h;
-  ra[i] = RayAux{R.time, R.kind, R.pad};
-  q[i] = i;
+  RayOD h;
+  for (int k = 0; k < 3; k++) { h.o[k] = r[k]; h.d[k] = r[3 + k]; }
+  ray[i] = h;
+  kind[i] = RAY_PATHLEN;  // not a Sampler call
+  tminmax[i] = make_double2(r[6], r[7]);
 }
-__global__ void k_trace_records(const DevScene sc, const RayHot* rr, const HitSt* hit, uint32_t n,
-                                izpi_hit* out) {
+__global__ void k_trace_records(const DevScene sc, const RayOD* rr, const HitSt* hit, uint32_t n, izpi_hit* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   izpi_hit h;
@@ -1818,7 +1846,7 @@ __global__ void k_trace_records(const DevScene sc, const RayHot* rr, const HitSt
   HitOut c;
   c.t = hit[i].t; c.prim = hit[i].prim; c.u = hit[i].u; c.v = hit[i].v; c.pad = 0;
   if (c.prim >= 0) {
-    const RayHot R = rr[i];
+    const RayOD R = rr[i];
     HitRec hr;
     const GShade gs = sc.shade[c.prim];
     hit_record(sc, c, hit + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
@@ -1892,12 +1920,7 @@ struct izpi_ctx {
   double* d_bg = nullptr; size_t bg_cap = 0;
   uint32_t* d_misc = nullptr;              // [0] unit head, [1] error, [2] trace cursor, [3..4] queue counts
   unsigned long long* d_counters = nullptr;
-  RayHot* d_rhot = nullptr; size_t rhot_cap = 0;
-  RayAux* d_raux = nullptr; size_t raux_cap = 0;
-  HitSt* d_hit = nullptr; size_t hit_cap = 0;
-  PathHot* d_phot = nullptr; size_t phot_cap = 0;
-  PathCold* d_pcold = nullptr; size_t pcold_cap = 0;
-  uint32_t* d_queue = nullptr; size_t queue_cap = 0;   // two ping-pong queues of `slots`
+  char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
   double* d_share = nullptr; size_t share_cap = 0;    // multi-GPU: this device's packed tiles
@@ -1944,8 +1967,32 @@ int grow(izpi_ctx* ctx, void** p, size_t* cap, size_t bytes) {
 // Device bytes of the render workspace (the buffers `grow` manages).
 uint64_t workspace_bytes(const izpi_ctx* ctx) {
   return (uint64_t)ctx->samples_cap + ctx->recs_cap + ctx->pool_cap + ctx->ring_cap + ctx->running_cap + ctx->out_cap +
-         ctx->tiles_cap + ctx->utiles_cap + ctx->bg_cap + ctx->rhot_cap + ctx->raux_cap + ctx->hit_cap + ctx->phot_cap +
-         ctx->pcold_cap + ctx->queue_cap + ctx->spill_cap + ctx->post_cap + ctx->share_cap + ctx->gather_cap;
+         ctx->tiles_cap + ctx->utiles_cap + ctx->bg_cap + ctx->state_cap + ctx->spill_cap + ctx->post_cap + ctx->share_cap +
+         ctx->gather_cap;
+}
+
+// The two sides of the wavefront state, `slots` entries each, in one allocation:
+// returns the bytes (base == nullptr) or fills b[0], b[1].
+size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, WaveBuf* b) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> char* {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+    return p;
+  };
+  for (int k = 0; k < 2; k++) {
+    WaveBuf w{};
+    w.ray = (RayOD*)take((size_t)slots * sizeof(RayOD));
+    w.kind = (uint32_t*)take((size_t)slots * sizeof(uint32_t));
+    w.time = time ? (double*)take((size_t)slots * sizeof(double)) : nullptr;
+    w.path = (PathHot*)take((size_t)slots * sizeof(PathHot));
+    w.blk = blk ? (uint32_t*)take((size_t)slots * sizeof(uint32_t)) : nullptr;
+    w.cold = cold ? (PathCold*)take((size_t)slots * sizeof(PathCold)) : nullptr;
+    w.hit = (HitSt*)take((size_t)slots * sizeof(HitSt));
+    w.tminmax = nullptr;
+    if (b) b[k] = w;
+  }
+  return off;
 }
 
 void free_scene(izpi_ctx* ctx) {
@@ -1986,7 +2033,6 @@ int make_tracer(izpi_ctx* ctx, Tracer* t) {
   if (const char* e = getenv("IZPI_TRACE_DIST")) t->p2 = atoi(e) != 0;
   if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
-  if (IZPI_TRACE_PREQ) t->tchunk = std::min<uint32_t>(t->tchunk, 128);  // two prefetched entries per lane
   if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
   // DIST packs (primitive << 6 | lane) into one LDS word
   if (ctx->num_prims >= (1u << 26)) t->p2 = false;
@@ -2048,7 +2094,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
   if (const char* e = getenv("IZPI_TAIL")) tail_max = strtoull(e, nullptr, 10);
   // k_tail's allocations cannot park: every tail path must find a published block
   if (sp.rec_pool) tail_max = std::min<uint64_t>(tail_max, pool_blocks);
-  uint32_t* q[2] = {ctx->d_queue, ctx->d_queue + sp.slots};
+  const WaveBuf q[2] = {wp.in, wp.out};  // the two sides of the state; entry counts in d_misc[3..4]
   uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
   if (sp.rec_pool)
     hipLaunchKernelGGL(k_pool_init, dim3((pool_blocks + 255) / 256), dim3(256), 0, st, sp.pool_ring, pool_blocks,
@@ -2060,7 +2106,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     const uint32_t fill = std::min<uint32_t>(sp.slots, sp.total_units);
     HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)fill, 1, st));  // unit head: k_start gives slot i unit i
     HIP_TRY(hipMemsetAsync(ctx->d_misc + 3, 0, 2 * sizeof(uint32_t), st));  // queue counts
-    wp.q_out = q[0]; wp.q_out_count = qn[0];
+    wp.out = q[0]; wp.out_count = qn[0];
     hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, ctx->sc, sp, wp);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -2074,8 +2120,8 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     const int B = IZPI_PASS_BATCH;
     while (n > 0) {
       for (int b = 0; b < B; b++) {
-        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
-        wp.q_out = q[1 - cur]; wp.q_out_count = qn[1 - cur];
+        wp.in = q[cur]; wp.in_count = qn[cur];
+        wp.out = q[1 - cur]; wp.out_count = qn[1 - cur];
         HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
         HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
@@ -2100,7 +2146,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
       n = ctx->h_count[3 + cur];
       // every unit has started: finish the remaining paths in one k_tail launch
       if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
-        wp.q_in = q[cur]; wp.q_in_count = qn[cur];
+        wp.in = q[cur]; wp.in_count = qn[cur];
         HIP_TRY(hipEventRecord(ctx->ev2, st));
         if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
         if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
@@ -2214,8 +2260,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // a smaller share of launch tails.
   uint64_t slot_cap = 40ull << 20;  // C3: 16M -> 435 ms/frame, 24M -> 414, 40M -> 407 (fewer passes, fewer pass tails)
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
-  const uint64_t per_slot = sizeof(RayHot) + sizeof(RayAux) + sizeof(HitSt) + sizeof(PathHot) +
-                            (need_cold ? sizeof(PathCold) : 0) + 3 * sizeof(uint32_t) + (uint64_t)rec_dense * D * sizeof(double);
+  const uint64_t per_slot = 2 * (sizeof(RayOD) + sizeof(uint32_t) + (ctx->sc.tri_only ? 0 : sizeof(double)) + sizeof(PathHot) +
+                                 sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(HitSt)) +
+                            (uint64_t)rec_dense * D * sizeof(double);
   // overflow blocks per 16 slots (C3: ~3% of the paths in flight are deeper than 8)
   uint32_t pool_div = 16;
   if (const char* e = getenv("IZPI_POOL_DIV")) pool_div = (uint32_t)std::max(1, atoi(e));
@@ -2236,12 +2283,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   }
   if ((rc = grow(ctx, (void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)))) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_rhot, &ctx->rhot_cap, (size_t)slots * sizeof(RayHot)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_raux, &ctx->raux_cap, (size_t)slots * sizeof(RayAux)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_hit, &ctx->hit_cap, (size_t)slots * sizeof(HitSt)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_phot, &ctx->phot_cap, (size_t)slots * sizeof(PathHot)))) return rc;
-  if (need_cold && (rc = grow(ctx, (void**)&ctx->d_pcold, &ctx->pcold_cap, (size_t)slots * sizeof(PathCold)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_queue, &ctx->queue_cap, (size_t)2 * slots * sizeof(uint32_t)))) return rc;
+  const bool need_time = !ctx->sc.tri_only;  // only sphere tests read the ray time
+  if ((rc = grow(ctx, (void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, nullptr))))
+    return rc;
+  WaveBuf bufs[2];
+  carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, bufs);
   const size_t nbg = req->num_bg_spd;
   if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
   hipStream_t st = ctx->stream;
@@ -2270,8 +2316,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
   WaveParams wp{};
-  wp.rhot = ctx->d_rhot; wp.raux = ctx->d_raux; wp.hit = ctx->d_hit; wp.phot = ctx->d_phot;
-  wp.pcold = need_cold ? ctx->d_pcold : nullptr; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  // entries other than plain main rays: path-length rays, parked entries, dead entries
+  wp.read_kind = (!ctx->sc.no_pathlen || rec_pool != 0 || spectral || req->max_depth == 0) ? 1u : 0u;
   wp.pool_ctr = sp.pool_ctr;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
@@ -2443,8 +2490,8 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   free_scene(ctx);
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_pool, ctx->d_ring, ctx->d_pool_ctr, ctx->d_running, ctx->d_out,
-                  ctx->d_tiles, ctx->d_utiles, ctx->d_bg, ctx->d_misc, ctx->d_counters, ctx->d_rhot, ctx->d_raux,
-                  ctx->d_hit, ctx->d_phot, ctx->d_pcold, ctx->d_queue, ctx->d_spill, ctx->d_post, ctx->d_share,
+                  ctx->d_tiles, ctx->d_utiles, ctx->d_bg, ctx->d_misc, ctx->d_counters, ctx->d_state,
+                  ctx->d_spill, ctx->d_post, ctx->d_share,
                   ctx->d_gather};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
@@ -2807,19 +2854,20 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (!ctx->have_scene) { ctx->err = "no scene"; return IZPI_ERR_NO_SCENE; }
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
-  double* dr; izpi_hit* dh; RayHot* rr; RayAux* rx; HitSt* hh; uint32_t* q;
+  double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; HitSt* hh;
   HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 8 * sizeof(double)));
   HIP_TRY(hipMalloc((void**)&dh, (size_t)n * sizeof(izpi_hit)));
-  HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayHot)));
-  HIP_TRY(hipMalloc((void**)&rx, (size_t)n * sizeof(RayAux)));
+  HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayOD)));
+  HIP_TRY(hipMalloc((void**)&kk, (size_t)n * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc((void**)&tm, (size_t)n * sizeof(double2)));
   HIP_TRY(hipMalloc((void**)&hh, (size_t)n * sizeof(HitSt)));
-  HIP_TRY(hipMalloc((void**)&q, (size_t)n * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
-  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, rx, q, ctx->d_misc + 3);
+  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, ctx->d_misc + 3);
   WaveParams wp{};
-  wp.rhot = rr; wp.raux = rx; wp.hit = hh; wp.q_in = q; wp.q_in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n;
+  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh;
+  wp.in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n; wp.read_kind = 1;
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;
@@ -2829,7 +2877,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));
-  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(rx); (void)hipFree(hh); (void)hipFree(q);
+  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(kk); (void)hipFree(tm); (void)hipFree(hh);
   return IZPI_OK;
 }
 
