@@ -214,8 +214,11 @@ struct alignas(16) RayOD { double o[3], d[3]; };  // 48 B
 // RAY_PARKED: the entry's shading pass waits for an overflow record block (pool_alloc);
 // k_trace2 skips it and the next k_shade shades the same traced ray again (the pass reads
 // only stored state, so the retry computes exactly what the first attempt would have).
-// RAY_DEAD: an entry reserved for a new path whose sample completed without a ray
-// (spectral pdf 0, maxDepth 0); every kernel skips it.
+// RAY_DEAD: an entry reserved for a new path that has no ray (its sample completed at once:
+// spectral pdf 0, maxDepth 0; or the units ran out); every kernel skips it. Its ray origin
+// x also holds DEAD_BITS, a signalling-NaN pattern no arithmetic produces, so k_trace2
+// tells it apart without reading kind words.
+constexpr uint64_t DEAD_BITS = 0x7FF4DEADDEADDEADull;
 enum { RAY_MAIN = 0, RAY_PATHLEN = 1, RAY_PARKED = 4, RAY_DEAD = 8, KIND_MAT_SHIFT = 4 };
 IZPI_DEV uint32_t kind_of(uint32_t k) { return k & 3u; }
 // Closest hit of an entry's ray: ONE aligned 32-B record (t, primitive, barycentrics).
@@ -391,7 +394,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   const uint32_t n = *wp.in_count;
   if (wp.pool_ctr && blockIdx.x == 0) pool_publish(wp.pool_ctr);
   // kind words other than RAY_MAIN exist only with dielectrics (path-length rays), an
-  // overflow record pool (parked entries), dead entries or explicit tMin / tMax
+  // overflow record pool (parked entries) or explicit tMin / tMax (dead entries are
+  // recognised by their ray)
   const bool read_kind = wp.read_kind != 0;
   // Small queues (the wavefront's tail passes): chunks shrink so the rays spread over
   // more waves, and waves past the last chunk exit at once instead of each paying a
@@ -444,10 +448,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (!busy && rank < take) {
           const uint32_t k = read_kind ? wp.in.kind[my] : (uint32_t)RAY_MAIN;
           // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
-          if (!(k & (RAY_PARKED | RAY_DEAD))) {
+          const RayOD& r = wp.in.ray[my];
+          if (!(k & (RAY_PARKED | RAY_DEAD)) && (uint64_t)__double_as_longlong(r.o[0]) != DEAD_BITS) {
             qi = my;
             lkind = k;
-            const RayOD& r = wp.in.ray[my];
             tmax = ray_tmax(wp.in, my, k);
             main_ray = kind_of(k) == RAY_MAIN;
             ix = (float)(1.0 / r.d[0]); iy = (float)(1.0 / r.d[1]); iz = (float)(1.0 / r.d[2]);
@@ -1112,6 +1116,10 @@ IZPI_DEV void store_entry(const WaveBuf& b, uint32_t pos, const PathSt& P, const
   }
 }
 // A parked entry moves to the output unchanged (its hit record too), flagged RAY_PARKED.
+IZPI_DEV void dead_entry(const WaveBuf& out, uint32_t pos) {
+  out.kind[pos] = RAY_DEAD;
+  out.ray[pos].o[0] = __longlong_as_double((long long)DEAD_BITS);
+}
 IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint32_t pos) {
   out.ray[pos] = in.ray[i];
   out.kind[pos] = in.kind[i] | RAY_PARKED;
@@ -1212,9 +1220,9 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
 // `unit_want` lanes get consecutive output entries, `put` lanes first. A granted lane
 // whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
 IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
-                             uint32_t& pos, uint32_t& parity) {
+                             uint32_t& pos, uint32_t& parity, bool& exhausted) {
   __shared__ uint32_t s_p[2][4], s_u[2][4];
-  __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2];
+  __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2], s_nent[2];
   const uint32_t b = parity;
   parity ^= 1u;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1223,25 +1231,28 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); }
   __syncthreads();
   if (threadIdx.x == 0) {
+    // both atomics in flight together: entries are reserved for every unit_want lane
+    // until this block has seen the unit head run out (`exhausted`, thread 0's register);
+    // a lane reserved an entry but denied a unit leaves a dead entry (at most one
+    // iteration per block, in the frame's last passes)
     const uint32_t np = s_p[b][0] + s_p[b][1] + s_p[b][2] + s_p[b][3];
-    const uint32_t nu = s_u[b][0] + s_u[b][1] + s_u[b][2] + s_u[b][3];
-    uint32_t u0 = 0, granted = 0;
-    if (nu) {
-      u0 = atomicAdd(sp.head, nu);
-      granted = u0 >= sp.total_units ? 0u : min(nu, sp.total_units - u0);
-    }
+    const uint32_t nu = exhausted ? 0u : s_u[b][0] + s_u[b][1] + s_u[b][2] + s_u[b][3];
+    const uint32_t ne = np + nu;
+    const uint32_t u0 = nu ? atomicAdd(sp.head, nu) : sp.total_units;
+    if (u0 + nu >= sp.total_units) exhausted = true;
+    s_pbase[b] = ne ? atomicAdd(out_count, ne) : 0u;
     s_ubase[b] = u0;
-    s_granted[b] = granted;
+    s_granted[b] = u0 >= sp.total_units ? 0u : min(nu, sp.total_units - u0);
     s_nput[b] = np;
-    s_pbase[b] = (np + granted) ? atomicAdd(out_count, np + granted) : 0u;
+    s_nent[b] = ne;
   }
   __syncthreads();
   uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
   for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
-  unit = s_ubase[b] + ur;
+  const bool has_entry = unit_want && s_nput[b] + ur < s_nent[b];
   const bool granted = unit_want && ur < s_granted[b];
-  if (!granted) unit = 0xFFFFFFFFu;
-  pos = put ? s_pbase[b] + pr : (granted ? s_pbase[b] + s_nput[b] + ur : 0xFFFFFFFFu);
+  unit = granted ? s_ubase[b] + ur : 0xFFFFFFFFu;
+  pos = put ? s_pbase[b] + pr : (has_entry ? s_pbase[b] + s_nput[b] + ur : 0xFFFFFFFFu);
 }
 
 // A lane whose path finished got `unit` and entry `pos` (block_reserve2): start the
@@ -1259,7 +1270,7 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
     }
     unit = atomicAdd(sp.head, 1u);
     if (unit >= sp.total_units) {
-      out.kind[pos] = RAY_DEAD;
+      dead_entry(out, pos);
       return;
     }
   }
@@ -1544,7 +1555,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve LDS buffer set
   const uint32_t n = *wp.in_count;
-  const bool read_kind = wp.read_kind != 0;
+  bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * 256;
 #ifdef IZPI_SHADE_CLOCKS
@@ -1565,7 +1576,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     RayRec R;
     P.rslot = 0; P.blk = 0; P.depth = 0;
     uint32_t kind = RAY_DEAD;
-    if (valid) kind = (read_kind ? wp.in.kind[i] : (uint32_t)RAY_MAIN) & ~(uint32_t)RAY_PARKED;  // a parked entry retries
+    if (valid) kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
     const bool live = valid && !(kind & RAY_DEAD);
     if (live) load_path<SAMPLER>(wp.in, i, P);
     if (sp.rec_pool) {  // a path at depth >= rec_dense writes its records to an overflow block
@@ -1585,7 +1596,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     // one reservation phase: output entries for continuing and parked paths, new units
     // (and their entries) for finished ones
     uint32_t unit, pos;
-    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity);
+    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted);
     if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
     if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS
@@ -1594,6 +1605,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     t0 = t1;
 #endif
     if (unit != 0xFFFFFFFFu) refill_one<SAMPLER>(sc, sp, wp.out, unit, pos, P);
+    else if (done && pos != 0xFFFFFFFFu) dead_entry(wp.out, pos);  // entry reserved, the units ran out
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
     k_ref += t1 - t0;
@@ -2317,8 +2329,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
   WaveParams wp{};
   wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
-  // entries other than plain main rays: path-length rays, parked entries, dead entries
-  wp.read_kind = (!ctx->sc.no_pathlen || rec_pool != 0 || spectral || req->max_depth == 0) ? 1u : 0u;
+  // kind words other than plain main rays: path-length rays, parked entries
+  wp.read_kind = (!ctx->sc.no_pathlen || rec_pool != 0) ? 1u : 0u;
   wp.pool_ctr = sp.pool_ctr;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
