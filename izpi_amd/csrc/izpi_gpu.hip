@@ -964,7 +964,7 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
 IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.out + (size_t)unit * 3; }
 
 // Write the finished path's radiance after unwinding the recursion of
-// colour.go:80-94 / sampler/spectral.go:161-174 from depth-1 down to 0.
+// colour.go:44-57 / sampler/spectral.go:60-72 from depth-1 down to 0.
 template <int SAMPLER, bool NO_SPEC = false>
 IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
@@ -1283,7 +1283,7 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
 enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
 
 // One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
-// one bounce deep (colour.go:33-94, sampler/spectral.go:47-80). Sets `push` when the slot
+// one bounce deep (colour.go:33-65, sampler/spectral.go:47-80). Sets `push` when the path
 // has a ray to trace next and `done` when its sample finished.
 // Entry i of `in`: P is its path state (load_path), with blk set to the path's overflow
 // block when it needs one (P.depth >= rec_dense); `kind` its kind word. On return, P and
@@ -1453,7 +1453,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       fblk = P.blk;
     } else {
       if (have_pdf) {
-        // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:85-90, mixture.go:17-33)
+        // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:48-51, mixture.go:17-33)
         V3 dir;
         if (rng.next() < 0.5) dir = lights_random(sc, next_o, rng);
         else dir = cos_onb.local(random_cosine_direction(rng));
@@ -2030,11 +2030,16 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 // Runtime knobs: IZPI_PRIM_W (default 32) weighs primitive steps against node steps
 // (x/16); IZPI_TRACE_CHUNK queue entries per dequeue; IZPI_REFILL_MIN idle lanes per
 // refill. All settings give identical results and counters.
-constexpr int TRACE_RING = 16, TRACE_WPE = 5;
+#ifndef IZPI_TRACE_WPE
+#define IZPI_TRACE_WPE 5
+#endif
+constexpr int TRACE_RING = 16, TRACE_WPE = IZPI_TRACE_WPE;
 struct Tracer {
   bool p2 = true;    // DIST
   bool tri = false;  // TRI
-  uint32_t prim_w = 32, tchunk = 128, refill_min = 16;
+  // queue entries per dequeue and idle lanes per refill, measured on C3: chunk 128 / refill
+  // 16 -> 211 ms of k_trace2 per frame, 512 / 24 -> 201, 1024 -> 207, 2048 -> 216, 64 -> 303
+  uint32_t prim_w = 32, tchunk = 512, refill_min = 24;
   int blocks = 0;
 };
 
