@@ -1,16 +1,18 @@
 #!/bin/bash
-# Profiling recipe for the bench workload (run on the GPU box from the repo root).
-#   pass 1: kernel trace + stats (per-kernel durations)      -> gpurun_out/prof_$TAG/trace
-#   pass 2: PMC FETCH_SIZE (HBM read bytes, gfx950 reports 1/2 of wide reads)
-#   pass 3: PMC WRITE_SIZE
-# Counters are collected in their own passes with --kernel-trace only (no sys/runtime trace).
+# Profiling recipe for the bench workload (run on the GPU box from the repo root):
+#   bash profiles/run_profile.sh TAG
+# 1. the bench itself (its own PMC passes, CPU baseline, reference-tree check) -> bench.json
+# 2. rocprofv3 --kernel-trace --stats over the same timed frames (no PMC children, no
+#    CPU baseline: a profiler must not run inside a profiler) -> kernel_stats.csv
 set -e
-TAG=${1:-r1}
-SPP=${2:-512}
+TAG=${1:-r2}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-reference-check --spp $SPP > $OUT/bench_trace.log 2>&1
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-reference-check --spp $SPP > $OUT/bench_fetch.log 2>&1
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-reference-check --spp $SPP > $OUT/bench_write.log 2>&1
-find $OUT -name "*.csv" | head -20
+timeout -k 10 600 python3 bench.py > $OUT/bench.log 2>&1
+grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-pmc --no-cpu-baseline --no-reference-check > $OUT/bench_trace.log 2>&1
+find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+grep '^{' $OUT/bench_trace.log | tail -1 > $OUT/bench_under_rocprof.json
+head -5 $OUT/kernel_stats.csv
+python3 -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['cpu_baseline']['value'])"
