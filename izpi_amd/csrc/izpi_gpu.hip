@@ -1946,6 +1946,7 @@ struct izpi_ctx {
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
+  uint32_t pool_grow = 0;        // overflow pool doublings earned by frames that parked (render_impl)
 };
 
 namespace {
@@ -2280,8 +2281,13 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const uint64_t per_slot = 2 * (sizeof(RayOD) + sizeof(uint32_t) + (ctx->sc.tri_only ? 0 : sizeof(double)) + sizeof(PathHot) +
                                  sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(HitSt)) +
                             (uint64_t)rec_dense * D * sizeof(double);
-  // overflow blocks per 16 slots (C3: ~3% of the paths in flight are deeper than 8)
-  uint32_t pool_div = 16;
+  // Overflow blocks per slot. Lambert/light scenes: 1 per 16 slots (C3: ~3% of the paths
+  // in flight are deeper than 8). Scenes with specular materials or the spectral sampler
+  // run deep chains through glass: 1 per 4 slots (C5 at 1 per 16 parked 29% of its
+  // shading items, 574 -> 502 ms per 16-spp frame with no parks at 1 per 4). A frame that
+  // still parks more than 1/64 of its rays doubles the pool for the renderer's next frame.
+  uint32_t pool_div = (spectral || !ctx->basic_materials) ? 4u : 16u;
+  pool_div = std::max(1u, pool_div >> std::min(ctx->pool_grow, 4u));
   if (const char* e = getenv("IZPI_POOL_DIV")) pool_div = (uint32_t)std::max(1, atoi(e));
   const uint64_t per_block = (uint64_t)rec_pool * D * sizeof(double) + sizeof(uint32_t);
   if (avail > 0)  // the wavefront state within half of the HBM
@@ -2374,6 +2380,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.workspace_bytes = workspace_bytes(ctx);
   s.scene_bytes = ctx->scene_bytes;
   s.slots = slots; s.rec_dense = rec_dense; s.pool_blocks = pool_blocks; s.chunk_spp = chunk;
+  if (rec_pool && s.parks * 64 > s.rays && pool_blocks < slots) ctx->pool_grow++;
 #ifdef IZPI_SHADE_CLOCKS
   fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu (wave cycles)\n", cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL],
           cnt[CNT_SCLK_PUSH]);
@@ -2631,6 +2638,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   std::vector<uint32_t> mflags(d->num_materials, 0);
   ctx->mat_ok_rgb = ctx->mat_ok_spectral = true;
   ctx->basic_materials = true;
+  ctx->pool_grow = 0;
   for (uint32_t i = 0; i < d->num_materials; i++) {
     const izpi_material& m = d->materials[i];
     const int32_t ids[] = {m.albedo_tex, m.spectral_tex, m.normal_tex, m.roughness_tex, m.metalness_tex, m.absorb_tex};

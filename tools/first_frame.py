@@ -35,7 +35,8 @@ def main():
         dt = time.perf_counter() - t
         free, _ = torch.cuda.mem_get_info(0)
         out["frames"].append({"wall_ms": dt * 1e3, "device_ms": r.stats["total_ms"], "trace_ms": r.stats["kernel_ms"],
-                              "shade_ms": r.stats["shade_ms"], "hbm_used_gb": (free0 - free) / 1e9})
+                              "shade_ms": r.stats["shade_ms"], "tail_ms": r.stats["tail_ms"],
+                              "rays": r.stats["rays"], "parks": r.stats["parks"], "hbm_used_gb": (free0 - free) / 1e9})
         print(json.dumps(out["frames"][-1]), flush=True)
     r.close()
     print(json.dumps(out), flush=True)

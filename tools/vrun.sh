@@ -11,6 +11,6 @@ for r in $(seq 1 $R); do
     env $lib $envs timeout -k 10 300 python tools/first_frame.py --config $CFG --spp $SPP --frames 3 2>&1 | grep '^{"config' | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read()); f=d['frames'][1:]
-print('$name', 'device_ms %.1f trace %.1f shade %.1f hbm %.1f' % tuple(sum(x[k] for x in f)/len(f) for k in ('device_ms','trace_ms','shade_ms','hbm_used_gb')))" || exit 1
+print('$name', 'device_ms %.1f trace %.1f shade %.1f tail %.1f rays %.0f parks %.0f hbm %.1f' % tuple(sum(x[k] for x in f)/len(f) for k in ('device_ms','trace_ms','shade_ms','tail_ms','rays','parks','hbm_used_gb')))" || exit 1
   done
 done
