@@ -47,16 +47,17 @@ struct alignas(16) GPrim {
   uint32_t index;   // transport-order index (shading data, lights)
 };
 // Shading record of a primitive, in BVH leaf order next to GPrim: everything the
-// deferred hit record and a constant-textured Lambert / DiffuseLight bounce need, in one
-// 64-B line (the material and texture records are then not read).
-struct alignas(64) GShade {
+// deferred hit record needs, in 32 B (half a 64-B line: one sector per closest hit). The
+// material's constant RGB albedo / emit value, when it has one, is in DevScene::mat_const.
+struct alignas(32) GShade {
   double n[3];      // triangle: unit(e1 x e2) (triangle.go:100); sphere: unused
-  uint32_t mat;     // material index
   uint32_t ref;     // IZPI_PRIM_REF(kind, transport index)
-  double c[3];      // value of the material's constant RGB albedo / emit texture (cflags bit0)
-  uint32_t kind;    // material kind (izpi_material.kind)
-  uint32_t cflags;  // bit0: c is valid; bit1: a texture of the material reads the hit (u,v)
+  uint32_t mk;      // material index << 8 | material kind << 2 | cflags
+                    // (cflags bit0: mat_const holds the albedo; bit1: a texture of the material reads the hit (u,v))
 };
+__host__ __device__ inline uint32_t gs_mat(const GShade& g) { return g.mk >> 8; }
+__host__ __device__ inline uint32_t gs_kind(const GShade& g) { return (g.mk >> 2) & 63u; }
+__host__ __device__ inline uint32_t gs_cflags(const GShade& g) { return g.mk & 3u; }
 // Light record (Scene.Lights entry, transport order): everything PDFValue/Random read.
 struct alignas(16) GLight {
   double v0[3], v1[3], v2[3], e1[3], e2[3], n[3];  // triangle
@@ -81,6 +82,7 @@ struct DevScene {
   const izpi_material* materials;
   const izpi_texture* textures;
   const uint32_t* mat_flags;    // per material: bit0 needs hit-record UVs (image textures)
+  const double4* mat_const;     // per material: its constant RGB albedo / emit texture value (GShade cflags bit0)
   const double* texels;
   const double* spd_wl;
   const double* spd_val;

@@ -771,7 +771,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
                          bool want_uv, HitRec& h) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
-  h.mat = gs.mat;
+  h.mat = gs_mat(gs);
   if (IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
     const uint32_t ti = IZPI_PRIM_INDEX(gs.ref);
     V3 n = mk(gs.n[0], gs.n[1], gs.n[2]);
@@ -1338,17 +1338,19 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs.cflags & 2u) != 0, h);
+    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h);
     hit_n = h.n;
     next_o = h.p;
     // the shade record carries the material kind and, for a constant RGB texture, its
     // value: the common Lambert/light hit reads no material or texture record
     const izpi_material& m = sc.materials[h.mat];
-    const bool cconst = COLOUR && (gs.cflags & 1u) != 0;
-    switch (gs.kind) {
+    const bool cconst = COLOUR && (gs_cflags(gs) & 1u) != 0;
+    V3 cval = mk(0, 0, 0);
+    if (cconst) { const double4 c4 = sc.mat_const[h.mat]; cval = mk(c4.x, c4.y, c4.z); }
+    switch (gs_kind(gs)) {
       case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
         if (dot(h.n, rd) < 0.0) {
-          if (cconst) L = mk(gs.c[0], gs.c[1], gs.c[2]);
+          if (cconst) L = cval;
           else if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
           else L.x = tex_spectral(sc, m.spectral_tex, P.lambda);
         }
@@ -1359,7 +1361,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         rng.next();
         rng.next();
         cos_onb.build(h.n);
-        if (cconst) att = mk(gs.c[0], gs.c[1], gs.c[2]);
+        if (cconst) att = cval;
         else if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
         else att.x = tex_spectral(sc, m.spectral_tex, P.lambda);
         have_pdf = true;
@@ -2597,12 +2599,12 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     if (kind == IZPI_PRIM_TRIANGLE) {
       if (idx >= nt) { ctx->err = "triangle ref out of range"; return IZPI_ERR_INVALID; }
       memcpy(gs.n, d->tri_normal + 3 * (size_t)idx, 24);
-      gs.mat = d->tri_mat[idx];
+      gs.mk = d->tri_mat[idx];
       memcpy(g.a, d->tri_v0 + 3 * (size_t)idx, 24); memcpy(g.a + 3, d->tri_e1 + 3 * (size_t)idx, 24);
       memcpy(g.a + 6, d->tri_e2 + 3 * (size_t)idx, 24);
     } else {
       if (idx >= ns) { ctx->err = "sphere ref out of range"; return IZPI_ERR_INVALID; }
-      gs.mat = d->sph_mat[idx];
+      gs.mk = d->sph_mat[idx];
       memcpy(g.a, d->sph_center0 + 3 * (size_t)idx, 24); memcpy(g.a + 3, d->sph_center1 + 3 * (size_t)idx, 24);
       g.a[6] = d->sph_radius[idx]; g.a[7] = d->sph_time[2 * (size_t)idx]; g.a[8] = d->sph_time[2 * (size_t)idx + 1];
     }
@@ -2667,16 +2669,25 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     if (spec) mflags[i] |= 4u; else ctx->mat_ok_spectral = false;
   }
   // ---- material essentials in the per-primitive shade records
-  for (GShade& gs : shade) {
-    if (gs.mat >= d->num_materials) { ctx->err = "material index out of range"; return IZPI_ERR_INVALID; }
-    const izpi_material& m = d->materials[gs.mat];
-    gs.kind = m.kind;
-    gs.cflags = (mflags[gs.mat] & 1u) ? 2u : 0u;
+  // (gs.mk holds the bare material index until here)
+  if (d->num_materials >= (1u << 24)) { ctx->err = "too many materials"; return IZPI_ERR_INVALID; }
+  std::vector<double4> mconst(std::max<uint32_t>(1, d->num_materials), make_double4(0, 0, 0, 0));
+  std::vector<uint32_t> mcflags(d->num_materials, 0);
+  for (uint32_t i = 0; i < d->num_materials; i++) {
+    const izpi_material& m = d->materials[i];
+    mcflags[i] = (mflags[i] & 1u) ? 2u : 0u;
     if ((m.kind == IZPI_MAT_LAMBERT || m.kind == IZPI_MAT_DIFFUSE_LIGHT) && m.albedo_tex >= 0 &&
         d->textures[m.albedo_tex].kind == IZPI_TEX_CONSTANT) {
-      memcpy(gs.c, d->textures[m.albedo_tex].value, 24);
-      gs.cflags |= 1u;
+      const double* v = d->textures[m.albedo_tex].value;
+      mconst[i] = make_double4(v[0], v[1], v[2], 0.0);
+      mcflags[i] |= 1u;
     }
+  }
+  for (GShade& gs : shade) {
+    const uint32_t mat = gs.mk;
+    if (mat >= d->num_materials) { ctx->err = "material index out of range"; return IZPI_ERR_INVALID; }
+    if (d->materials[mat].kind >= 64u) { ctx->err = "unknown material kind"; return IZPI_ERR_INVALID; }
+    gs.mk = mat << 8 | d->materials[mat].kind << 2 | mcflags[mat];
   }
   // ---- upload
   DevScene& sc = ctx->sc;
@@ -2698,6 +2709,8 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(lights.data(), lights.size(), &dlt);
   UP(d->materials, d->num_materials, &dm);
   UP(mflags.data(), mflags.size(), &dmf);
+  double4* dmc;
+  UP(mconst.data(), mconst.size(), &dmc);
   // device copy of the textures: pad0 = 1 marks a tabulated SPD with non-decreasing
   // wavelengths, which tex_spectral searches by bisection
   std::vector<izpi_texture> texs(d->textures, d->textures + d->num_textures);
@@ -2716,7 +2729,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(d->spd_values, d->num_spd, &dsv);
   sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tri_normal = dn; sc.tri_uv = duv; sc.tri_tangent = dtg;
   sc.tri_bitangent = dbt; sc.tri_mat = dtm; sc.sph_mat = dsm; sc.lights = dlt; sc.materials = dm;
-  sc.mat_flags = dmf; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
+  sc.mat_flags = dmf; sc.mat_const = dmc; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
   sc.tri_only = d->num_spheres == 0 ? 1u : 0u;
