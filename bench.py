@@ -443,11 +443,14 @@ def main():
         roof["achieved"] = round(t["bytes_per_frame"] / (trace_ms_frame * 1e-3) / 1e9, 2)
         roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
         roof["traffic_per_frame"] = t["bytes_per_frame"]
+        roof["fetch_per_frame"] = t["fetch_bytes_per_frame"]
+        roof["write_per_frame"] = t["write_bytes_per_frame"]
         roof["tcc_hit_rate"] = t["tcc_hit_rate"]
         roof["pmc_dispatches"] = t["dispatches"]
         if "k_shade" in pmc:
             s = pmc["k_shade"]
-            roof["k_shade"] = {"bytes_per_frame": s["bytes_per_frame"], "tcc_hit_rate": s["tcc_hit_rate"],
+            roof["k_shade"] = {"bytes_per_frame": s["bytes_per_frame"], "fetch_per_frame": s["fetch_bytes_per_frame"],
+                               "write_per_frame": s["write_bytes_per_frame"], "tcc_hit_rate": s["tcc_hit_rate"],
                                "achieved": round(s["bytes_per_frame"] / (agg["shade_ms"] / steps * 1e-3) / 1e9, 2)}
     elif pmc.get("error"):
         roof["pmc_error"] = pmc["error"]

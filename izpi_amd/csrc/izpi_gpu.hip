@@ -923,6 +923,7 @@ struct ShadeParams {
   double* out;                 // [total_units][3] per-sample result
   double* recs;                // [slots][rec_dense][D] unwinding records
   double* pool;                // [blocks][rec_pool][D] overflow unwinding records
+  const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
   uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
@@ -938,24 +939,46 @@ struct ShadeParams {
 // the paths in flight at depth >= 8), so the deeper levels live in overflow blocks of
 // rec_pool levels, taken by a path when it reaches depth rec_dense and returned when it
 // finishes: the state of 40M slots at maxDepth 50 takes ~20 GB instead of ~100 GB.
-template <int SAMPLER>
+// MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
+// DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
+// footprint small; MATSET_CONST is MATSET_BASIC for scenes whose albedos are all
+// constant RGB textures (Colour sampler): a bounce's attenuation is then its material's
+// constant, so its unwinding record holds the material instead of the colour (24 B
+// instead of 48 B); MATSET_FULL adds Dielectric, Metal and PBR. The host picks the
+// variant from the scene's materials (results are identical).
+enum { MATSET_BASIC = 0, MATSET_FULL = 1, MATSET_CONST = 2 };
+// Record: Colour (flag, att xyz, s, p); Colour + MATSET_CONST (material, s, p); Spectral
+// (flag, att, s, p). p is always last.
+template <int SAMPLER, int MATSET>
 struct RecLayout {
-  static constexpr uint32_t D = SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 4;  // doubles per record
-  static constexpr uint32_t S = D - 2;                                   // index of s (p follows)
+  static constexpr bool COMPACT = SAMPLER == IZPI_SAMPLER_COLOUR && MATSET == MATSET_CONST;
+  static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 4);  // doubles per record
+  static constexpr uint32_t P = D - 1;                                                   // index of p
 };
-template <int SAMPLER>
+template <int SAMPLER, int MATSET>
 IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth) {
-  constexpr uint32_t D = RecLayout<SAMPLER>::D;
+  constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
   if (depth < sp.rec_dense) return sp.recs + ((size_t)rslot * sp.rec_dense + depth) * D;
   return sp.pool + ((size_t)(blk - 1) * sp.rec_pool + (depth - sp.rec_dense)) * D;
 }
-template <int SAMPLER>
+// A bounce's record without p (written once the light pdf is known).
+template <int SAMPLER, int MATSET>
 IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth, bool spec, V3 att, double s,
-                        double p) {
-  double2* r = reinterpret_cast<double2*>(rec_ptr<SAMPLER>(sp, rslot, blk, depth));
+                        uint32_t mat) {
+  double* rp = rec_ptr<SAMPLER, MATSET>(sp, rslot, blk, depth);
+  if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {  // never specular
+    rp[0] = (double)mat;
+    rp[1] = s;
+    return;
+  }
+  double2* r = reinterpret_cast<double2*>(rp);
   r[0] = make_double2(spec ? 1.0 : 0.0, att.x);
-  if (SAMPLER == IZPI_SAMPLER_COLOUR) r[1] = make_double2(att.y, att.z);
-  if (!spec) r[RecLayout<SAMPLER>::S / 2] = make_double2(s, p);
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) {
+    r[1] = make_double2(att.y, att.z);
+    if (!spec) rp[4] = s;
+  } else {
+    if (!spec) rp[2] = s;
+  }
 }
 
 // Result slot of work unit `unit` (= pixel * chunk_spp + sample). Unit-major: paths of
@@ -965,8 +988,9 @@ IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.ou
 
 // Write the finished path's radiance after unwinding the recursion of
 // colour.go:44-57 / sampler/spectral.go:60-72 from depth-1 down to 0.
-template <int SAMPLER, bool NO_SPEC = false>
+template <int SAMPLER, int MATSET>
 IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
+  constexpr bool NO_SPEC = MATSET != MATSET_FULL;
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
     // +0 radiance through only non-specular records: every level computes
     // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
@@ -977,14 +1001,42 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   }
   // The records are read four levels at a time (one batch of independent loads, then
   // the levels applied in order), so a path of depth d waits ~d/4 memory round trips.
-  constexpr uint32_t D = RecLayout<SAMPLER>::D;
+  constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
   constexpr int RB = 4;
   for (int dd = (int)P.depth - 1; dd >= 0; dd -= RB) {
     double rv[RB][D];
+    if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {
+      // (material, s, p): the attenuation is the material's constant albedo
+      double cv[RB][3];
+#pragma unroll
+      for (int j = 0; j < RB; j++) {
+        if (dd - j >= 0) {
+          const double* r = rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j));
+          rv[j][0] = r[0]; rv[j][1] = r[1]; rv[j][2] = r[2];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RB; j++) {
+        if (dd - j >= 0) {
+          const double4 c = sp.mat_const[(uint32_t)rv[j][0]];
+          cv[j][0] = c.x; cv[j][1] = c.y; cv[j][2] = c.z;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RB; j++) {
+        if (dd - j < 0) break;
+        const V3 att = mk(cv[j][0], cv[j][1], cv[j][2]);
+        V3 v1 = smul(L, rv[j][1]);                         // ScalarMul(Sample(...), ScatteringPDF)
+        V3 v2 = mul(att, v1);
+        V3 v3 = sdiv(v2, rv[j][2]);
+        L = mk(0.0 + v3.x, 0.0 + v3.y, 0.0 + v3.z);        // Add(emitted == 0, v3)
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < RB; j++) {
       if (dd - j >= 0) {
-        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER>(sp, P.rslot, P.blk, (uint32_t)(dd - j)));
+        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j)));
 #pragma unroll
         for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
       }
@@ -1086,7 +1138,7 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
   V3 rd = sub(sub(add(add(ld3(c.lower_left), smul(ld3(c.horizontal), u)), smul(ld3(c.vertical), v)), origin), offset);
   P.rng = rng.s;
   if (sp.max_depth == 0) {
-    finish<SAMPLER>(sp, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));
+    finish<SAMPLER, MATSET_FULL>(sp, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));  // depth 0: reads no record
     return false;
   }
   R.o[0] = ro.x; R.o[1] = ro.y; R.o[2] = ro.z;
@@ -1276,11 +1328,6 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
   }
 }
 
-// MATSET selects the compiled material code: MATSET_BASIC covers Lambertian +
-// DiffuseLight only (the Cornell/dragon configs) and keeps the kernel's register
-// footprint small; MATSET_FULL adds Dielectric, Metal and PBR. The host picks the
-// variant from the scene's material kinds (results are identical).
-enum { MATSET_BASIC = 0, MATSET_FULL = 1 };
 
 // One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
 // one bounce deep (colour.go:33-65, sampler/spectral.go:47-80). Sets `push` when the path
@@ -1312,6 +1359,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   bool spec = false, have_pdf = false;
   V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
   V3 hit_n = mk(0, 0, 0);
+  uint32_t rec_mat = 0;
   Onb cos_onb;
   if (MATSET == MATSET_FULL && kind_of(R.kind) == RAY_PATHLEN) {
     // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
@@ -1340,6 +1388,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
     HitRec h;
     hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h);
     hit_n = h.n;
+    rec_mat = h.mat;
     next_o = h.p;
     // the shade record carries the material kind and, for a constant RGB texture, its
     // value: the common Lambert/light hit reads no material or texture record
@@ -1368,7 +1417,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         break;
       }
       case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
-        if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
         const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
         bool reflected;
         next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
@@ -1389,7 +1438,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         break;
       }
       case IZPI_MAT_METAL: {  // metal.go:34-41 (RGB only: SpectralScatter is nonSpectral)
-        if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
         if (!COLOUR) { terminal = true; break; }
         V3 reflected = reflect(unit(rd), h.n);
         next_d = add(reflected, smul(random_in_unit_sphere(rng), m.fuzz));
@@ -1398,7 +1447,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         break;
       }
       case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
-        if constexpr (MATSET == MATSET_BASIC) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
         double alb_s = 0;
         if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
         else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda);
@@ -1450,7 +1499,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   }
   if (!push) {
     if (terminal) {
-      finish<SAMPLER, MATSET == MATSET_BASIC>(sp, P, L);
+      finish<SAMPLER, MATSET>(sp, P, L);
       done = true;
       fblk = P.blk;
     } else {
@@ -1466,17 +1515,17 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
         double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
         if (sc_cos < 0) sc_cos = 0;
-        rec_store<SAMPLER>(sp, P.rslot, P.blk, P.depth, false, att, sc_cos / 3.141592653589793, 0);
+        rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, sc_cos / 3.141592653589793, rec_mat);
         const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
-        rec_ptr<SAMPLER>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER>::S + 1] = pdf_val;
+        rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
         next_d = dir;
       } else {
-        rec_store<SAMPLER>(sp, P.rslot, P.blk, P.depth, true, att, 0, 0);
+        rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, true, att, 0, rec_mat);
       }
       P.depth++;
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
-        finish<SAMPLER>(sp, P, terminal_max_depth(sp, P, COLOUR));
+        finish<SAMPLER, MATSET>(sp, P, terminal_max_depth(sp, P, COLOUR));
         done = true;
         fblk = P.blk;
       } else {
@@ -1552,7 +1601,7 @@ IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
 #endif
 template <int SAMPLER, int MATSET>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET == MATSET_BASIC && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET != MATSET_FULL && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve LDS buffer set
@@ -1948,6 +1997,7 @@ struct izpi_ctx {
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
+  bool const_albedo = false;     // ... and every albedo / emit texture a constant RGB: MATSET_CONST (Colour)
   uint32_t pool_grow = 0;        // overflow pool doublings earned by frames that parked (render_impl)
 };
 
@@ -2268,7 +2318,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // blocks (ShadeParams::rec_pool). Colour records are 48 B, spectral 32 B, and spectral
   // glass paths run deeper, hence the larger dense part there.
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
-  const uint32_t D = spectral ? RecLayout<IZPI_SAMPLER_SPECTRAL>::D : RecLayout<IZPI_SAMPLER_COLOUR>::D;
+  const bool compact = !spectral && ctx->basic_materials && ctx->const_albedo;
+  const uint32_t D = spectral  ? RecLayout<IZPI_SAMPLER_SPECTRAL, MATSET_FULL>::D
+                     : compact ? RecLayout<IZPI_SAMPLER_COLOUR, MATSET_CONST>::D
+                               : RecLayout<IZPI_SAMPLER_COLOUR, MATSET_FULL>::D;
   const uint32_t max_depth = std::max(1u, req->max_depth);
   uint32_t rec_dense = spectral ? 16u : 8u;
   if (const char* e = getenv("IZPI_REC_DENSE")) rec_dense = (uint32_t)std::max(1, atoi(e));
@@ -2336,7 +2389,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.rec_dense = rec_dense; sp.rec_pool = rec_pool;
   sp.pool_shift = 0;
   while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
-  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.head = ctx->d_misc;
+  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = ctx->sc.mat_const; sp.head = ctx->d_misc;
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
@@ -2356,7 +2409,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
 #define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches)
   const bool basic = ctx->basic_materials;
   if (req->sampler == IZPI_SAMPLER_COLOUR)
-    rc = basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
+    rc = compact ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_CONST)
+         : basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC)
+                 : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
   else
     rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_FULL);
 #undef IZPI_RUN
@@ -2683,6 +2738,10 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       mcflags[i] |= 1u;
     }
   }
+  ctx->const_albedo = true;
+  for (uint32_t i = 0; i < d->num_materials; i++)
+    if ((d->materials[i].kind == IZPI_MAT_LAMBERT || d->materials[i].kind == IZPI_MAT_DIFFUSE_LIGHT) && !(mcflags[i] & 1u))
+      ctx->const_albedo = false;
   for (GShade& gs : shade) {
     const uint32_t mat = gs.mk;
     if (mat >= d->num_materials) { ctx->err = "material index out of range"; return IZPI_ERR_INVALID; }
