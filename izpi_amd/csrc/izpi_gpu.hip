@@ -258,6 +258,7 @@ struct WaveParams {
   unsigned long long* pool_ctr;  // overflow-record ring counters (k_trace2 publishes frees), or null
   uint32_t slots;
   uint32_t read_kind;         // entries other than plain RAY_MAIN rays can occur (k_trace2 reads kind words)
+  uint32_t hit_uv;            // k_shade may read a hit's (u, v): spheres (the root) or (u,v)-reading textures
 };
 IZPI_DEV double ray_tmin(const WaveBuf& b, uint32_t i, uint32_t kind) {
   return b.tminmax ? b.tminmax[i].x : (kind_of(kind) == RAY_PATHLEN ? 0.0 : 0.001);
@@ -730,7 +731,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
         const double2 uv = bprim >= 0 ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        wp.in.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
+        if (wp.hit_uv) {
+          wp.in.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
+        } else {  // nothing reads (u, v): half the record
+          *reinterpret_cast<double2*>(wp.in.hit + qi) = make_double2(bprim >= 0 ? tmax : 0.0, __hiloint2double(0, bprim));
+        }
         busy = false;
       }
     }
@@ -1998,6 +2003,7 @@ struct izpi_ctx {
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
   bool const_albedo = false;     // ... and every albedo / emit texture a constant RGB: MATSET_CONST (Colour)
+  bool any_uv = false;           // a material reads the hit's (u, v) (image textures)
   uint32_t pool_grow = 0;        // overflow pool doublings earned by frames that parked (render_impl)
 };
 
@@ -2397,6 +2403,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
   // kind words other than plain main rays: path-length rays, parked entries
   wp.read_kind = (!ctx->sc.no_pathlen || rec_pool != 0) ? 1u : 0u;
+  wp.hit_uv = (!ctx->sc.tri_only || ctx->any_uv) ? 1u : 0u;
   wp.pool_ctr = sp.pool_ctr;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
@@ -2739,6 +2746,9 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     }
   }
   ctx->const_albedo = true;
+  ctx->any_uv = false;
+  for (uint32_t i = 0; i < d->num_materials; i++)
+    if (mflags[i] & 1u) ctx->any_uv = true;
   for (uint32_t i = 0; i < d->num_materials; i++)
     if ((d->materials[i].kind == IZPI_MAT_LAMBERT || d->materials[i].kind == IZPI_MAT_DIFFUSE_LIGHT) && !(mcflags[i] & 1u))
       ctx->const_albedo = false;
@@ -2964,7 +2974,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, ctx->d_misc + 3);
   WaveParams wp{};
   wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh;
-  wp.in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n; wp.read_kind = 1;
+  wp.in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
   int rc = make_tracer(ctx, &tr);
   if (rc) return rc;

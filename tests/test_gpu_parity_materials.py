@@ -106,3 +106,34 @@ def test_thin_lens_camera_bitwise(gpu, sampler):
     scene.set_camera((50, 50, -140), (50, 50, 0), (0, 1, 0), 40, 1.0, 0.0, 190.0, 0.25, 0.75)
     pin, _ = oracle_canvas(scene, 40, 40, 6, sampler)
     assert pin.tobytes() != ref.tobytes()
+
+
+def textured_lambert_box():
+    """Lambert walls with an image albedo (image.go:73-101) and UVs, next to constant ones:
+    Lambert + DiffuseLight only, so the MATSET_BASIC shader with full (colour) unwinding
+    records runs; the all-constant scenes take MATSET_CONST's (material, s, p) records."""
+    s = Scene("textured_lambert")
+    alb, _, _, _ = configs._pbr_textures(s, res=32)
+    mats = configs.rgb_box_materials(s)
+    mats["White"] = s.lambert(albedo=alb)
+    for v0, v1, v2, mname, _ in configs._BOX:
+        P = np.array([v0, v1, v2], np.float64)
+        span = P.max(0) - P.min(0)
+        ax = [i for i in range(3) if span[i] > 0][:2]
+        uv = [(P[k, ax[0]] / 100.0, P[k, ax[1]] / 100.0) for k in range(3)]
+        s.add_triangles([v0], [v1], [v2], mats[mname], uv=[[c for p in uv for c in p]])
+    s.add_sphere((35, 20, 45), 18, s.lambert(albedo=alb))
+    configs.cornell_camera(s, 1.0)
+    return s
+
+
+@pytest.mark.parametrize("env", [{}, {"IZPI_REC_DENSE": "2", "IZPI_POOL_DIV": "100000"}])
+def test_textured_lambert_bitwise(gpu, env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scene = textured_lambert_box()
+    r = GPURenderer(scene, 48, 48, 8)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
