@@ -50,7 +50,9 @@ enum {
   IZPI_TEX_CONSTANT = 1,           /* texture.Constant (constant.go:20) */
   IZPI_TEX_IMAGE = 3,              /* texture.ImageTxt, float64 NRGBA (image.go:73-101) */
   IZPI_TEX_SPECTRAL_GAUSSIAN = 5,  /* SpectralConstant, Gaussian (spectral_constant.go:72) */
-  IZPI_TEX_SPECTRAL_TABULATED = 7  /* SpectralConstant from SPD (spectral_constant.go:77-106) */
+  IZPI_TEX_SPECTRAL_TABULATED = 7, /* SpectralConstant from SPD (spectral_constant.go:77-106) */
+  IZPI_TEX_SPECTRAL_IMAGE = 9      /* texture.SpectralImage of an IMAGE texture's texels (spectral_image.go:64-259;
+                                      transport.go:486-497): width/height/texel_offset as IMAGE */
 };
 
 typedef struct izpi_texture {
@@ -68,6 +70,7 @@ typedef struct izpi_texture {
 enum {
   IZPI_MAT_DIELECTRIC = 1,    /* dielectric.go */
   IZPI_MAT_DIFFUSE_LIGHT = 2, /* diffuselight.go */
+  IZPI_MAT_ISOTROPIC = 3,     /* isotropic.go (RGB albedo; transport.go:269-289) */
   IZPI_MAT_LAMBERT = 4,       /* lambertian.go */
   IZPI_MAT_METAL = 5,         /* metal.go */
   IZPI_MAT_PBR = 6            /* pbr.go */
@@ -77,9 +80,10 @@ enum {
 
 typedef struct izpi_material {
   uint32_t kind;
-  int32_t albedo_tex;     /* LAMBERT/PBR albedo, DIFFUSE_LIGHT emit (RGB texture), -1 none */
+  int32_t albedo_tex;     /* LAMBERT/PBR/ISOTROPIC albedo, DIFFUSE_LIGHT emit (RGB texture), -1 none */
   int32_t spectral_tex;   /* LAMBERT spectral albedo, DIFFUSE_LIGHT spectral emit,
-                             DIELECTRIC spectral refractive index, PBR spectral albedo */
+                             DIELECTRIC spectral refractive index, PBR spectral albedo
+                             (LAMBERT / DIFFUSE_LIGHT / PBR may use a SPECTRAL_IMAGE) */
   int32_t normal_tex;     /* PBR normal map (also read by Triangle.Hit, triangle.go:250) */
   int32_t roughness_tex;  /* PBR */
   int32_t metalness_tex;  /* PBR */

@@ -22,8 +22,8 @@ COMM_ID_BYTES = 128
 IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE = range(6)
 IZPI_ABI_VERSION = 1
 PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
-TEX_CONSTANT, TEX_IMAGE, TEX_SPECTRAL_GAUSSIAN, TEX_SPECTRAL_TABULATED = 1, 3, 5, 7
-MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_LAMBERT, MAT_METAL, MAT_PBR = 1, 2, 4, 5, 6
+TEX_CONSTANT, TEX_IMAGE, TEX_SPECTRAL_GAUSSIAN, TEX_SPECTRAL_TABULATED, TEX_SPECTRAL_IMAGE = 1, 3, 5, 7, 9
+MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC, MAT_LAMBERT, MAT_METAL, MAT_PBR = 1, 2, 3, 4, 5, 6
 MATF_BEER_LAMBERT = 1
 SAMPLER_COLOUR, SAMPLER_SPECTRAL = 2, 5
 OUT_CANVAS, OUT_PACKED = 0, 1

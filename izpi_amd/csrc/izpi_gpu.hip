@@ -102,9 +102,50 @@ IZPI_DEV uint32_t sorted_interval(const double* wl, uint32_t n, double w) {
   return lo - 1;
 }
 
-// texture.SpectralConstant.Value (spectral_constant.go:65-106)
-IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda) {
+// SpectralImage.rgbToSpectralValue (spectral_image.go:130-190): the spectral value of an
+// RGB texel at a bucket wavelength.
+IZPI_DEV double spectral_image_value(double r, double g, double b, double wl) {
+  double sv = 0;
+  if (wl >= 580.0 && wl <= 750.0) {  // red: Gaussian falloff around 650 nm, width 60
+    const double dist = gm::abs(wl - 650.0);
+    sv += r * gm::exp(-(dist * dist) / (2.0 * 60.0 * 60.0));
+  }
+  if (wl >= 480.0 && wl <= 620.0) {  // green: around 550 nm
+    const double dist = gm::abs(wl - 550.0);
+    sv += g * gm::exp(-(dist * dist) / (2.0 * 60.0 * 60.0));
+  }
+  if (wl >= 380.0 && wl <= 520.0) {  // blue: around 450 nm
+    const double dist = gm::abs(wl - 450.0);
+    sv += b * gm::exp(-(dist * dist) / (2.0 * 60.0 * 60.0));
+  }
+  if (gm::abs(r - g) < 0.15 && gm::abs(g - b) < 0.15 && gm::abs(r - b) < 0.15) sv = gm::max(sv, gm::max(r, gm::max(g, b)));
+  const double mx = gm::max(r, gm::max(g, b));
+  if (mx > 0.7 && sv < mx * 0.8) sv = gm::max(sv, mx * 0.8);
+  return gm::max(0.0, gm::min(1.0, sv));
+}
+// SpectralImage.Value (spectral_image.go:193-259): the texel ImageTxt.Value reads, at the
+// first 5-nm bucket (380..750 nm) >= lambda. The reference tabulates rgbToSpectralValue
+// per texel and bucket up front; the same function is evaluated here per lookup.
+IZPI_DEV double tex_spectral_image(const DevScene& sc, const izpi_texture& t, double u, double v, double lambda) {
+  int64_t i = go_int(u * (double)t.width);
+  int64_t j = go_int((1 - v) * ((double)t.height - 0.001));
+  if (i < 0) i = 0;
+  if (j < 0) j = 0;
+  if (i > (int64_t)t.width - 1) i = (int64_t)t.width - 1;
+  if (j > (int64_t)t.height - 1) j = (int64_t)t.height - 1;
+  int k = 74;  // findWavelengthIndex: below 380 -> 0, above 750 (or NaN) -> 74
+  if (lambda < 380.0) k = 0;
+  else if (!(lambda > 750.0))
+    for (k = 0; k < 74; k++)
+      if (lambda <= 380.0 + 5.0 * (double)k) break;
+  const double* px = sc.texels + t.texel_offset + ((uint64_t)j * t.width + (uint64_t)i) * 4;
+  return spectral_image_value(px[0], px[1], px[2], 380.0 + 5.0 * (double)k);
+}
+
+// texture.SpectralConstant.Value (spectral_constant.go:65-106); SpectralImage reads (u, v)
+IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda, double u = 0.0, double v = 0.0) {
   const izpi_texture& t = sc.textures[id];
+  if (t.kind == IZPI_TEX_SPECTRAL_IMAGE) return tex_spectral_image(sc, t, u, v, lambda);
   if (t.kind == IZPI_TEX_SPECTRAL_TABULATED) {
     const double* wl = sc.spd_wl + t.spd_offset;
     const double* vl = sc.spd_val + t.spd_offset;
@@ -1361,7 +1402,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   const V3 ro = mk(R.o[0], R.o[1], R.o[2]), rd = mk(R.d[0], R.d[1], R.d[2]);
   V3 L = mk(0, 0, 0);
   bool terminal = false;
-  bool spec = false, have_pdf = false;
+  bool spec = false, have_pdf = false, zero_spdf = false;
   V3 att = mk(0, 0, 0), next_o = mk(0, 0, 0), next_d = mk(0, 0, 0);
   V3 hit_n = mk(0, 0, 0);
   uint32_t rec_mat = 0;
@@ -1406,7 +1447,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         if (dot(h.n, rd) < 0.0) {
           if (cconst) L = cval;
           else if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-          else L.x = tex_spectral(sc, m.spectral_tex, P.lambda);
+          else L.x = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
         }
         terminal = true;
         break;
@@ -1417,8 +1458,19 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         cos_onb.build(h.n);
         if (cconst) att = cval;
         else if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-        else att.x = tex_spectral(sc, m.spectral_tex, P.lambda);
+        else att.x = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
         have_pdf = true;
+        break;
+      }
+      case IZPI_MAT_ISOTROPIC: {  // isotropic.go:32-60: a randomInUnitSphere ray the sampler discards,
+        // Cosine(N) as the material pdf of the mixture, ScatteringPDF 0; Spectral: the albedo's red
+        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
+        (void)random_in_unit_sphere(rng);
+        cos_onb.build(h.n);
+        const V3 a = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+        if (COLOUR) att = a; else att.x = a.x;
+        have_pdf = true;
+        zero_spdf = true;
         break;
       }
       case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
@@ -1455,7 +1507,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
         double alb_s = 0;
         if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-        else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda);
+        else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
         else { V3 c = tex_rgb(sc, m.albedo_tex, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
         V3 normal = h.n;
         if (m.normal_tex >= 0) {
@@ -1520,7 +1572,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         const double cos_pdf = cosv > 0 ? cosv / 3.141592653589793 : 0;
         double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
         if (sc_cos < 0) sc_cos = 0;
-        rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, sc_cos / 3.141592653589793, rec_mat);
+        const double spdf = zero_spdf ? 0.0 : sc_cos / 3.141592653589793;  // Isotropic.ScatteringPDF is 0
+        rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, spdf, rec_mat);
         const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
         next_d = dir;
@@ -2708,16 +2761,29 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     const int32_t ids[] = {m.albedo_tex, m.spectral_tex, m.normal_tex, m.roughness_tex, m.metalness_tex, m.absorb_tex};
     for (int32_t t : ids) {
       if (t < -1 || t >= (int32_t)d->num_textures) { ctx->err = "texture index out of range"; return IZPI_ERR_INVALID; }
-      if (t >= 0 && d->textures[t].kind == IZPI_TEX_IMAGE) mflags[i] |= 1u;
+      if (t >= 0 && (d->textures[t].kind == IZPI_TEX_IMAGE || d->textures[t].kind == IZPI_TEX_SPECTRAL_IMAGE)) mflags[i] |= 1u;
+    }
+    // a SpectralImage is made for PBR albedos (transport.go:486-497) and reads the hit's
+    // (u, v): Lambert / DiffuseLight / PBR spectral textures only
+    for (int32_t t : {m.normal_tex, m.roughness_tex, m.metalness_tex, m.absorb_tex, m.albedo_tex})
+      if (t >= 0 && d->textures[t].kind == IZPI_TEX_SPECTRAL_IMAGE) { ctx->err = "SpectralImage outside a spectral albedo"; return IZPI_ERR_INVALID; }
+    if (m.spectral_tex >= 0 && d->textures[m.spectral_tex].kind == IZPI_TEX_SPECTRAL_IMAGE && m.kind != IZPI_MAT_LAMBERT &&
+        m.kind != IZPI_MAT_DIFFUSE_LIGHT && m.kind != IZPI_MAT_PBR) {
+      ctx->err = "SpectralImage outside a spectral albedo";
+      return IZPI_ERR_INVALID;
     }
     auto is_rgb = [&](int32_t t) { return t >= 0 && (d->textures[t].kind == IZPI_TEX_CONSTANT || d->textures[t].kind == IZPI_TEX_IMAGE); };
-    auto is_spec = [&](int32_t t) { return t >= 0 && (d->textures[t].kind == IZPI_TEX_SPECTRAL_GAUSSIAN || d->textures[t].kind == IZPI_TEX_SPECTRAL_TABULATED); };
+    auto is_spec = [&](int32_t t) {
+      return t >= 0 && (d->textures[t].kind == IZPI_TEX_SPECTRAL_GAUSSIAN || d->textures[t].kind == IZPI_TEX_SPECTRAL_TABULATED ||
+                        d->textures[t].kind == IZPI_TEX_SPECTRAL_IMAGE);
+    };
     auto opt_rgb = [&](int32_t t) { return t == -1 || is_rgb(t); };
     bool rgb = false, spec = false;
     switch (m.kind) {
       case IZPI_MAT_LAMBERT: case IZPI_MAT_DIFFUSE_LIGHT: rgb = is_rgb(m.albedo_tex); spec = is_spec(m.spectral_tex); break;
       case IZPI_MAT_DIELECTRIC: rgb = true; spec = is_spec(m.spectral_tex) && (m.absorb_tex == -1 || is_spec(m.absorb_tex)); break;
       case IZPI_MAT_METAL: rgb = spec = true; break;
+      case IZPI_MAT_ISOTROPIC: rgb = spec = is_rgb(m.albedo_tex); break;  // SpectralScatter reads the RGB albedo's X
       case IZPI_MAT_PBR: {
         bool aux = opt_rgb(m.normal_tex) && opt_rgb(m.roughness_tex) && opt_rgb(m.metalness_tex);
         rgb = aux && is_rgb(m.albedo_tex);
@@ -2780,6 +2846,14 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(mflags.data(), mflags.size(), &dmf);
   double4* dmc;
   UP(mconst.data(), mconst.size(), &dmc);
+  for (uint32_t i = 0; i < d->num_textures; i++) {
+    const izpi_texture& t = d->textures[i];
+    if (t.kind != IZPI_TEX_IMAGE && t.kind != IZPI_TEX_SPECTRAL_IMAGE) continue;
+    if (t.width == 0 || t.height == 0 || t.texel_offset + 4ull * t.width * t.height > d->num_texels || !d->texels) {
+      ctx->err = "image texture outside the texel array";
+      return IZPI_ERR_INVALID;
+    }
+  }
   // device copy of the textures: pad0 = 1 marks a tabulated SPD with non-decreasing
   // wavelengths, which tex_spectral searches by bisection
   std::vector<izpi_texture> texs(d->textures, d->textures + d->num_textures);

@@ -900,8 +900,9 @@ struct Converter {
         const PMsg* l = m->msg("isotropic");
         const std::string w = l ? l->oneof(1) : "";
         if (w == "albedo") {
-          texture(l->msg("albedo"));
-          fail(IZPI_ERR_UNSUPPORTED, "material " + mname + ": isotropic materials are not on the GPU path");
+          izpi_material r = blank_mat(IZPI_MAT_ISOTROPIC);
+          r.albedo_tex = texture(l->msg("albedo"));
+          return r;
         }
         if (w == "spectral_albedo") {
           spectral_texture(l->msg("spectral_albedo"));
@@ -919,11 +920,16 @@ struct Converter {
         r.normal_tex = texture(pb ? pb->msg("normal_map") : nullptr);
         texture(pb ? pb->msg("sss") : nullptr);  // required by the reference, unused by PBR.Scatter
         if (spectral) {  // textureToSpectralTexture (transport.go:486-520)
-          const izpi_texture& a = s.texs[r.albedo_tex];
-          if (a.kind == IZPI_TEX_IMAGE)
-            fail(IZPI_ERR_UNSUPPORTED, "material " + mname + ": spectral image albedo (SpectralImage) is not on the GPU path");
-          const double lum = 0.299 * a.value[0] + 0.587 * a.value[1] + 0.114 * a.value[2];
-          r.spectral_tex = neutral(lum);
+          const izpi_texture a = s.texs[r.albedo_tex];
+          if (a.kind == IZPI_TEX_IMAGE) {  // NewSpectralImageFromImage of the image's texels
+            izpi_texture si = blank(IZPI_TEX_SPECTRAL_IMAGE);
+            si.width = a.width; si.height = a.height; si.texel_offset = a.texel_offset;
+            s.texs.push_back(si);
+            r.spectral_tex = (int32_t)s.texs.size() - 1;
+          } else {
+            const double lum = 0.299 * a.value[0] + 0.587 * a.value[1] + 0.114 * a.value[2];
+            r.spectral_tex = neutral(lum);
+          }
         }
         return r;
       }

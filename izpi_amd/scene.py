@@ -62,6 +62,16 @@ class Scene:
         self.textures.append(t)
         return len(self.textures) - 1
 
+    def spectral_image(self, image_tex):
+        """texture.SpectralImage of an image texture (NewSpectralImageFromImage,
+        spectral_image.go:64-190): what transport.textureToSpectralTexture makes of a PBR
+        image albedo for the Spectral sampler (transport.go:486-497). Shares its texels."""
+        src = self.textures[image_tex]
+        assert src.kind == N.TEX_IMAGE
+        t = N.Texture(kind=N.TEX_SPECTRAL_IMAGE, width=src.width, height=src.height, texel_offset=src.texel_offset)
+        self.textures.append(t)
+        return len(self.textures) - 1
+
     def spectral_gaussian(self, peak, center, width):
         t = N.Texture(kind=N.TEX_SPECTRAL_GAUSSIAN, peak=float(f32(peak)), center=float(f32(center)),
                       width_nm=float(f32(width)))
@@ -116,6 +126,10 @@ class Scene:
             flags = N.MATF_BEER_LAMBERT  # NewSpectralDielectric(refidx, computeBeerLambert)
         return self._mat(kind=N.MAT_DIELECTRIC, ref_idx=float(f32(ref_idx)), spectral_tex=spectral_refidx,
                          absorb_tex=spectral_absorb, rgb=absorb, flags=flags)
+
+    def isotropic(self, albedo):
+        """material.NewIsotropic (isotropic.go; transport.go:269-278): RGB albedo texture."""
+        return self._mat(kind=N.MAT_ISOTROPIC, albedo_tex=albedo)
 
     def metal(self, albedo, fuzz):
         return self._mat(kind=N.MAT_METAL, rgb=[float(v) for v in f32(albedo)], fuzz=float(f32(fuzz)))

@@ -19,9 +19,9 @@
  *   hitable/sphere.go:29-145           getSphereUV, Hit, BoundingBox, center, PDFValue, Random
  *   hitable/hitable_slice.go:30-110    Hit, PDFValue, Random
  *   material/material.go:10-43         randomInUnitSphere, reflect, refract, schlick
- *   material/lambertian.go, diffuselight.go, dielectric.go, metal.go, pbr.go
+ *   material/lambertian.go, diffuselight.go, dielectric.go, metal.go, pbr.go, isotropic.go
  *   pdf/cosine.go, hitable.go, mixture.go
- *   texture/constant.go, image.go:73-101, spectral_constant.go:65-106
+ *   texture/constant.go, image.go:73-101, spectral_constant.go:65-106, spectral_image.go:64-259
  *   spectral/spectral.go:151-253, firefly_rejection.go:12-113, rgb_image.go:28-67
  *   sampler/colour.go:33-65, sampler/spectral.go:47-80
  *   render/rgb.go:12-57, render/spectral.go:71-106, common/tiles.go, grid/grid.go
@@ -286,6 +286,70 @@ struct SpectralConstantTex : SpectralTexture {  // spectral_constant.go:65-106
   }
 };
 
+// spectral_image.go:64-259 (NewSpectralImageFromImage of a Float64NRGBA image): the
+// spectral value of every texel at every 5-nm bucket is tabulated up front, as the
+// reference does; Value reads the texel ImageTxt.Value would and the first bucket >= lambda.
+struct SpectralImageTex : SpectralTexture {
+  int sizeX = 0, sizeY = 0;
+  std::vector<double> wavelengths;          // 380, 385, ..., 750
+  std::vector<std::vector<double>> data;    // [bucket][pixel]
+  static double rgbToSpectralValue(double r, double g, double b, double wavelength) {  // :130-190
+    double spectralValue = 0;
+    if (wavelength >= 580.0 && wavelength <= 750.0) {
+      double center = 650.0, distance = go_abs(wavelength - center), width = 60.0;
+      double falloff = go_exp(-(distance * distance) / (2.0 * width * width));
+      spectralValue += r * falloff;
+    }
+    if (wavelength >= 480.0 && wavelength <= 620.0) {
+      double center = 550.0, distance = go_abs(wavelength - center), width = 60.0;
+      double falloff = go_exp(-(distance * distance) / (2.0 * width * width));
+      spectralValue += g * falloff;
+    }
+    if (wavelength >= 380.0 && wavelength <= 520.0) {
+      double center = 450.0, distance = go_abs(wavelength - center), width = 60.0;
+      double falloff = go_exp(-(distance * distance) / (2.0 * width * width));
+      spectralValue += b * falloff;
+    }
+    if (go_abs(r - g) < 0.15 && go_abs(g - b) < 0.15 && go_abs(r - b) < 0.15) {
+      double maxRGB = go_max(r, go_max(g, b));
+      spectralValue = go_max(spectralValue, maxRGB);
+    }
+    double maxRGB = go_max(r, go_max(g, b));
+    if (maxRGB > 0.7 && spectralValue < maxRGB * 0.8) spectralValue = go_max(spectralValue, maxRGB * 0.8);
+    return go_max(0.0, go_min(1.0, spectralValue));
+  }
+  void Build(int w, int h, const double* pix) {  // NewSpectralImageFromImage + transformRGBToSpectral
+    sizeX = w; sizeY = h;
+    for (int k = 0; k < 75; k++) wavelengths.push_back(380.0 + 5.0 * k);
+    data.assign(wavelengths.size(), std::vector<double>((size_t)w * h));
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) {
+        const double* px = pix + ((size_t)y * w + x) * 4;
+        for (size_t i = 0; i < wavelengths.size(); i++) data[i][(size_t)y * w + x] = rgbToSpectralValue(px[0], px[1], px[2], wavelengths[i]);
+      }
+  }
+  int findWavelengthIndex(double lambda) const {
+    if (lambda < wavelengths[0]) return 0;
+    if (lambda > wavelengths.back()) return (int)wavelengths.size() - 1;
+    for (size_t i = 0; i < wavelengths.size(); i++)
+      if (lambda <= wavelengths[i]) return (int)i;
+    return (int)wavelengths.size() - 1;
+  }
+  double Value(double u, double v, double lambda, Vec3) const override {
+    int64_t i = go_int(u * (double)sizeX);
+    int64_t j = go_int((1 - v) * ((double)sizeY - 0.001));
+    if (i < 0) i = 0;
+    if (j < 0) j = 0;
+    if (i > (int64_t)(sizeX - 1)) i = sizeX - 1;
+    if (j > (int64_t)(sizeY - 1)) j = sizeY - 1;
+    const int64_t pixelIndex = j * sizeX + i;
+    const int wi = findWavelengthIndex(lambda);
+    if (wi < 0 || wi >= (int)data.size()) return 0.0;
+    if (pixelIndex < 0 || pixelIndex >= (int64_t)data[(size_t)wi].size()) return 0.0;
+    return data[(size_t)wi][(size_t)pixelIndex];
+  }
+};
+
 // ---------------------------------------------------------------- pdfs
 struct HitableBase;
 struct CosinePDF {  // pdf/cosine.go
@@ -383,6 +447,29 @@ struct Lambertian : Material {  // lambertian.go
     if (cosine < 0) cosine = 0;
     return cosine / GO_PI;
   }
+};
+
+struct Isotropic : Material {  // isotropic.go
+  const Texture* albedo = nullptr;
+  bool Scatter(const Ray& r, const HitRecord& hr, LCG& rnd, ScatterRecord& srec) const override {
+    (void)r;
+    (void)randomInUnitSphere(rnd);  // the scattered ray: built and discarded by the sampler
+    srec.albedo = albedo->Value(hr.u, hr.v, hr.p);
+    srec.pdf.Init(hr.normal);
+    srec.hasPDF = true;
+    srec.isSpecular = false;
+    return true;
+  }
+  bool SpectralScatter(const Ray& r, const HitRecord& hr, LCG& rnd, SpectralScatterRecord& srec) const override {
+    (void)randomInUnitSphere(rnd);
+    srec.lambda = r.lambda;
+    srec.albedo = albedo->Value(hr.u, hr.v, hr.p).X;  // "red component as approximation"
+    srec.pdf.Init(hr.normal);
+    srec.hasPDF = true;
+    srec.isSpecular = false;
+    return true;
+  }
+  // ScatteringPDF: 0 (Material's default)
 };
 
 struct DiffuseLight : Material {  // diffuselight.go
@@ -1255,6 +1342,10 @@ oracle_scene* oracle_build(const izpi_scene_input* in) {
       c->spd.wl.assign(in->spd_wavelengths + t.spd_offset, in->spd_wavelengths + t.spd_offset + t.spd_count);
       c->spd.val.assign(in->spd_values + t.spd_offset, in->spd_values + t.spd_offset + t.spd_count);
       W.stexs.emplace_back(c); spec[i] = c;
+    } else if (t.kind == IZPI_TEX_SPECTRAL_IMAGE) {
+      SpectralImageTex* c = new SpectralImageTex();
+      c->Build((int)t.width, (int)t.height, W.texels.data() + t.texel_offset);
+      W.stexs.emplace_back(c); spec[i] = c;
     }
   }
   auto R = [&](int32_t id) -> const Texture* { return id < 0 ? nullptr : rgb[(size_t)id]; };
@@ -1273,6 +1364,7 @@ oracle_scene* oracle_build(const izpi_scene_input* in) {
         d->spectralAbsorptionCoeff = S(m.absorb_tex); dielectrics.push_back(d); out = d; break;
       }
       case IZPI_MAT_METAL: { Metal* mm = new Metal(); mm->albedo = Load(m.rgb); mm->fuzz = m.fuzz; out = mm; break; }
+      case IZPI_MAT_ISOTROPIC: { Isotropic* is = new Isotropic(); is->albedo = R(m.albedo_tex); out = is; break; }
       case IZPI_MAT_PBR: {
         PBR* p = new PBR(); p->albedo = R(m.albedo_tex); p->spectralAlbedo = S(m.spectral_tex); p->normalMap = R(m.normal_tex);
         p->roughness = R(m.roughness_tex); p->metalness = R(m.metalness_tex); out = p; break;

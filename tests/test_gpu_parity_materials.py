@@ -53,6 +53,12 @@ def test_rgb_dielectric_bitwise(gpu, coloured):
 
 
 def spectral_pbr_box(spectral_albedo):
+    """spectral_albedo: True = a Gaussian spectral albedo, "image" = the SpectralImage of the
+    image albedo (transport.go:486-497), False = no spectral albedo (the luminance fallback)."""
+    return _spectral_pbr_box(spectral_albedo)
+
+
+def _spectral_pbr_box(spectral_albedo):
     tabs = configs.spectral_tables()
     s = Scene("spectral_pbr")
     alb, nrm, rough, metal = configs._pbr_textures(s, res=64)
@@ -62,7 +68,8 @@ def spectral_pbr_box(spectral_albedo):
         "light": s.diffuse_light(spectral=s.spectral_spd(tabs["cie_wavelengths"],
                                                           tabs["light_sources"]["cie_f1_daylight_fluorescent"])),
     }
-    spec = s.spectral_gaussian(0.8, 600, 60) if spectral_albedo else -1
+    spec = (s.spectral_image(alb) if spectral_albedo == "image"
+            else s.spectral_gaussian(0.8, 600, 60) if spectral_albedo else -1)
     # White walls: PBR with image textures and UVs (normal map through Triangle.Hit's TBN
     # and again in PBR.SpectralScatter, A19)
     mats["White"] = s.pbr(alb, normal=nrm, roughness=rough, metalness=metal, spectral=spec)
@@ -79,7 +86,7 @@ def spectral_pbr_box(spectral_albedo):
     return s
 
 
-@pytest.mark.parametrize("spectral_albedo", [True, False])
+@pytest.mark.parametrize("spectral_albedo", [True, False, "image"])
 def test_spectral_pbr_bitwise(gpu, spectral_albedo):
     scene = spectral_pbr_box(spectral_albedo)
     r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL)
@@ -135,5 +142,38 @@ def test_textured_lambert_bitwise(gpu, env, monkeypatch):
     r = GPURenderer(scene, 48, 48, 8)
     img = r.render()
     ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
+
+
+def isotropic_box(spectral):
+    """Isotropic walls and spheres (isotropic.go): randomInUnitSphere draws, Cosine(N) in
+    the mixture, ScatteringPDF 0 (so they pass on no light but keep every draw and ray);
+    the Spectral sampler reads the RGB albedo's red (SpectralScatter)."""
+    s = Scene("isotropic")
+    alb, _, _, _ = configs._pbr_textures(s, res=32)
+    if spectral:
+        tabs = configs.spectral_tables()
+        mats = {"White": s.lambert(spectral=s.spectral_neutral(0.73)),
+                "Green": s.lambert(spectral=s.spectral_gaussian(0.9, 540, 40)),
+                "Red": s.isotropic(s.constant((0.73, 0.2, 0.1))),
+                "light": s.diffuse_light(spectral=s.spectral_spd(tabs["cie_wavelengths"],
+                                                                  tabs["light_sources"]["cie_f1_daylight_fluorescent"]))}
+    else:
+        mats = configs.rgb_box_materials(s)
+        mats["Red"] = s.isotropic(s.constant((0.73, 0.2, 0.1)))
+    configs.add_box(s, mats)
+    s.add_sphere((35, 20, 45), 18, s.isotropic(alb))
+    s.add_sphere((70, 15, 30), 12, mats["White"])
+    configs.cornell_camera(s, 1.0)
+    return s
+
+
+@pytest.mark.parametrize("sampler", [N.SAMPLER_COLOUR, N.SAMPLER_SPECTRAL])
+def test_isotropic_bitwise(gpu, sampler):
+    scene = isotropic_box(sampler == N.SAMPLER_SPECTRAL)
+    r = GPURenderer(scene, 48, 48, 8, sampler=sampler)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 48, 48, 8, sampler)
     assert_parity(img, ref, r.stats, ostats)
     r.close()

@@ -248,10 +248,40 @@ materials { key: "g" value { name: "gauss" type: LAMBERT lambert { spectral_albe
         assert g.kind == N.TEX_SPECTRAL_GAUSSIAN and (g.peak, g.center, g.width_nm) == (float(np.float32(0.9)), 540.0, 40.0)
 
 
-def test_isotropic_and_displacement_are_outside_the_gpu_path():
-    s = ingest.ProtoScene(b'materials { key: "i" value { name: "i" type: ISOTROPIC isotropic { albedo { constant {} } } } }')
-    with pytest.raises(RuntimeError, match="isotropic"):
+def test_isotropic_materials():
+    """toSceneIsotropicMaterial (transport.go:269-289): an RGB albedo converts; a spectral
+    albedo is the reference's own error."""
+    s = ingest.ProtoScene(b'materials { key: "i" value { name: "i" type: ISOTROPIC isotropic '
+                          b'{ albedo { constant { value { x: 0.5 y: 0.25 z: 1 } } } } } }')
+    si = _input(s)
+    m = si.materials[0]
+    assert m.kind == N.MAT_ISOTROPIC
+    t = si.textures[m.albedo_tex]
+    assert t.kind == N.TEX_CONSTANT and list(t.value) == [0.5, 0.25, 1.0]
+    s = ingest.ProtoScene(b'materials { key: "i" value { name: "i" type: ISOTROPIC isotropic '
+                          b'{ spectral_albedo { neutral { reflectance: 0.5 } } } } }')
+    with pytest.raises(RuntimeError, match="spectral isotropic materials not yet implemented"):
         s.to_input()
+
+
+def test_spectral_pbr_image_albedo_becomes_a_spectral_image():
+    """textureToSpectralTexture (transport.go:486-497): a PBR image albedo under the
+    Spectral sampler is read through NewSpectralImageFromImage of the same texels."""
+    text = ('colour_representation: SPECTRAL\n'
+            'image_textures { key: "k" value { filename: "albedo.exr" } }\n'
+            'materials { key: "m" value { name: "m" type: PBR pbr { albedo { image { filename: "albedo.exr" } } '
+            'roughness { constant { } } metalness { constant { } } normal_map { constant { } } sss { constant { } } } } }')
+    s = ingest.ProtoScene(text.encode())
+    rgba = np.arange(2 * 3 * 4, dtype=np.float64).reshape(2, 3, 4) / 24.0
+    s.set_image("albedo.exr", rgba)
+    si = _input(s)
+    m = si.materials[0]
+    a, t = si.textures[m.albedo_tex], si.textures[m.spectral_tex]
+    assert a.kind == N.TEX_IMAGE and t.kind == N.TEX_SPECTRAL_IMAGE
+    assert (t.width, t.height, t.texel_offset) == (a.width, a.height, a.texel_offset)
+
+
+def test_displacement_is_outside_the_gpu_path():
     s = ingest.ProtoScene(b'materials { key: "w" value { name: "w" type: METAL } }\n'
                           b'objects { triangles { material_name: "w" operator: DISPLACE } }')
     with pytest.raises(RuntimeError, match="DISPLACE"):
