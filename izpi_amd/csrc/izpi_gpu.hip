@@ -990,9 +990,23 @@ struct ShadeParams {
 // footprint small; MATSET_CONST is MATSET_BASIC for scenes whose albedos are all
 // constant RGB textures (Colour sampler): a bounce's attenuation is then its material's
 // constant, so its unwinding record holds the material instead of the colour (24 B
-// instead of 48 B); MATSET_FULL adds Dielectric, Metal and PBR. The host picks the
-// variant from the scene's materials (results are identical).
-enum { MATSET_BASIC = 0, MATSET_FULL = 1, MATSET_CONST = 2 };
+// instead of 48 B); MATSET_SURF adds Metal and PBR, MATSET_FULL Dielectric and Isotropic
+// too. The host picks the variant from the scene's materials (results are identical).
+// A MATSET is a set of feature bits: only the material branches it holds are compiled in.
+// The host runs the smallest instance holding the scene's material kinds: MATSET_SURF for
+// Metal/PBR scenes (C4: shading -2% against MATSET_FULL). A Lambert/light/dielectric
+// instance measured 3% SLOWER than MATSET_FULL on C5 (its register allocation came out
+// worse), so dielectric scenes run MATSET_FULL.
+enum { MS_DIEL = 1, MS_METAL = 2, MS_PBR = 4, MS_ISO = 8, MS_CONST = 16 };
+enum {
+  MATSET_BASIC = 0,
+  MATSET_SURF = MS_METAL | MS_PBR,
+  MATSET_FULL = MS_DIEL | MS_METAL | MS_PBR | MS_ISO,
+  MATSET_CONST = MS_CONST
+};
+constexpr bool ms_has(int matset, int feature) { return (matset & feature) != 0; }
+// specular bounces (records without a pdf) can occur
+constexpr bool ms_spec(int matset) { return (matset & (MS_DIEL | MS_METAL | MS_PBR)) != 0; }
 // Record: Colour (flag, att xyz, s, p); Colour + MATSET_CONST (material, s, p); Spectral
 // (flag, att, s, p). p is always last.
 template <int SAMPLER, int MATSET>
@@ -1036,7 +1050,7 @@ IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.ou
 // colour.go:44-57 / sampler/spectral.go:60-72 from depth-1 down to 0.
 template <int SAMPLER, int MATSET>
 IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
-  constexpr bool NO_SPEC = MATSET != MATSET_FULL;
+  constexpr bool NO_SPEC = !ms_spec(MATSET);
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
     // +0 radiance through only non-specular records: every level computes
     // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
@@ -1337,7 +1351,9 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
     const uint32_t nu = exhausted ? 0u : s_u[b][0] + s_u[b][1] + s_u[b][2] + s_u[b][3];
     const uint32_t ne = np + nu;
     const uint32_t u0 = nu ? atomicAdd(sp.head, nu) : sp.total_units;
-    if (u0 + nu >= sp.total_units) exhausted = true;
+    // (an iteration without finished paths asks for nothing and learns nothing: it must
+    // not mark the block exhausted, or the block's later finished paths lose their slots)
+    if (nu && u0 + nu >= sp.total_units) exhausted = true;
     s_pbase[b] = ne ? atomicAdd(out_count, ne) : 0u;
     s_ubase[b] = u0;
     s_granted[b] = u0 >= sp.total_units ? 0u : min(nu, sp.total_units - u0);
@@ -1407,7 +1423,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   V3 hit_n = mk(0, 0, 0);
   uint32_t rec_mat = 0;
   Onb cos_onb;
-  if (MATSET == MATSET_FULL && kind_of(R.kind) == RAY_PATHLEN) {
+  if (ms_has(MATSET, MS_DIEL) && kind_of(R.kind) == RAY_PATHLEN) {
     // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
     const PathCold& pc = in.cold[i];
     const V3 hp = mk(pc.pend[0], pc.pend[1], pc.pend[2]);
@@ -1464,7 +1480,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       }
       case IZPI_MAT_ISOTROPIC: {  // isotropic.go:32-60: a randomInUnitSphere ray the sampler discards,
         // Cosine(N) as the material pdf of the mixture, ScatteringPDF 0; Spectral: the albedo's red
-        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (!ms_has(MATSET, MS_ISO)) { atomicOr(sp.error, 2u); terminal = true; break; }
         (void)random_in_unit_sphere(rng);
         cos_onb.build(h.n);
         const V3 a = tex_rgb(sc, m.albedo_tex, h.u, h.v);
@@ -1474,7 +1490,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         break;
       }
       case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
-        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (!ms_has(MATSET, MS_DIEL)) { atomicOr(sp.error, 2u); terminal = true; break; }
         const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
         bool reflected;
         next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
@@ -1495,7 +1511,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         break;
       }
       case IZPI_MAT_METAL: {  // metal.go:34-41 (RGB only: SpectralScatter is nonSpectral)
-        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (!ms_has(MATSET, MS_METAL)) { atomicOr(sp.error, 2u); terminal = true; break; }
         if (!COLOUR) { terminal = true; break; }
         V3 reflected = reflect(unit(rd), h.n);
         next_d = add(reflected, smul(random_in_unit_sphere(rng), m.fuzz));
@@ -1504,7 +1520,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         break;
       }
       case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
-        if constexpr (MATSET != MATSET_FULL) { atomicOr(sp.error, 2u); terminal = true; break; }
+        if constexpr (!ms_has(MATSET, MS_PBR)) { atomicOr(sp.error, 2u); terminal = true; break; }
         double alb_s = 0;
         if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
         else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
@@ -1659,7 +1675,7 @@ IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
 #endif
 template <int SAMPLER, int MATSET>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATSET != MATSET_FULL && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve LDS buffer set
@@ -2055,6 +2071,7 @@ struct izpi_ctx {
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
+  uint32_t matset = 0;           // MS_* bits of the scene's material kinds
   bool const_albedo = false;     // ... and every albedo / emit texture a constant RGB: MATSET_CONST (Colour)
   bool any_uv = false;           // a material reads the hit's (u, v) (image textures)
   uint32_t pool_grow = 0;        // overflow pool doublings earned by frames that parked (render_impl)
@@ -2247,6 +2264,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     // host only polls the queue length once per batch (overshoot costs a few empty
     // launches of ~5 us).
     const int B = IZPI_PASS_BATCH;
+    const bool pass_log = getenv("IZPI_PASS_LOG") != nullptr;  // diagnostics: per-pass times on stderr
     while (n > 0) {
       for (int b = 0; b < B; b++) {
         wp.in = q[cur]; wp.in_count = qn[cur];
@@ -2270,8 +2288,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         HIP_TRY(hipEventElapsedTime(&s_ms, ctx->evb[3 * b + 1], ctx->evb[3 * b + 2]));
         *trace_ms += t_ms;
         *shade_ms += s_ms;
+        if (pass_log) fprintf(stderr, "IZPI_PASS %u trace %.3f shade %.3f\n", *launches, t_ms, s_ms);
         (*launches)++;
       }
+      if (pass_log) fprintf(stderr, "IZPI_BATCH queue %u head %u\n", ctx->h_count[3 + cur], ctx->h_count[0]);
       n = ctx->h_count[3 + cur];
       // every unit has started: finish the remaining paths in one k_tail launch
       if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
@@ -2467,13 +2487,18 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
 #define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches)
-  const bool basic = ctx->basic_materials;
+  // the smallest compiled material set holding the scene's material kinds
+  const uint32_t ms = ctx->matset;
+  const int set = ms == 0 ? MATSET_BASIC : (ms & ~(uint32_t)MATSET_SURF) == 0 ? MATSET_SURF : MATSET_FULL;
   if (req->sampler == IZPI_SAMPLER_COLOUR)
-    rc = compact ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_CONST)
-         : basic ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC)
-                 : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
+    rc = compact               ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_CONST)
+         : set == MATSET_BASIC ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_BASIC)
+         : set == MATSET_SURF  ? IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_SURF)
+                               : IZPI_RUN(IZPI_SAMPLER_COLOUR, MATSET_FULL);
   else
-    rc = basic ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_BASIC) : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_FULL);
+    rc = set == MATSET_BASIC  ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_BASIC)
+         : set == MATSET_SURF ? IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_SURF)
+                              : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_FULL);
 #undef IZPI_RUN
   if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, st));
@@ -2755,6 +2780,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   std::vector<uint32_t> mflags(d->num_materials, 0);
   ctx->mat_ok_rgb = ctx->mat_ok_spectral = true;
   ctx->basic_materials = true;
+  ctx->matset = 0;
   ctx->pool_grow = 0;
   for (uint32_t i = 0; i < d->num_materials; i++) {
     const izpi_material& m = d->materials[i];
@@ -2793,6 +2819,8 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       default: ctx->err = "unknown material kind"; return IZPI_ERR_INVALID;
     }
     if (m.kind != IZPI_MAT_LAMBERT && m.kind != IZPI_MAT_DIFFUSE_LIGHT) ctx->basic_materials = false;
+    ctx->matset |= m.kind == IZPI_MAT_DIELECTRIC ? MS_DIEL : m.kind == IZPI_MAT_METAL ? MS_METAL
+                 : m.kind == IZPI_MAT_PBR ? MS_PBR : m.kind == IZPI_MAT_ISOTROPIC ? MS_ISO : 0u;
     if (rgb) mflags[i] |= 2u; else ctx->mat_ok_rgb = false;
     if (spec) mflags[i] |= 4u; else ctx->mat_ok_spectral = false;
   }

@@ -200,6 +200,34 @@ def test_tiles_packed_and_unpack(gpu):
     r.close()
 
 
+@pytest.mark.parametrize("name", ["C4", "C3"])
+def test_queue_keeps_every_slot_while_units_remain(gpu, name, monkeypatch, capfd):
+    """While work units remain, every finished path's record slot starts a new unit, so the
+    queue stays at its first-fill length. (Round 2 regression: a block-iteration with no
+    finished path marked its block "units exhausted" for the rest of the pass; on C4 the
+    queue of 42M entries collapsed to one iteration per block and the frame took 3304
+    passes instead of ~100. Images were still bit-exact, only slower.)"""
+    monkeypatch.setenv("IZPI_PASS_LOG", "1")
+    monkeypatch.setenv("IZPI_SLOTS", "600000")  # several shading iterations per block, units >> slots
+    cfg = configs.configs()[name]
+    scene = cfg.build() if name == "C4" else configs.cornell_dragon(1.0, n=60)
+    W, H, spp = (192, 108, 64) if name == "C4" else (128, 128, 64)
+    r = GPURenderer(scene, W, H, spp)
+    r.render()
+    units = W * H * spp
+    log = capfd.readouterr().err
+    batches = [l.split() for l in log.splitlines() if l.startswith("IZPI_BATCH")]
+    assert batches, log[-2000:]
+    slots = r.stats["slots"]
+    assert slots == 600000
+    for b in batches:
+        queue, head = int(b[2]), int(b[4])
+        if head < units:  # units remain: no slot may have been dropped
+            assert queue == slots, (b, slots)
+    assert r.stats["launches"] <= 2 * (r.stats["rays"] // slots) + 48, r.stats
+    r.close()
+
+
 @pytest.mark.parametrize("env", [{"IZPI_PRIM_W": "1"},
                                  {"IZPI_PRIM_W": "100000"}, {"IZPI_SLOTS": "3000", "IZPI_CHUNK_UNITS": "5000"},
                                  {"IZPI_NO_LEAF_SHORTCUT": "1"}, {"IZPI_TRACE_CHUNK": "1", "IZPI_REFILL_MIN": "1"},

@@ -17,6 +17,7 @@ def main():
     p.add_argument("--config", default="C3")
     p.add_argument("--frames", type=int, default=2)
     p.add_argument("--spp", type=int, default=None)
+    p.add_argument("--stats", action="store_true", help="print every counter of the last frame")
     a = p.parse_args()
     import torch
     from izpi_amd import configs
@@ -38,6 +39,8 @@ def main():
                               "shade_ms": r.stats["shade_ms"], "tail_ms": r.stats["tail_ms"],
                               "rays": r.stats["rays"], "parks": r.stats["parks"], "hbm_used_gb": (free0 - free) / 1e9})
         print(json.dumps(out["frames"][-1]), flush=True)
+    if a.stats:
+        print(json.dumps({"stats": r.stats}), flush=True)
     r.close()
     print(json.dumps(out), flush=True)
 
