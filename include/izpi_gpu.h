@@ -242,7 +242,8 @@ int izpi_gpu_ray_aabb4(izpi_ctx* ctx, const float* boxes, const float* rays, uin
 /* Go-math on device, op codes in izpi_amd/csrc/gomath.h order: 0 sin 1 cos 2 tan 3 exp
  * 4 log 5 pow(x,y) 6 atan2(x,y) 7 asin 8 sqrt 9 div(x,y) 10 atan; spectral helpers:
  * 32/33 SampleWavelength(x) lambda/pdf (spectral.go:184-224), 34/35/36 GetCIEValues(x)
- * x/y/z (spectral.go:227-253). */
+ * x/y/z (spectral.go:227-253); 37 SpectralConstant.Value(x) of the uploaded scene's texture
+ * number y (spectral_constant.go:65-106, needs a scene). */
 int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uint32_t n, double* out);
 
 #ifdef __cplusplus

@@ -247,6 +247,14 @@ IZPI_HD double pow_zero(double x, double y) {
   return (signbit(x) && is_odd_int(y)) ? x : 0;
 }
 IZPI_HD double pow(double x, double y) {
+  // Pow(x, 2) (the spectral Gaussian textures' exponent, spectral_constant.go:102): pow.go's
+  // loop computes frexp's mantissa m squared, rounded once, times 2^(2e) by exact steps,
+  // which is the correctly rounded x * x whenever x * x is a normal number, 0 or inf.
+  // Only 0 < |x| < 2^-511 (a subnormal or zero square: the loop rounds twice) takes the loop.
+  if (y == 2.0) {
+    const double ax = abs(x);
+    if (ax >= 0x1p-511 || ax == 0) return x * x;  // (NaN: Go returns its own NaN bits, below)
+  }
   if (y == 0 || x == 1) return 1;
   if (y == 1) return x;
   if (is_nan(x) || is_nan(y)) return nan();

@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -153,6 +154,21 @@ IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda, doub
     if (n == 0) return 0.0;
     if (lambda < wl[0]) return vl[0];
     if (lambda > wl[n - 1]) return vl[n - 1];
+    if (t.pad0 == 2 && lambda == lambda) {
+      // near-uniform wavelengths (set at upload): the interval's index is guessed from
+      // lambda, its two wavelengths and values load together, and a short walk fixes a
+      // wrong guess, so the result is the scan's interval exactly
+      uint32_t g = 1u + (uint32_t)((lambda - t.value[0]) * t.value[1]);
+      g = g > n - 1 ? n - 1 : g;
+      double w1 = wl[g - 1], w2 = wl[g], v1 = vl[g - 1], v2 = vl[g];
+      if (!((g == 1 || w1 < lambda) && w2 >= lambda)) {
+        while (g > 1 && wl[g - 1] >= lambda) g--;
+        while (wl[g] < lambda) g++;
+        w1 = wl[g - 1]; w2 = wl[g]; v1 = vl[g - 1]; v2 = vl[g];
+      }
+      const double tt = (lambda - w1) / (w2 - w1);
+      return v1 + tt * (v2 - v1);
+    }
     if (t.pad0 && lambda == lambda) {  // pad0: wavelengths non-decreasing (set at upload)
       const uint32_t i = sorted_interval(wl, n, lambda);
       const double w1 = wl[i], w2 = wl[i + 1];
@@ -2007,7 +2023,7 @@ __global__ void k_aabb4(const float* boxes, const float* rays, uint32_t n, uint8
   masks[i] = m;
 }
 
-__global__ void k_gomath(int op, const double* x, const double* y, uint32_t n, double* out) {
+__global__ void k_gomath(const DevScene sc, int op, const double* x, const double* y, uint32_t n, double* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   double a = x[i], b = y ? y[i] : 0.0, r;
@@ -2025,6 +2041,7 @@ __global__ void k_gomath(int op, const double* x, const double* y, uint32_t n, d
     case 10: r = gm::atan(a); break;
     case 32: case 33: { double l, pdf; sample_wavelength(a, l, pdf); r = op == 32 ? l : pdf; break; }
     case 34: case 35: case 36: { double cx, cy, cz; cie_values(a, cx, cy, cz); r = op == 34 ? cx : op == 35 ? cy : cz; break; }
+    case 37: r = tex_spectral(sc, (int32_t)b, a); break;
     default: r = gm::nan();
   }
   out[i] = r;
@@ -2039,6 +2056,7 @@ struct izpi_ctx {
   int num_cus = 0;
   // scene
   bool have_scene = false;
+  uint32_t num_textures = 0;     // of the uploaded scene (izpi_gpu_gomath texture lookups)
   DevScene sc{};
   uint32_t stack_needed = 0;
   uint32_t num_prims = 0;
@@ -2883,16 +2901,27 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     }
   }
   // device copy of the textures: pad0 = 1 marks a tabulated SPD with non-decreasing
-  // wavelengths, which tex_spectral searches by bisection
+  // wavelengths, which tex_spectral searches by bisection; pad0 = 2 one whose wavelengths
+  // are also near-uniform (entry j within half a step of wl[0] + j * step), whose interval
+  // tex_spectral guesses from lambda with value[0] = wl[0] and value[1] = 1 / step
   std::vector<izpi_texture> texs(d->textures, d->textures + d->num_textures);
   for (izpi_texture& t : texs) {
     t.pad0 = 0;
     if (t.kind != IZPI_TEX_SPECTRAL_TABULATED || t.spd_count < 2) continue;  // n = 1: the scan returns 0.0
     if ((uint64_t)t.spd_offset + t.spd_count > d->num_spd) { ctx->err = "SPD range out of bounds"; return IZPI_ERR_INVALID; }
+    const double* wl = d->spd_wavelengths + t.spd_offset;
+    const uint32_t n = t.spd_count;
     bool sorted = true;
-    for (uint32_t i = 1; i < t.spd_count; i++)
-      if (!(d->spd_wavelengths[t.spd_offset + i - 1] <= d->spd_wavelengths[t.spd_offset + i])) sorted = false;
+    for (uint32_t i = 1; i < n; i++)
+      if (!(wl[i - 1] <= wl[i])) sorted = false;
     t.pad0 = sorted ? 1u : 0u;
+    const double span = wl[n - 1] - wl[0];
+    if (!sorted || !(span > 0) || !std::isfinite(span)) continue;
+    const double scale = (double)(n - 1) / span;
+    bool uniform = std::isfinite(scale);
+    for (uint32_t i = 0; i < n && uniform; i++)
+      if (!(std::fabs((wl[i] - wl[0]) * scale - (double)i) <= 0.5)) uniform = false;
+    if (uniform) { t.pad0 = 2; t.value[0] = wl[0]; t.value[1] = scale; }
   }
   UP(texs.data(), d->num_textures, &dtx);
   UP(d->texels, d->num_texels, &dtex);
@@ -2937,6 +2966,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     ctx->num_prims = d->num_prims;
   }
   ctx->have_scene = true;
+  ctx->num_textures = d->num_textures;
   return IZPI_OK;
 }
 
@@ -3111,6 +3141,12 @@ int izpi_gpu_ray_aabb4(izpi_ctx* ctx, const float* boxes, const float* rays, uin
 int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uint32_t n, double* out) {
   if (!ctx || !x || !out) return IZPI_ERR_INVALID;
   if (n == 0) return IZPI_OK;
+  if (op == 37) {  // texture lookups: a scene, and texture numbers in range
+    if (!ctx->have_scene) { ctx->err = "texture lookup before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
+    if (!y) { ctx->err = "texture lookup without texture numbers"; return IZPI_ERR_INVALID; }
+    for (uint32_t i = 0; i < n; i++)
+      if (!(y[i] >= 0 && y[i] < (double)ctx->num_textures)) { ctx->err = "texture number out of range"; return IZPI_ERR_INVALID; }
+  }
   HIP_TRY(hipSetDevice(ctx->device));
   double *dx, *dy = nullptr, *dout;
   HIP_TRY(hipMalloc((void**)&dx, (size_t)n * sizeof(double)));
@@ -3120,7 +3156,7 @@ int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uin
     HIP_TRY(hipMalloc((void**)&dy, (size_t)n * sizeof(double)));
     HIP_TRY(hipMemcpy(dy, y, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
   }
-  hipLaunchKernelGGL(k_gomath, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, op, dx, dy, n, dout);
+  hipLaunchKernelGGL(k_gomath, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, op, dx, dy, n, dout);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));

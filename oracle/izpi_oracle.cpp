@@ -1942,6 +1942,14 @@ uint32_t oracle_tiles(uint32_t W, uint32_t H, uint32_t* tiles, uint32_t max_tile
 
 void oracle_sample_wavelength(double r, double* lambda, double* pdf) { SampleWavelength(r, lambda, pdf); }
 void oracle_cie_values(double w, double* out3) { GetCIEValues(w, out3, out3 + 1, out3 + 2); }
+// SpectralConstant.Value of a tabulated SPD (spectral_constant.go:88-106): the linear scan
+double oracle_spd_tabulated_value(const double* wl, const double* val, uint32_t n, double lambda) {
+  SpectralConstantTex t;
+  t.tabulated = true;
+  t.spd.wl.assign(wl, wl + n);
+  t.spd.val.assign(val, val + n);
+  return t.Value(0, 0, lambda, Vec3());
+}
 double oracle_spectral_value(int gaussian, double a, double b, double c, double lambda) {
   SpectralConstantTex t; t.peak = a; t.center = b; t.width = c; (void)gaussian;
   return t.Value(0, 0, lambda, Vec3());

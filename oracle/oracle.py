@@ -79,6 +79,8 @@ def lib():
     L.oracle_cie_values.argtypes = [C.c_double, C.POINTER(C.c_double)]
     L.oracle_spectral_value.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double, C.c_double]
     L.oracle_spectral_value.restype = C.c_double
+    L.oracle_spd_tabulated_value.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_double]
+    L.oracle_spd_tabulated_value.restype = C.c_double
     _lib = L
     return L
 

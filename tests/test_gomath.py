@@ -96,6 +96,28 @@ def test_accuracy_against_libm(op):
     assert worst <= MAX_ULP[op], (op, worst)
 
 
+def pow_square_inputs():
+    """x across the whole exponent range (subnormals, the 2^-511 edge of pow's x*x shortcut,
+    huge values whose square overflows) with y = 2."""
+    rng = np.random.default_rng(5)
+    k = np.arange(-1074, 1024)
+    x = np.ldexp(rng.uniform(1, 2, k.size), k) * np.where(rng.random(k.size) < 0.5, -1, 1)
+    edge = np.ldexp(1.0, -511)
+    x = np.concatenate([x, [edge, np.nextafter(edge, 0), np.nextafter(edge, 1), -edge, 5e-324, -5e-324, 1e-160, 1e154,
+                            1.4e154, 0.0, -0.0, float("inf"), float("-inf"), float("nan")]])
+    return x, np.full_like(x, 2.0)
+
+
+def test_pow_square_shortcut_bitwise():
+    """gomath.h's Pow(x, 2) shortcut (x * x outside the subnormal-square range) equals the
+    oracle's restatement of pow.go's loop on every binade."""
+    L = N.lib()
+    for a, b in zip(*pow_square_inputs()):
+        p = L.izpi_host_gomath(OPS["pow"], float(a), float(b))
+        o = O.gomath(OPS["pow"], float(a), float(b))
+        assert struct.pack("<d", p) == struct.pack("<d", o), (a, p, o)
+
+
 def test_special_values():
     assert O.gomath(OPS["sin"], -0.0) == 0.0 and math.copysign(1, O.gomath(OPS["sin"], -0.0)) < 0
     assert math.isnan(O.gomath(OPS["cos"], float("inf")))

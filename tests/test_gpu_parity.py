@@ -56,11 +56,11 @@ def assert_parity(gpu_img, ora_img, gstats=None, ostats=None):
 
 
 def test_gomath_device_bitwise(gpu):
-    from tests.test_gomath import OPS, inputs
+    from tests.test_gomath import OPS, inputs, pow_square_inputs
     r = GPURenderer(configs.cornell_rgb(), 8, 8, 1)
     L = N.lib()
-    for name, op in OPS.items():
-        x, y = inputs(name, n=20000, seed=3)
+    for name, op in list(OPS.items()) + [("pow2", OPS["pow"])]:
+        x, y = pow_square_inputs() if name == "pow2" else inputs(name, n=20000, seed=3)
         x = np.ascontiguousarray(x, np.float64)
         y = np.ascontiguousarray(y, np.float64)
         out = np.zeros_like(x)
@@ -628,6 +628,48 @@ def test_spectral_table_lookups_bitwise(gpu, table):
     img = r.render()
     ref_img, ostats = oracle_canvas(s, 40, 40, 8, N.SAMPLER_SPECTRAL, bg=bg)
     assert_parity(img, ref_img, r.stats, ostats)
+    r.close()
+
+
+def test_spectral_tabulated_lookup_device_bitwise(gpu):
+    """SpectralConstant.Value of tabulated SPDs on the device (spectral_constant.go:88-106)
+    against the oracle's linear scan, bit for bit: near-uniform tables (the interval is
+    guessed from lambda, then checked), a table with a jittered grid, one with a repeated
+    wavelength and an unsorted one (bisection / scan); lambdas on every grid point, one ulp
+    either side, random ones and out-of-range ones."""
+    import ctypes as C
+    from izpi_amd.scene import Scene
+    tabs = configs.spectral_tables()
+    cie = np.asarray(tabs["cie_wavelengths"], np.float64)
+    rng = np.random.default_rng(3)
+    tables = [
+        (cie, rng.random(len(cie))),                                   # uniform 5 nm (the CIE grid)
+        (np.arange(380.0, 781.0, 10.0), rng.random(41)),                # uniform 10 nm
+        (np.arange(400.0, 701.0, 20.0) + rng.uniform(-6, 6, 16), rng.random(16)),  # jittered grid
+        (np.array([380.0, 430, 480, 480, 530, 580, 630, 680, 730, 780]), rng.random(10)),  # a tie
+        (np.array([380.0, 500, 450, 600, 780]), rng.random(5)),           # unsorted
+        (np.array([380.0, 780.0]), np.array([0.25, 0.75])),              # two entries
+    ]
+    tables[2] = (np.sort(tables[2][0]), tables[2][1])
+    s = Scene("tabs")
+    ids = [s.spectral_tabulated(wl, vl, proto_float=False) for wl, vl in tables]
+    mats = {k: s.lambert(spectral=s.spectral_neutral(0.5)) for k in ("Green", "Red", "White")}
+    mats["light"] = s.diffuse_light(spectral=s.spectral_neutral(4.0))
+    configs.add_box(s, mats)
+    s.set_camera((50, 50, -120), (50, 50, 50), (0, 1, 0), 35, 1.0, 0, 10, 0, 1, 1.0)
+    r = GPURenderer(s, 8, 8, 1, sampler=N.SAMPLER_SPECTRAL)
+    L = N.lib()
+    for tid, (wl, vl) in zip(ids, tables):
+        wl = np.ascontiguousarray(wl, np.float64)
+        vl = np.ascontiguousarray(vl, np.float64)
+        lams = np.ascontiguousarray(np.concatenate([wl, np.nextafter(wl, 0), np.nextafter(wl, 1e4),
+                                                    rng.uniform(wl.min() - 5, wl.max() + 5, 5000),
+                                                    [300.0, 900.0, float(wl[0]), float(wl[-1])]]))
+        ids_arr = np.full(len(lams), float(tid))
+        out = np.zeros_like(lams)
+        assert L.izpi_gpu_gomath(r.ctx, 37, O.dptr(lams), O.dptr(ids_arr), len(lams), O.dptr(out)) == 0
+        ref = np.array([O.lib().oracle_spd_tabulated_value(O.dptr(wl), O.dptr(vl), len(wl), float(x)) for x in lams])
+        assert out.tobytes() == ref.tobytes(), (tid, np.flatnonzero(out != ref)[:10])
     r.close()
 
 
