@@ -2281,7 +2281,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     // their queue length from device memory and exit at once when it is zero, so the
     // host only polls the queue length once per batch (overshoot costs a few empty
     // launches of ~5 us).
-    const int B = IZPI_PASS_BATCH;
+    // Once every unit has started, the queue only shrinks: poll after every pass, so that
+    // k_tail takes over as soon as few enough paths remain instead of up to 8 passes later
+    // (each of those last passes costs ~0.3-1 ms of mostly idle machine).
+    int B = IZPI_PASS_BATCH;
     const bool pass_log = getenv("IZPI_PASS_LOG") != nullptr;  // diagnostics: per-pass times on stderr
     while (n > 0) {
       for (int b = 0; b < B; b++) {
@@ -2311,6 +2314,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
       }
       if (pass_log) fprintf(stderr, "IZPI_BATCH queue %u head %u\n", ctx->h_count[3 + cur], ctx->h_count[0]);
       n = ctx->h_count[3 + cur];
+      if (ctx->h_count[0] >= sp.total_units) B = 1;
       // every unit has started: finish the remaining paths in one k_tail launch
       if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
         wp.in = q[cur]; wp.in_count = qn[cur];
