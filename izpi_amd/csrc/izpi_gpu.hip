@@ -1684,9 +1684,6 @@ IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
 #ifndef IZPI_SHADE_WPE
 #define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (168 VGPRs, 6 spilled; 4 waves spill 47 VGPRs and measured 1% slower)
 #endif
-#ifndef IZPI_SHADE_PREQ
-#define IZPI_SHADE_PREQ 1
-#endif
 #ifndef IZPI_SHADE_WPE_OTHER
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
 #endif
