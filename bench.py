@@ -299,11 +299,14 @@ def main():
     import numpy as np
     import torch
     from izpi_amd import build
-    build.build_gpu(verbose=False)
+    dist = dist_setup(world, rank) if mode == "ranks" else None
+    # one rank (re)builds the library when its sources are newer, the others wait for it
+    if dist is None or rank == 0:
+        build.build_gpu(verbose=False)
+    if dist is not None:
+        dist.barrier()
     from izpi_amd import _native as N
     from izpi_amd.renderer import GPURenderer, MultiGPURenderer
-
-    dist = dist_setup(world, rank) if mode == "ranks" else None
     cfg, scene, scene_s = load_config(args)
     spp = args.spp or cfg.spp
     post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE

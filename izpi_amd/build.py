@@ -85,7 +85,7 @@ def build_gpu(force=False, verbose=True):
         subprocess.run(cmd, check=True)
     with ThreadPoolExecutor(len(cmds)) as ex:
         list(ex.map(run, cmds))
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = LIB.with_suffix(".so.tmp%d" % os.getpid())  # os.replace below: readers never see a partial file
     run([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), *LINK])
     os.replace(tmp, LIB)
     build_cli(True, verbose)
