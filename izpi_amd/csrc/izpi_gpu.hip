@@ -2413,15 +2413,18 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (const char* e = getenv("IZPI_CHUNK_UNITS")) max_units = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
-  // blocks (ShadeParams::rec_pool). Colour records are 48 B, spectral 32 B, and spectral
-  // glass paths run deeper, hence the larger dense part there.
+  // blocks (ShadeParams::rec_pool). Colour records are 48 B (24 B compact), spectral 32 B.
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
   const bool compact = !spectral && ctx->basic_materials && ctx->const_albedo;
   const uint32_t D = spectral  ? RecLayout<IZPI_SAMPLER_SPECTRAL, MATSET_FULL>::D
                      : compact ? RecLayout<IZPI_SAMPLER_COLOUR, MATSET_CONST>::D
                                : RecLayout<IZPI_SAMPLER_COLOUR, MATSET_FULL>::D;
   const uint32_t max_depth = std::max(1u, req->max_depth);
-  uint32_t rec_dense = spectral ? 16u : 8u;
+  // Spectral glass paths run deep (C5: 12 rays per sample): with 16 dense levels the first
+  // frame parked 15% of its shading items on an empty overflow pool; 32 levels park none
+  // (C5 256 spp first frame 8854 -> 8130 ms; 92 GB of workspace, less than a pool twice the
+  // size would take).
+  uint32_t rec_dense = spectral ? 32u : 8u;
   if (const char* e = getenv("IZPI_REC_DENSE")) rec_dense = (uint32_t)std::max(1, atoi(e));
   rec_dense = std::min(rec_dense, max_depth);
   const uint32_t rec_pool = max_depth - rec_dense;
