@@ -1840,7 +1840,19 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
   if (p >= ap.num_pixels) return;
   double c0 = ap.running[3 * (size_t)p], c1 = ap.running[3 * (size_t)p + 1], c2 = ap.running[3 * (size_t)p + 2];
   const double* s = ap.samples + (size_t)p * ap.chunk_spp * 3;
-  for (uint32_t k = 0; k < ap.chunk_spp; k++) {  // sample order, as rgb.go:36
+  uint32_t k = 0;
+  if ((ap.chunk_spp & 1u) == 0) {
+    // two samples (48 B, 16-B aligned for an even chunk_spp) per three 16-B loads: the
+    // lanes' runs lie chunk_spp * 24 B apart, so every load instruction touches 64 lines
+    // and the instruction count, not the bytes, bounds this loop
+    const double2* s2 = reinterpret_cast<const double2*>(s);
+    for (; k + 1 < ap.chunk_spp; k += 2) {  // sample order, as rgb.go:36
+      const double2 a = s2[3 * (k >> 1)], b = s2[3 * (k >> 1) + 1], c = s2[3 * (k >> 1) + 2];
+      c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;  // sample k
+      c0 = c0 + b.y; c1 = c1 + c.x; c2 = c2 + c.y;  // sample k + 1
+    }
+  }
+  for (; k < ap.chunk_spp; k++) {  // sample order, as rgb.go:36
     c0 = c0 + s[3 * k];
     c1 = c1 + s[3 * k + 1];
     c2 = c2 + s[3 * k + 2];
