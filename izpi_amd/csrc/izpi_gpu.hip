@@ -1267,31 +1267,6 @@ IZPI_DEV void load_path(const WaveBuf& b, uint32_t i, PathSt& P) {
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { const double2 c = *reinterpret_cast<const double2*>(b.cold + i); P.lambda = c.x; P.lpdf = c.y; }
 }
 
-// Block-wide reservation: every lane with `want` gets a distinct index from `counter`,
-// with ONE atomic per 256-thread block (a single counter word saturates near 88
-// returning atomics/us chip-wide, MI355X_MICROARCH.md "dequeue"). All threads of the
-// block must call it (block-uniform control flow).
-IZPI_DEV uint32_t block_reserve(uint32_t* counter, bool want, uint32_t& parity) {
-  // two LDS buffer sets used alternately, so no trailing barrier is needed before reuse
-  __shared__ uint32_t s_w[2][4];
-  __shared__ uint32_t s_base[2];
-  const uint32_t b = parity;
-  parity ^= 1u;
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t m = __ballot(want);
-  if (lane == 0) s_w[b][w] = (uint32_t)__popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t tot = s_w[b][0] + s_w[b][1] + s_w[b][2] + s_w[b][3];
-    s_base[b] = tot ? atomicAdd(counter, tot) : 0u;
-  }
-  __syncthreads();
-  uint32_t off = s_base[b];
-  for (uint32_t i = 0; i < w; i++) off += s_w[b][i];
-  off += (uint32_t)__popcll(m & ((1ull << lane) - 1));
-  return off;
-}
-
 // Take units for the lanes that ask (one atomic per wave); returns UINT32_MAX when drained.
 IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
   const uint64_t m = __ballot(want);
@@ -1308,7 +1283,7 @@ IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
 // First fill of the queue (first pass of a chunk): record slot j takes unit j (the host
 // starts the unit head at min(slots, units), so no atomic is needed: one counter word
 // serialises ~88 atomics/us), then further units from the head while its path needs no
-// tracing. The traceable paths are appended to `out`, one reservation per block.
+// tracing; the path goes to entry j of `out`.
 template <int SAMPLER>
 __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
@@ -1337,9 +1312,16 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
       }
     }
   }
-  uint32_t parity = 0;
-  const uint32_t pos = block_reserve(wp.out_count, push, parity);
-  if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
+  // Entry j of the first queue belongs to record slot j (no queue atomic: one per block on
+  // one counter word made this kernel 1.9 ms per C3 frame); a slot whose samples all
+  // completed without a ray (spectral pdf 0, the units ran out) leaves a dead entry, which
+  // the first shading pass drops.
+  const uint32_t fill = min(sp.slots, sp.total_units);
+  if (j < fill) {
+    if (push) store_entry<SAMPLER>(wp.out, j, P, R);
+    else dead_entry(wp.out, j);
+  }
+  if (j == 0) *wp.out_count = fill;
 }
 
 // One block-wide reservation phase for a shading iteration (ONE pair of barriers, two
@@ -1691,7 +1673,7 @@ template <int SAMPLER, int MATSET>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
-  uint32_t parity = 0;  // block_reserve LDS buffer set
+  uint32_t parity = 0;  // block_reserve2 LDS buffer set
   const uint32_t n = *wp.in_count;
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
