@@ -451,6 +451,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = *wp.in_count;
   if (wp.pool_ctr && blockIdx.x == 0) pool_publish(wp.pool_ctr);
+  // the next k_shade appends to out_count from 0 (its old value, an earlier pass's input
+  // count, is read by no one any more): no memset launch per pass
+  if (wp.out_count && blockIdx.x == 0 && threadIdx.x == 0) *wp.out_count = 0;
   // kind words other than RAY_MAIN exist only with dielectrics (path-length rays), an
   // overflow record pool (parked entries) or explicit tMin / tMax (dead entries are
   // recognised by their ray)
@@ -1675,6 +1678,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MATSE
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   uint32_t parity = 0;  // block_reserve2 LDS buffer set
   const uint32_t n = *wp.in_count;
+  // this pass's k_trace2 is done with its dequeue cursor: reset it for the next pass's
+  if (blockIdx.x == 0 && threadIdx.x == 0) *wp.trace_next = 0;
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * 256;
@@ -2260,7 +2265,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     sp.chunk_spp = cs; sp.s0 = s0; sp.total_units = num_pixels * cs;
     const uint32_t fill = std::min<uint32_t>(sp.slots, sp.total_units);
     HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)fill, 1, st));  // unit head: k_start gives slot i unit i
-    HIP_TRY(hipMemsetAsync(ctx->d_misc + 3, 0, 2 * sizeof(uint32_t), st));  // queue counts
+    HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, 3 * sizeof(uint32_t), st));  // dequeue cursor, queue counts
     wp.out = q[0]; wp.out_count = qn[0];
     hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, ctx->sc, sp, wp);
     HIP_TRY(hipGetLastError());
@@ -2281,8 +2286,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
       for (int b = 0; b < B; b++) {
         wp.in = q[cur]; wp.in_count = qn[cur];
         wp.out = q[1 - cur]; wp.out_count = qn[1 - cur];
-        HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, sizeof(uint32_t), st));
-        HIP_TRY(hipMemsetAsync(qn[1 - cur], 0, sizeof(uint32_t), st));
+        // (k_trace2 zeroes out_count, k_shade the dequeue cursor for the next pass)
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
         launch_trace(ctx, tr, wp, st, ctx->d_spill);
         HIP_TRY(hipGetLastError());
