@@ -314,7 +314,9 @@ struct WaveParams {
   uint32_t* trace_next;       // dynamic-fetch cursor of k_trace2
   unsigned long long* pool_ctr;  // overflow-record ring counters (k_trace2 publishes frees), or null
   uint32_t slots;
-  uint32_t read_kind;         // entries other than plain RAY_MAIN rays can occur (k_trace2 reads kind words)
+  uint32_t read_kind;         // path-length rays or explicit tMin / tMax can occur (k_trace2 reads kind words)
+  const uint32_t* in_park;    // nonzero: the pass that wrote `in` parked entries (k_trace2 reads kind words), or null
+  uint32_t* out_park;         // set by k_shade when it parks an entry of `out` (zeroed by k_trace2)
   uint32_t hit_uv;            // k_shade may read a hit's (u, v): spheres (the root) or (u,v)-reading textures
 };
 IZPI_DEV double ray_tmin(const WaveBuf& b, uint32_t i, uint32_t kind) {
@@ -454,10 +456,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // the next k_shade appends to out_count from 0 (its old value, an earlier pass's input
   // count, is read by no one any more): no memset launch per pass
   if (wp.out_count && blockIdx.x == 0 && threadIdx.x == 0) *wp.out_count = 0;
-  // kind words other than RAY_MAIN exist only with dielectrics (path-length rays), an
-  // overflow record pool (parked entries) or explicit tMin / tMax (dead entries are
-  // recognised by their ray)
-  const bool read_kind = wp.read_kind != 0;
+  if (wp.out_park && blockIdx.x == 0 && threadIdx.x == 0) *wp.out_park = 0;
+  // kind words other than RAY_MAIN exist only with dielectrics (path-length rays), explicit
+  // tMin / tMax, or after a shading pass that parked entries on an empty overflow pool (dead
+  // entries are recognised by their ray)
+  const bool read_kind = wp.read_kind != 0 || (wp.in_park && *wp.in_park != 0);
   // Small queues (the wavefront's tail passes): chunks shrink so the rays spread over
   // more waves, and waves past the last chunk exit at once instead of each paying a
   // dequeue atomic on the one counter word (~88/us chip-wide).
@@ -1744,6 +1747,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     atomicAdd(sp.counters + CNT_SCLK_PUSH, (unsigned long long)k_push);
   }
 #endif
+  if (c_park && wp.out_park) *wp.out_park = 1u;  // the next k_trace2 must read kind words
   unsigned long long vals[3] = {c_lt, c_ls, c_park};
   const int idx[3] = {CNT_LTRI, CNT_LSPH, CNT_PARK};
   for (int k = 0; k < 3; k++) {
@@ -2069,7 +2073,7 @@ struct izpi_ctx {
   uint32_t* d_tiles = nullptr; size_t tiles_cap = 0;
   uint32_t* d_utiles = nullptr; size_t utiles_cap = 0;  // tile lists of k_unpack (multi-GPU root)
   double* d_bg = nullptr; size_t bg_cap = 0;
-  uint32_t* d_misc = nullptr;              // [0] unit head, [1] error, [2] trace cursor, [3..4] queue counts
+  uint32_t* d_misc = nullptr;              // [0] unit head, [1] error, [2] trace cursor, [3..4] queue counts, [6..7] park flags
   unsigned long long* d_counters = nullptr;
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
@@ -2266,6 +2270,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     const uint32_t fill = std::min<uint32_t>(sp.slots, sp.total_units);
     HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)fill, 1, st));  // unit head: k_start gives slot i unit i
     HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, 3 * sizeof(uint32_t), st));  // dequeue cursor, queue counts
+    HIP_TRY(hipMemsetAsync(ctx->d_misc + 6, 0, 2 * sizeof(uint32_t), st));  // park flags of the two sides
     wp.out = q[0]; wp.out_count = qn[0];
     hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, ctx->sc, sp, wp);
     HIP_TRY(hipGetLastError());
@@ -2286,7 +2291,8 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
       for (int b = 0; b < B; b++) {
         wp.in = q[cur]; wp.in_count = qn[cur];
         wp.out = q[1 - cur]; wp.out_count = qn[1 - cur];
-        // (k_trace2 zeroes out_count, k_shade the dequeue cursor for the next pass)
+        wp.in_park = ctx->d_misc + 6 + cur; wp.out_park = ctx->d_misc + 6 + (1 - cur);
+        // (k_trace2 zeroes out_count and out_park, k_shade the dequeue cursor for the next pass)
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
         launch_trace(ctx, tr, wp, st, ctx->d_spill);
         HIP_TRY(hipGetLastError());
@@ -2495,7 +2501,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   WaveParams wp{};
   wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
   // kind words other than plain main rays: path-length rays, parked entries
-  wp.read_kind = (!ctx->sc.no_pathlen || rec_pool != 0) ? 1u : 0u;
+  wp.read_kind = !ctx->sc.no_pathlen ? 1u : 0u;  // parked entries: wp.in_park, per pass
   wp.hit_uv = (!ctx->sc.tri_only || ctx->any_uv) ? 1u : 0u;
   wp.pool_ctr = sp.pool_ctr;
   AccumParams ap{};
