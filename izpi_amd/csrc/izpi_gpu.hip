@@ -2436,7 +2436,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const bool need_cold = spectral || !ctx->sc.no_pathlen;
   // Paths in flight per wavefront pass. Larger = fewer k_trace/k_shade launches and
   // a smaller share of launch tails.
-  uint64_t slot_cap = 40ull << 20;  // C3: 16M -> 435 ms/frame, 24M -> 414, 40M -> 407 (fewer passes, fewer pass tails)
+  // C3 per frame (round 2, tiered records): 40M slots 349 ms, 100M 334, 160M 326, 250M 320
+  // (fewer passes and pass tails; the first frame, fresh allocations included, is faster
+  // too: 371 ms at 40M, 349 ms at 250M); C5 at 64 spp 120M slots: -6%; C4 100M: -3%.
+  // The state stays within half of the HBM (below).
+  uint64_t slot_cap = 256ull << 20;
   if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
   const uint64_t per_slot = 2 * (sizeof(RayOD) + sizeof(uint32_t) + (ctx->sc.tri_only ? 0 : sizeof(double)) + sizeof(PathHot) +
                                  sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(HitSt)) +
