@@ -2454,8 +2454,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   pool_div = std::max(1u, pool_div >> std::min(ctx->pool_grow, 4u));
   if (const char* e = getenv("IZPI_POOL_DIV")) pool_div = (uint32_t)std::max(1, atoi(e));
   const uint64_t per_block = (uint64_t)rec_pool * D * sizeof(double) + sizeof(uint32_t);
-  if (avail > 0)  // the wavefront state within half of the HBM
-    slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (avail / 2) / (per_slot + per_block / pool_div + 1)));
+  // The wavefront state within half of the HBM. The overflow pool rounds up to a power of
+  // two per ring, up to twice slots / pool_div blocks: counted at that worst case (C4 at
+  // 256M slots otherwise took 271 GB of the 288).
+  if (avail > 0)
+    slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (avail / 2) / (per_slot + 2 * per_block / pool_div + 1)));
   const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);
   uint32_t pool_blocks = 0;
   if (rec_pool) {  // POOL_SHARDS rings of a power of two each, at least 16 blocks per ring
