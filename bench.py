@@ -45,7 +45,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_PASSES = {"fetch": ["FETCH_SIZE"], "write": ["WRITE_SIZE"], "tcc": ["TCC_HIT_sum", "TCC_MISS_sum"]}
+PMC_PASSES = {"fetch": ["FETCH_SIZE"], "write": ["WRITE_SIZE"], "tcc": ["TCC_HIT_sum", "TCC_MISS_sum"],
+              "sq": ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                     "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_ANY"]}
 KERNELS = {"k_trace2": "k_trace2<", "k_shade": "k_shade<"}
 
 
@@ -181,50 +183,68 @@ def traffic_summary(pmc):
         out[short] = {"fetch_bytes_per_frame": fb, "write_bytes_per_frame": wb, "bytes_per_frame": fb + wb,
                       "dispatches": e["dispatches"],
                       "tcc_hit_rate": hit / (hit + miss) if hit is not None and miss and hit + miss > 0 else None}
+        wc = e.get("SQ_WAVE_CYCLES")
+        if wc:  # what the kernel's waves spend their cycles on, measured in this run
+            out[short]["wave_cycles"] = {
+                "waiting": e.get("SQ_WAIT_ANY", 0.0) / wc, "issuing_any": e.get("SQ_ACTIVE_INST_ANY", 0.0) / wc,
+                "issuing_valu": e.get("SQ_ACTIVE_INST_VALU", 0.0) / wc,
+                "issuing_vmem": e.get("SQ_ACTIVE_INST_VMEM", 0.0) / wc,
+                "waiting_to_issue": e.get("SQ_WAIT_INST_ANY", 0.0) / wc}
     return out
 
 
 # ---------------------------------------------------------------- CPU baseline
 def cpu_baseline(cfg, scene, budget_s, spp, bvh):
     """Oracle render of a bounded sample of the same frame (tiles spread over the frame,
-    full spp when it fits the budget), timed on the CPUs this process may use."""
+    full spp when it fits the budget), timed on the CPUs this process may use, on the tree
+    the GPU figure uses (like for like) and on izpi's own NewBVH4 tree; half the budget each."""
     import ctypes as C
     import numpy as np
     from izpi_amd import _native as N
-    from izpi_amd.renderer import common_tiles
+    from izpi_amd.renderer import GPU_BVH_LEAF_MAX, GPU_BVH_METHOD, common_tiles
     from oracle import oracle as O
     cpus = host_cpus()
     threads = cpus["usable"]
-    o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
     tiles = common_tiles(cfg.width, cfg.height)
-
-    def run(ts, s):
-        req = N.RenderReq(width=cfg.width, height=cfg.height, spp=s, max_depth=cfg.max_depth, sampler=cfg.sampler,
-                          seed=12345)
-        t = np.ascontiguousarray(ts, np.uint32)
-        req.num_tiles = len(t)
-        req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
-        _, st = o.render(req, threads=threads)
-        return st
-    # calibrate on one tile per thread at 2 spp, then size the sample for the budget
-    st = run(tiles[:threads], 2)
-    rate = st["samples"] / max(st["seconds"], 1e-6)
     px_per_tile = int((tiles[0, 2] - tiles[0, 0] + 1) * (tiles[0, 3] - tiles[0, 1] + 1))
-    want_samples = rate * budget_s
-    s = spp
-    ntiles = int(want_samples // (px_per_tile * s))
-    if ntiles < threads:
-        ntiles = threads
-        s = max(1, int(want_samples // (px_per_tile * ntiles)))
-    ntiles = min(ntiles, len(tiles))
-    stride = max(1, len(tiles) // ntiles)
-    st = run(tiles[::stride][:ntiles], s)
+
+    def measure(o, budget):
+        def run(ts, s):
+            req = N.RenderReq(width=cfg.width, height=cfg.height, spp=s, max_depth=cfg.max_depth, sampler=cfg.sampler,
+                              seed=12345)
+            t = np.ascontiguousarray(ts, np.uint32)
+            req.num_tiles = len(t)
+            req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
+            _, st = o.render(req, threads=threads)
+            return st
+        # calibrate on one tile per thread at 2 spp, then size the sample for the budget
+        st = run(tiles[:threads], 2)
+        rate = st["samples"] / max(st["seconds"], 1e-6)
+        want_samples = rate * budget
+        s = spp
+        ntiles = int(want_samples // (px_per_tile * s))
+        if ntiles < threads:
+            ntiles = threads
+            s = max(1, int(want_samples // (px_per_tile * ntiles)))
+        ntiles = min(ntiles, len(tiles))
+        stride = max(1, len(tiles) // ntiles)
+        st = run(tiles[::stride][:ntiles], s)
+        return st["samples"] / st["seconds"] / 1e6, "%d evenly spread tiles (%d px) x %d spp = %d samples, %.1f s" % (
+            ntiles, ntiles * px_per_tile, s, st["samples"], st["seconds"])
+
+    o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
+    ref_value, ref_sample = measure(o, budget_s / 2)
+    value, sample, tree = ref_value, ref_sample, "izpi's own NewBVH4 tree"
+    if bvh == "gpu":  # the GPU-built tree, restated on the CPU node for node (oracle.lbvh4)
+        nodes, order = O.lbvh4(o.prim_boxes(), GPU_BVH_LEAF_MAX, GPU_BVH_METHOD)
+        o.set_bvh(nodes, order)
+        value, sample = measure(o, budget_s / 2)
+        tree = "the GPU-built PLOC tree (the tree of `value`)"
     o.close()
-    value = st["samples"] / st["seconds"] / 1e6
     res = {"value": value, "unit": "Msamples/s", "cores": threads, "kind": "port",
-           "sample": "%s: %d evenly spread tiles (%d px) x %d spp = %d samples, %.1f s on %d threads of the CPU "
-                     "oracle (C++ restatement of the Go hot path, per-sample RNG streams, izpi's own BVH4 tree)"
-                     % (cfg.name, ntiles, ntiles * px_per_tile, s, st["samples"], st["seconds"], threads),
+           "sample": "%s: %s on %d threads of the CPU oracle (C++ restatement of the Go hot path, per-sample RNG "
+                     "streams) on %s; on izpi's own tree: %s" % (cfg.name, sample, threads, tree, ref_sample),
+           "tree": "gpu" if bvh == "gpu" else "reference", "value_reference_tree": ref_value,
            "cpu_model": cpus["model"], "host_threads": cpus["host_threads"], "affinity_cpus": cpus["affinity"],
            "cgroup_cpus": cpus["cgroup_cpus"]}
     if cpus["host_threads"] and cpus["host_threads"] > threads:
@@ -437,9 +457,7 @@ def main():
             "achieved": None, "frac": None, "traffic": None,
             "achieved_algorithmic": round(achieved_alg, 2),
             "algorithmic_bytes_per_launch": alg_frame / launches,
-            "avg_launch_ms": trace_ms_frame / launches, "launches_per_frame": launches,
-            "binding_limit": "latency/issue (VALU ~53% busy, 57% of wave cycles waiting on memory, DESIGN.md §3.1), "
-                             "not HBM bandwidth"}
+            "avg_launch_ms": trace_ms_frame / launches, "launches_per_frame": launches}
     if "k_trace2" in pmc:
         t = pmc["k_trace2"]
         roof["traffic"] = t["bytes_per_frame"] / max(t["dispatches"], 1)  # HBM bytes per launch
@@ -450,19 +468,24 @@ def main():
         roof["write_per_frame"] = t["write_bytes_per_frame"]
         roof["tcc_hit_rate"] = t["tcc_hit_rate"]
         roof["pmc_dispatches"] = t["dispatches"]
+        if "wave_cycles" in t:  # SQ counters of the same workload: fractions of k_trace2's wave cycles
+            roof["wave_cycles"] = {k: round(v, 4) for k, v in t["wave_cycles"].items()}
         if "k_shade" in pmc:
             s = pmc["k_shade"]
             roof["k_shade"] = {"bytes_per_frame": s["bytes_per_frame"], "fetch_per_frame": s["fetch_bytes_per_frame"],
                                "write_per_frame": s["write_bytes_per_frame"], "tcc_hit_rate": s["tcc_hit_rate"],
                                "achieved": round(s["bytes_per_frame"] / (agg["shade_ms"] / steps * 1e-3) / 1e9, 2)}
+            if "wave_cycles" in s:
+                roof["k_shade"]["wave_cycles"] = {k: round(v, 4) for k, v in s["wave_cycles"].items()}
     elif pmc.get("error"):
         roof["pmc_error"] = pmc["error"]
     cpu = None
     if mode == "single" and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, scene, args.cpu_seconds, spp, args.bvh)
+        # like for like: the GPU and the CPU oracle on the same tree
         cpu["gpu_speedup"] = value / cpu["value"]
-        if ref_check:
-            cpu["gpu_speedup_reference_tree"] = ref_check["value"] / cpu["value"]
+        if ref_check and cpu.get("value_reference_tree"):
+            cpu["gpu_speedup_reference_tree"] = ref_check["value"] / cpu["value_reference_tree"]
         if cpu.get("extrapolated_all_host_threads"):
             cpu["gpu_speedup_vs_extrapolated"] = value / cpu["extrapolated_all_host_threads"]
     line = {

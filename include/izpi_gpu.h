@@ -77,6 +77,30 @@ enum {
                           by izpi_gpu_unpack_tiles */
 };
 
+/* Launch tuning of one render call. Every setting gives a bit-identical canvas and
+ * identical counters; they trade memory and scheduling only. Zero fields take the
+ * defaults, and a NULL izpi_render_req.tuning means all defaults. The library reads
+ * no environment variables: an inherited variable cannot change a production render. */
+typedef struct izpi_render_tuning {
+  uint32_t slots;        /* cap on paths in flight; 0 = 256M, within half of the HBM this context may use */
+  uint32_t chunk_units;  /* per-sample results held at once (pixels x spp of a chunk); 0 = 1/4 of that HBM */
+  uint32_t rec_dense;    /* unwinding levels per record slot; 0 = 8 (Colour), 32 (Spectral) */
+  uint32_t pool_div;     /* record slots per overflow block; 0 = 16 (Lambert/light scenes), 4 (others) */
+  uint32_t trace_chunk;  /* queue entries per k_trace2 dequeue; 0 = 512 */
+  uint32_t refill_min;   /* idle lanes before a k_trace2 refill (1..64); 0 = 24 */
+  uint32_t prim_weight;  /* k_trace2 primitive-step weight against node steps, x/16; 0 = 32 */
+  uint32_t flags;        /* IZPI_TUNE_* */
+  uint64_t tail_paths;   /* k_tail takes over at <= this many paths; 0 = the resident lanes */
+} izpi_render_tuning;
+enum {
+  IZPI_TUNE_NO_DIST = 1,          /* k_trace2 runs each leaf's tests in its own lane */
+  IZPI_TUNE_GENERAL_TRACE = 2,    /* the sphere-capable k_trace2 instance on triangle-only scenes */
+  IZPI_TUNE_NO_LEAF_SHORTCUT = 4, /* re-test every leaf box (A10) instead of inferring it */
+  IZPI_TUNE_SCALAR_SLAB = 8,      /* the scalar twin of RayAABB4 for every ray */
+  IZPI_TUNE_NO_TAIL = 16,         /* no k_tail: wavefront passes to the end */
+  IZPI_TUNE_PASS_LOG = 32         /* diagnostics: per-pass device times on stderr */
+};
+
 typedef struct izpi_render_req {
   uint32_t width, height;     /* canvas size = Renderer sizeX, sizeY */
   uint32_t spp;               /* numSamples */
@@ -93,6 +117,7 @@ typedef struct izpi_render_req {
   uint32_t post;              /* IZPI_POST_*: post-processing of a whole-frame IZPI_OUT_CANVAS render */
   uint32_t pad_post;
   double exposure;            /* XYZToRGB exposure (Scene.Exposure = camera exposure) */
+  const izpi_render_tuning* tuning; /* NULL = defaults */
 } izpi_render_req;
 
 /* Post-processing applied by Render for the Spectral sampler (renderer.go:215-219):
@@ -139,6 +164,9 @@ typedef struct izpi_render_stats {
   /* wavefront configuration of the call: paths in flight, unwinding records per path kept
    * in the dense array, overflow record blocks, samples per pixel per chunk */
   uint32_t slots, rec_dense, pool_blocks, chunk_spp;
+  /* host wall time of the call's workspace allocations (a fresh context's first frame pays
+   * for its HBM here; 0 when every buffer was already large enough) */
+  double alloc_ms;
 } izpi_render_stats;
 
 /* Hit record returned by izpi_gpu_trace: BVH4.Hit (bvh4.go:49-164) followed by
@@ -227,8 +255,15 @@ int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint
 /* Collective: every rank passes the same whole-frame request. Rank r renders the tiles
  * t % nranks == r, ncclGather moves the packed shares to rank 0, which writes the canvas
  * into out_dev (device memory on its GPU; ignored on other ranks) and applies req->post.
- * stats: this rank's share. */
+ * stats: this rank's share. Every rank runs the same collectives whatever fails locally,
+ * and two ncclAllReduce(max) agreement steps (after the buffers, after the gather) give
+ * every rank the worst status: a rank's own failure returns its status, a failure of
+ * another rank IZPI_ERR_PEER (last_error names the rank). */
 int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats);
+
+/* Test hook (fault injection): where = 1 makes izpi_gpu_render_rank fail this rank's local
+ * checks, 2 makes every render on this context fail as a device fault would; 0 = off. */
+int izpi_gpu_debug_fault(izpi_ctx* ctx, int where);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);

@@ -27,7 +27,8 @@ enum {
   IZPI_ERR_HIP = 2,         /* HIP runtime failure */
   IZPI_ERR_NO_SCENE = 3,    /* render before upload */
   IZPI_ERR_UNSUPPORTED = 4, /* feature outside this build (e.g. Payne-Hanek trig) */
-  IZPI_ERR_DEVICE = 5       /* device-side guard tripped (stack overflow, …) */
+  IZPI_ERR_DEVICE = 5,      /* device-side guard tripped (stack overflow, …) */
+  IZPI_ERR_PEER = 6         /* multi-GPU: this device/rank succeeded but another one failed */
 };
 
 /* ---- BVH4 node: byte-identical to hitable.BVH4Node (bvh4.go:23-39), 128 B ---- */

@@ -1,7 +1,8 @@
 /* go_shim_replay.c — the C call sequence of integration/go/render/gpu/renderer_gpu.go,
  * step for step, so that it runs (and is tested) where no Go toolchain exists.
  *
- *   gpu.New (renderer_gpu.go:90-213) and Renderer.Render (:216-235):
+ *   gpu.New (renderer_gpu.go:101-226), Renderer.Render (:229-245), Renderer.RenderTiles
+ *   (:251-283):
  *   1. proto.Marshal(scene) -> izpi_scene_parse_binary   (here: a .izpi file = those bytes)
  *   2. izpi_scene_set_image per loaded image texture      (here: none / a flat test texture)
  *   3. izpi_scene_to_input(aspect = W/H, bvh seed 12345) -> izpi_host_build_scene_ex(SKIP_BVH)
@@ -9,10 +10,16 @@
  *      izpi_gpu_build_bvh4(leaf 3, PLOC) -> izpi_host_scene_set_bvh
  *   5. izpi_gpu_upload_scene / izpi_gpu_multi_upload_scene, the whole-frame request:
  *      sampler from the scene's colour representation, IZPI_POST_SPECTRAL for the
- *      spectral sampler, IZPI_POST_GAMMA_CLAMP with --png-pipeline, exposure = camera's
- *   6. Render: izpi_gpu_render / izpi_gpu_multi_render into a zeroed W*H*4 float64 canvas
+ *      spectral sampler, IZPI_POST_GAMMA_CLAMP with --png-pipeline, exposure = camera's;
+ *      with --bg-spd the spectral background of Options.SpectralBackground (75 zeros, as
+ *      leader mode's colours.SpectralBlack) in malloc'ed memory, as the shim's C.malloc
+ *   6. Render: izpi_gpu_render / izpi_gpu_multi_render into a zeroed W*H*4 float64 canvas;
+ *      with --tiles N instead RenderTiles over the frame's first N tiles (common.Tiles,
+ *      spiral order): one izpi_gpu_render with IZPI_OUT_PACKED, tile list in malloc'ed
+ *      memory, the packed tiles written out
  *
  *   usage: go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices 0,0,...]
+ *                         [--bg-spd] [--tiles N]
  * Exit status 0 on success; the canvas is written as raw little-endian float64.
  */
 #include <stdint.h>
@@ -31,9 +38,11 @@ static int fail(const char* what, const char* msg) {
 int main(int argc, char** argv) {
   if (argc < 6) return fail("usage", "go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices a,b,..]");
   const uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]), spp = (uint32_t)atoi(argv[4]);
-  int png = 0, devices[16], ndev = 0;
+  int png = 0, devices[16], ndev = 0, bg_spd = 0, ntiles = 0;
   for (int i = 6; i < argc; i++) {
     if (!strcmp(argv[i], "--png-pipeline")) png = 1;
+    else if (!strcmp(argv[i], "--bg-spd")) bg_spd = 1;
+    else if (!strcmp(argv[i], "--tiles") && i + 1 < argc) ntiles = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--devices") && i + 1 < argc) {
       for (char* t = strtok(argv[++i], ","); t && ndev < 16; t = strtok(NULL, ",")) devices[ndev++] = atoi(t);
     }
@@ -98,27 +107,53 @@ int main(int argc, char** argv) {
   req.exposure = desc->camera.exposure;
   uint32_t post = IZPI_POST_NONE;
   req.sampler = IZPI_SAMPLER_COLOUR;
+  double* bg = NULL;
   if (info.colour_representation == IZPI_COLOUR_SPECTRAL) {  /* leader.go:77-81 */
     req.sampler = IZPI_SAMPLER_SPECTRAL;
     post |= IZPI_POST_SPECTRAL;
+    if (bg_spd) {  /* colours.SpectralBlack: 75 zeros at 380, 385, ... 750 nm */
+      bg = (double*)malloc(2 * 75 * sizeof(double));
+      for (int i = 0; i < 75; i++) { bg[i] = 380 + 5 * (double)i; bg[75 + i] = 0.0; }
+      req.num_bg_spd = 75;
+      req.bg_spd_wavelengths = bg;
+      req.bg_spd_values = bg + 75;
+    }
   }
   if (png) post |= IZPI_POST_GAMMA_CLAMP;
   req.post = post;
-  /* 6. Render */
-  double* pix = (double*)calloc((size_t)W * H * 4, sizeof(double));
+  /* 6. Render, or RenderTiles */
+  size_t nout = (size_t)W * H * 4;
+  double* pix = NULL;
   izpi_render_stats st;
-  if (m ? izpi_gpu_multi_render(m, &req, pix, NULL) : izpi_gpu_render(ctx, &req, pix, &st))
-    return fail("render", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
+  if (ntiles > 0) {
+    uint32_t* all = (uint32_t*)malloc(4 * sizeof(uint32_t) * ((size_t)W * H / 16 + 16));
+    const uint32_t nt = izpi_host_tiles(W, H, all, (uint32_t)((size_t)W * H / 16 + 16));
+    if (nt == 0 || (uint32_t)ntiles > nt) return fail("tiles", "bad --tiles");
+    izpi_render_req tr = req;
+    tr.num_tiles = (uint32_t)ntiles;
+    tr.tiles = all;
+    tr.out_layout = IZPI_OUT_PACKED;
+    tr.post = IZPI_POST_NONE;
+    nout = (size_t)(izpi_gpu_output_bytes(&tr) / sizeof(double));
+    pix = (double*)calloc(nout, sizeof(double));
+    if (izpi_gpu_render(ctx, &tr, pix, &st)) return fail("render tiles", izpi_gpu_last_error(ctx));
+    free(all);
+  } else {
+    pix = (double*)calloc(nout, sizeof(double));
+    if (m ? izpi_gpu_multi_render(m, &req, pix, NULL) : izpi_gpu_render(ctx, &req, pix, &st))
+      return fail("render", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
+  }
   FILE* o = fopen(argv[5], "wb");
-  if (!o || fwrite(pix, sizeof(double), (size_t)W * H * 4, o) != (size_t)W * H * 4) return fail("write", argv[5]);
+  if (!o || fwrite(pix, sizeof(double), nout, o) != nout) return fail("write", argv[5]);
   fclose(o);
   free(pix);
+  free(bg);
   /* Renderer.Close */
   if (m) izpi_gpu_multi_close(m);
   else izpi_gpu_close(ctx);
   izpi_host_scene_free(host);
   izpi_scene_free(ps);
-  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u}\n", req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour",
-         ndev > 1 ? ndev : 1, post);
+  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u, \"bg_spd\": %u, \"tiles\": %d}\n",
+         req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour", ndev > 1 ? ndev : 1, post, req.num_bg_spd, ntiles);
   return 0;
 }

@@ -67,18 +67,25 @@ type Options struct {
 	PNGPipeline                        bool          // Gamma + Clamp(1.0) on the GPU (leader.go:179-182)
 }
 
-// Renderer renders one frame per Render call on one MI355X.
+// Renderer renders one frame per Render call on one MI355X (or several, Options.Devices).
+//
+// cgo pointer rules: every request passed to C is a Go value that holds C pointers only.
+// The spectral background and tile lists live in C.malloc memory, because Go memory
+// passed to C (the request) may not hold Go pointers.
 type Renderer struct {
 	ctx   *C.izpi_ctx   // single device, or device 0's context of m
 	m     *C.izpi_multi // multi-GPU form (Options.Devices), nil otherwise
 	ps    *C.izpi_proto_scene
 	host  *C.izpi_host_scene
 	req   C.izpi_render_req
-	bgWl  []float64
-	bgVal []float64
+	bg    *C.double // C.malloc: [75] wavelengths then [75] values of the spectral background, or nil
 	sizeX int
 	sizeY int
 }
+
+// Tile is one workUnit rectangle with inclusive bounds (renderer.go:56-70), as a
+// RenderTileRequest carries it (worker/render.go:18-21).
+type Tile struct{ X0, Y0, X1, Y1 int }
 
 func lastHostError() error { return errors.New(C.GoString(C.izpi_host_last_error())) }
 
@@ -198,12 +205,16 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 	if opt.SamplerType == sampler.SpectralSampler {
 		r.req.sampler = C.IZPI_SAMPLER_SPECTRAL
 		post |= C.IZPI_POST_SPECTRAL // FireflyRejection + XYZToRGB
-		if len(opt.SpectralBackground) == 75 {
-			r.bgWl = make([]float64, 75)
-			r.bgVal = append([]float64(nil), opt.SpectralBackground...)
-			for i := range r.bgWl {
-				r.bgWl[i] = 380 + 5*float64(i)
+		if len(opt.SpectralBackground) == 75 { // e.g. colours.SpectralBlack in leader mode (leader.go:142)
+			r.bg = (*C.double)(C.malloc(C.size_t(2 * 75 * 8)))
+			bg := unsafe.Slice((*float64)(unsafe.Pointer(r.bg)), 2*75)
+			for i := 0; i < 75; i++ {
+				bg[i] = 380 + 5*float64(i) // the CIE wavelengths of the 75 values
+				bg[75+i] = opt.SpectralBackground[i]
 			}
+			r.req.num_bg_spd = 75
+			r.req.bg_spd_wavelengths = r.bg
+			r.req.bg_spd_values = (*C.double)(unsafe.Add(unsafe.Pointer(r.bg), 75*8))
 		}
 	}
 	if opt.PNGPipeline {
@@ -217,13 +228,7 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 // Render mirrors RendererImpl.Render (renderer.go:108-222): the whole frame in one call.
 func (r *Renderer) Render(ctx context.Context) image.Image {
 	pix := make([]float64, r.sizeX*r.sizeY*4) // floatimage.NewFloat64NRGBA backing store (renderer.go:88)
-	req := r.req
-	if len(r.bgWl) > 0 {
-		// Go slices passed for the duration of the call: they hold no Go pointers
-		req.num_bg_spd = C.uint32_t(len(r.bgWl))
-		req.bg_spd_wavelengths = (*C.double)(unsafe.Pointer(&r.bgWl[0]))
-		req.bg_spd_values = (*C.double)(unsafe.Pointer(&r.bgVal[0]))
-	}
+	req := r.req                              // C pointers only
 	if r.m != nil {
 		if rc := C.izpi_gpu_multi_render(r.m, &req, (*C.double)(unsafe.Pointer(&pix[0])), nil); rc != 0 {
 			panic(r.deviceError("izpi_gpu_multi_render", rc))
@@ -235,6 +240,46 @@ func (r *Renderer) Render(ctx context.Context) image.Image {
 		panic(r.deviceError("izpi_gpu_render", rc)) // the reference log.Fatals on render errors
 	}
 	return floatimage.NewFloat64NRGBA(image.Rect(0, 0, r.sizeX, r.sizeY), pix)
+}
+
+// RenderTiles is the worker's RenderTile (worker/render.go:17-75) for a batch of
+// equal-sized tiles in one device call. Per tile it returns (Y1-Y0+1) rows of (X1-X0+1)*4
+// float64 — R,G,B (CIE X,Y,Z for the spectral sampler) and alpha 1 — row Y0 first: the
+// Pixels of the RenderTileResponse sequence the worker streams (Width = X1-X0+1,
+// Height = 1, PosY = y), with no post-processing, as in the worker. Tiles of different
+// sizes go in separate calls.
+func (r *Renderer) RenderTiles(tiles []Tile) ([][]float64, error) {
+	if len(tiles) == 0 {
+		return nil, nil
+	}
+	ct := (*C.uint32_t)(C.malloc(C.size_t(16 * len(tiles))))
+	defer C.free(unsafe.Pointer(ct))
+	t := unsafe.Slice((*uint32)(unsafe.Pointer(ct)), 4*len(tiles))
+	for i, tl := range tiles {
+		if tl.X0 < 0 || tl.Y0 < 0 || tl.X1 < tl.X0 || tl.Y1 < tl.Y0 {
+			return nil, fmt.Errorf("bad tile %+v", tl)
+		}
+		t[4*i], t[4*i+1], t[4*i+2], t[4*i+3] = uint32(tl.X0), uint32(tl.Y0), uint32(tl.X1), uint32(tl.Y1)
+	}
+	req := r.req // C pointers only
+	req.num_tiles = C.uint32_t(len(tiles))
+	req.tiles = ct
+	req.out_layout = C.IZPI_OUT_PACKED
+	req.post = C.IZPI_POST_NONE
+	packed := make([]float64, int(C.izpi_gpu_output_bytes(&req))/8)
+	var st C.izpi_render_stats
+	// on a multi-GPU renderer the batch runs on device 0 (r.ctx)
+	if rc := C.izpi_gpu_render(r.ctx, &req, (*C.double)(unsafe.Pointer(&packed[0])), &st); rc != 0 {
+		return nil, fmt.Errorf("izpi_gpu_render (tiles): status %d: %s", int(rc), C.GoString(C.izpi_gpu_last_error(r.ctx)))
+	}
+	out := make([][]float64, len(tiles))
+	off := 0
+	for i, tl := range tiles {
+		n := (tl.X1 - tl.X0 + 1) * (tl.Y1 - tl.Y0 + 1) * 4
+		out[i] = packed[off : off+n : off+n]
+		off += n
+	}
+	return out, nil
 }
 
 // Close releases the device context and the host-side scene.
@@ -254,6 +299,11 @@ func (r *Renderer) Close() {
 	if r.ps != nil {
 		C.izpi_scene_free(r.ps)
 		r.ps = nil
+	}
+	if r.bg != nil {
+		r.req.num_bg_spd, r.req.bg_spd_wavelengths, r.req.bg_spd_values = 0, nil, nil
+		C.free(unsafe.Pointer(r.bg))
+		r.bg = nil
 	}
 }
 

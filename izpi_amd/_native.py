@@ -5,13 +5,10 @@ their sizes against the compiled library's expectations. Loading fails loudly wh
 the native library is missing: there is no Python fallback for the hot path.
 """
 import ctypes as C
-import os
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 LIB_PATH = ROOT / "izpi_amd" / "_lib" / "libizpi_gpu.so"
-if os.environ.get("IZPI_LIB_PATH"):  # experiments only (tools/vrun.sh): a variant build of the same library
-    LIB_PATH = Path(os.environ["IZPI_LIB_PATH"])
 
 c_double_p = C.POINTER(C.c_double)
 c_uint32_p = C.POINTER(C.c_uint32)
@@ -19,7 +16,7 @@ c_float_p = C.POINTER(C.c_float)
 
 # ---- include/izpi_types.h
 COMM_ID_BYTES = 128
-IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE = range(6)
+IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE, IZPI_ERR_PEER = range(7)
 IZPI_ABI_VERSION = 1
 PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
 TEX_CONSTANT, TEX_IMAGE, TEX_SPECTRAL_GAUSSIAN, TEX_SPECTRAL_TABULATED, TEX_SPECTRAL_IMAGE = 1, 3, 5, 7, 9
@@ -82,12 +79,32 @@ class SceneDesc(C.Structure):
                 ("camera", Camera)]
 
 
+class RenderTuning(C.Structure):
+    _fields_ = [("slots", C.c_uint32), ("chunk_units", C.c_uint32), ("rec_dense", C.c_uint32),
+                ("pool_div", C.c_uint32), ("trace_chunk", C.c_uint32), ("refill_min", C.c_uint32),
+                ("prim_weight", C.c_uint32), ("flags", C.c_uint32), ("tail_paths", C.c_uint64)]
+
+
+TUNE_NO_DIST, TUNE_GENERAL_TRACE, TUNE_NO_LEAF_SHORTCUT, TUNE_SCALAR_SLAB, TUNE_NO_TAIL, TUNE_PASS_LOG = 1, 2, 4, 8, 16, 32
+
+
+def tuning(**kw):
+    """izpi_render_tuning from keyword fields; `flags` may also be given as a list of TUNE_* bits."""
+    t = RenderTuning()
+    for k, v in kw.items():
+        if k == "flags" and not isinstance(v, int):
+            v = sum(v)
+        setattr(t, k, v)
+    return t
+
+
 class RenderReq(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32),
                 ("sampler", C.c_uint32), ("out_layout", C.c_uint32), ("num_tiles", C.c_uint32),
                 ("num_bg_spd", C.c_uint32), ("tiles", c_uint32_p), ("bg_spd_wavelengths", c_double_p),
                 ("bg_spd_values", c_double_p), ("background", C.c_double * 3), ("seed", C.c_uint64),
-                ("post", C.c_uint32), ("pad_post", C.c_uint32), ("exposure", C.c_double)]
+                ("post", C.c_uint32), ("pad_post", C.c_uint32), ("exposure", C.c_double),
+                ("tuning", C.POINTER(RenderTuning))]
 
 
 class RenderStats(C.Structure):
@@ -99,7 +116,7 @@ class RenderStats(C.Structure):
                 ("tail_ms", C.c_double), ("tail_node_visits", C.c_uint64), ("tail_tri_tests", C.c_uint64),
                 ("tail_sph_tests", C.c_uint64), ("parks", C.c_uint64), ("workspace_bytes", C.c_uint64),
                 ("scene_bytes", C.c_uint64), ("slots", C.c_uint32), ("rec_dense", C.c_uint32),
-                ("pool_blocks", C.c_uint32), ("chunk_spp", C.c_uint32)]
+                ("pool_blocks", C.c_uint32), ("chunk_spp", C.c_uint32), ("alloc_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
@@ -169,7 +186,7 @@ class ObjMaterial(C.Structure):
 
 
 ABI_STRUCTS = [BVH4Node, Texture, Material, Camera, SceneDesc, RenderReq, RenderStats, Hit, TriIn, SphereIn, CameraIn,
-               SceneInput, ProtoInfo, ObjInfo, ObjGroup, ObjMaterial]
+               SceneInput, ProtoInfo, ObjInfo, ObjGroup, ObjMaterial, RenderTuning]
 
 # Symbols include/izpi_gpu.h and include/izpi_host.h declare (checked by tests).
 EXPORTS = [
@@ -178,7 +195,7 @@ EXPORTS = [
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
     "izpi_gpu_build_bvh4", "izpi_gpu_multi_open", "izpi_gpu_multi_close", "izpi_gpu_multi_last_error",
     "izpi_gpu_multi_size", "izpi_gpu_multi_context", "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render",
-    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
+    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_serialize", "izpi_scene_info", "izpi_scene_image_file",
@@ -235,6 +252,7 @@ def lib():
     L.izpi_gpu_comm_id.argtypes = [C.POINTER(C.c_uint8)]
     L.izpi_gpu_comm_init.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
     L.izpi_gpu_render_rank.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
+    L.izpi_gpu_debug_fault.argtypes = [C.c_void_p, C.c_int]
     L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]
     L.izpi_host_scene_prim_boxes.argtypes = [C.c_void_p, c_double_p]
     L.izpi_host_scene_set_bvh.argtypes = [C.c_void_p, C.POINTER(BVH4Node), C.c_uint32, c_uint32_p]

@@ -589,6 +589,7 @@ uint32_t izpi_abi_struct_size(int which) {
     case 13: return sizeof(izpi_obj_info);
     case 14: return sizeof(izpi_obj_group);
     case 15: return sizeof(izpi_obj_material);
+    case 16: return sizeof(izpi_render_tuning);
   }
   return 0;
 }

@@ -29,6 +29,7 @@
 
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <thread>
 
 #include "../../include/izpi_host.h"
@@ -2048,6 +2049,21 @@ __global__ void k_gomath(const DevScene sc, int op, const double* x, const doubl
 }
 
 // ================================================================ host side
+// Scratch device buffers of one ABI call, freed when it returns (on every path).
+struct DevBufs {
+  std::vector<void*> p;
+  template <typename T>
+  hipError_t alloc(T** out, size_t count) {
+    *out = nullptr;
+    const hipError_t e = hipMalloc((void**)out, count * sizeof(T));
+    if (e == hipSuccess) p.push_back(*out);
+    return e;
+  }
+  ~DevBufs() {
+    for (void* q : p) (void)hipFree(q);
+  }
+};
+
 struct izpi_ctx {
   int device = 0;
   std::string err;
@@ -2086,6 +2102,8 @@ struct izpi_ctx {
   // RCCL communicator of a multi-process render (izpi_gpu_comm_init), or null
   ncclComm_t comm = nullptr;
   uint32_t comm_rank = 0, comm_size = 1;
+  int32_t* d_status = nullptr;   // agreement word of izpi_gpu_render_rank ([0] in, [1] max over ranks)
+  int fault_inject = 0;          // izpi_gpu_debug_fault: 1 fail before rendering, 2 fail the render
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
@@ -2093,6 +2111,7 @@ struct izpi_ctx {
   bool const_albedo = false;     // ... and every albedo / emit texture a constant RGB: MATSET_CONST (Colour)
   bool any_uv = false;           // a material reads the hit's (u, v) (image textures)
   uint32_t pool_grow = 0;        // overflow pool doublings earned by frames that parked (render_impl)
+  uint32_t dev_share = 1;        // contexts of this process on this device (izpi_gpu_multi_open): they split its HBM
 };
 
 namespace {
@@ -2128,6 +2147,44 @@ uint64_t workspace_bytes(const izpi_ctx* ctx) {
   return (uint64_t)ctx->samples_cap + ctx->recs_cap + ctx->pool_cap + ctx->ring_cap + ctx->running_cap + ctx->out_cap +
          ctx->tiles_cap + ctx->utiles_cap + ctx->bg_cap + ctx->state_cap + ctx->spill_cap + ctx->post_cap + ctx->share_cap +
          ctx->gather_cap;
+}
+
+// Device bytes of the buffers render_impl sizes per frame and may release to re-size
+// (not the output, share, gather and post-processing buffers, which it never frees).
+uint64_t render_buffer_bytes(const izpi_ctx* ctx) {
+  return (uint64_t)ctx->samples_cap + ctx->recs_cap + ctx->pool_cap + ctx->ring_cap + ctx->running_cap + ctx->state_cap +
+         ctx->spill_cap;
+}
+
+struct RenderBuf {
+  void** p;
+  size_t* cap;
+  size_t bytes;
+};
+
+// Make every buffer of `b` at least its `bytes`: if any must grow, free them all first,
+// then allocate each at exactly its size.
+int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n) {
+  bool must = false;
+  for (size_t i = 0; i < n; i++) must = must || *b[i].cap < b[i].bytes;
+  if (!must) return IZPI_OK;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < n; i++) {
+    if (*b[i].p) HIP_TRY(hipFree(*b[i].p));
+    *b[i].p = nullptr;
+    *b[i].cap = 0;
+  }
+  for (size_t i = 0; i < n; i++) {
+    if (b[i].bytes == 0) continue;
+    const hipError_t e = hipMalloc(b[i].p, b[i].bytes);
+    if (e != hipSuccess) {
+      *b[i].p = nullptr;
+      ctx->err = "render workspace: hipMalloc of " + std::to_string(b[i].bytes) + " bytes: " + hipGetErrorString(e);
+      return IZPI_ERR_HIP;
+    }
+    *b[i].cap = b[i].bytes;
+  }
+  return IZPI_OK;
 }
 
 // The two sides of the wavefront state, `slots` entries each, in one allocation:
@@ -2172,11 +2229,11 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
 
 // Traversal kernel selection: k_trace2 with a 16-entry LDS stack ring and global spill,
 // 5 waves/SIMD. Instances: DIST (leaf tests spread over the wave; off only when primitive
-// indices do not fit the 26-bit LDS packing, or IZPI_TRACE_DIST=0) x TRI (sphere code
-// compiled out for triangle-only scenes; IZPI_TRACE_NO_TRI forces the general one).
-// Runtime knobs: IZPI_PRIM_W (default 32) weighs primitive steps against node steps
-// (x/16); IZPI_TRACE_CHUNK queue entries per dequeue; IZPI_REFILL_MIN idle lanes per
-// refill. All settings give identical results and counters.
+// indices do not fit the 26-bit LDS packing, or IZPI_TUNE_NO_DIST) x TRI (sphere code
+// compiled out for triangle-only scenes; IZPI_TUNE_GENERAL_TRACE forces the general one).
+// izpi_render_tuning: prim_weight (default 32) weighs primitive steps against node steps
+// (x/16); trace_chunk queue entries per dequeue; refill_min idle lanes per refill. All
+// settings give identical results and counters.
 #ifndef IZPI_TRACE_WPE
 #define IZPI_TRACE_WPE 5
 #endif
@@ -2188,34 +2245,43 @@ struct Tracer {
   // 16 -> 211 ms of k_trace2 per frame, 512 / 24 -> 201, 1024 -> 207, 2048 -> 216, 64 -> 303
   uint32_t prim_w = 32, tchunk = 512, refill_min = 24;
   int blocks = 0;
+  size_t spill_bytes = 0;  // the per-thread traversal-stack spill area this launch needs
 };
+
+const izpi_render_tuning kDefaultTuning{};
+inline const izpi_render_tuning& tuning_of(const izpi_render_req* req) {
+  return req && req->tuning ? *req->tuning : kDefaultTuning;
+}
 
 #define IZPI_T2_LIST(X) X(true, false) X(true, true) X(false, false) X(false, true)
 
-int make_tracer(izpi_ctx* ctx, Tracer* t) {
+// Pick the k_trace2 instance and its grid (no allocation: the caller grows d_spill to
+// t->spill_bytes).
+int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
   *t = Tracer();
-  if (const char* e = getenv("IZPI_TRACE_DIST")) t->p2 = atoi(e) != 0;
-  if (const char* e = getenv("IZPI_PRIM_W")) t->prim_w = (uint32_t)std::max(1, atoi(e));
-  if (const char* e = getenv("IZPI_TRACE_CHUNK")) t->tchunk = (uint32_t)std::max(1, atoi(e));
-  if (const char* e = getenv("IZPI_REFILL_MIN")) t->refill_min = (uint32_t)std::min(64, std::max(1, atoi(e)));
+  if (tu.flags & IZPI_TUNE_NO_DIST) t->p2 = false;
+  if (tu.prim_weight) t->prim_w = tu.prim_weight;
+  if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
+  if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
   // DIST packs (primitive << 6 | lane) into one LDS word
   if (ctx->num_prims >= (1u << 26)) t->p2 = false;
-  t->tri = ctx->sc.tri_only != 0 && !getenv("IZPI_TRACE_NO_TRI");
+  t->tri = ctx->sc.tri_only != 0 && !(tu.flags & IZPI_TUNE_GENERAL_TRACE);
   int rc = IZPI_ERR_INVALID;
 #define IZPI_T2_OCC(P, T) \
   if (t->p2 == P && t->tri == T) rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
 #undef IZPI_T2_OCC
   if (rc) return rc;
-  return grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, (size_t)t->blocks * 256 * 64 * sizeof(int32_t));
+  t->spill_bytes = (size_t)t->blocks * 256 * 64 * sizeof(int32_t);
+  return IZPI_OK;
 }
 
-void launch_trace(izpi_ctx* ctx, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
+void launch_trace(izpi_ctx* ctx, const DevScene& sc, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
   const dim3 g(t.blocks), b(256);
   const uint32_t stride = (uint32_t)t.blocks * 256;
 #define IZPI_T2_LAUNCH(P, T)                                                                                   \
   if (t.p2 == P && t.tri == T) {                                                                               \
-    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T>), g, b, 0, st, ctx->sc, wp, ctx->d_counters,     \
+    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T>), g, b, 0, st, sc, wp, ctx->d_counters,          \
                        ctx->d_misc + 1, spill, stride, t.prim_w, t.tchunk, t.refill_min);                      \
     return;                                                                                                    \
   }
@@ -2240,22 +2306,22 @@ uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint3
 // in k_tail); k_accumulate folds the chunk's per-sample radiance into the pixels in
 // sample order.
 template <int SAMPLER, int MATSET>
-int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveParams& wp, AccumParams& ap,
-               uint32_t num_pixels, uint32_t chunk, uint32_t pool_blocks, float* trace_ms, float* shade_ms, float* tail_ms,
-               uint32_t* launches) {
+int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, const Tracer& tr, ShadeParams& sp,
+               WaveParams& wp, AccumParams& ap, uint32_t num_pixels, uint32_t chunk, uint32_t pool_blocks,
+               float* trace_ms, float* shade_ms, float* tail_ms, uint32_t* launches) {
   hipStream_t st = ctx->stream;
+  const izpi_render_tuning& tu = tuning_of(req);
   int shade_res = 0;
-  Tracer tr;
-  int rc = make_tracer(ctx, &tr);
+  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res);
   if (rc) return rc;
-  if ((rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res))) return rc;
   // tail kernel: used once every unit has started and at most `tail_max` paths remain
   const bool tail_deep = ctx->stack_needed > 32;
   int tail_res = 0;
   if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res)
                       : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
   uint64_t tail_max = (uint64_t)tail_res * 256;
-  if (const char* e = getenv("IZPI_TAIL")) tail_max = strtoull(e, nullptr, 10);
+  if (tu.tail_paths) tail_max = tu.tail_paths;
+  if (tu.flags & IZPI_TUNE_NO_TAIL) tail_max = 0;
   // k_tail's allocations cannot park: every tail path must find a published block
   if (sp.rec_pool) tail_max = std::min<uint64_t>(tail_max, pool_blocks);
   const WaveBuf q[2] = {wp.in, wp.out};  // the two sides of the state; entry counts in d_misc[3..4]
@@ -2272,7 +2338,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, 3 * sizeof(uint32_t), st));  // dequeue cursor, queue counts
     HIP_TRY(hipMemsetAsync(ctx->d_misc + 6, 0, 2 * sizeof(uint32_t), st));  // park flags of the two sides
     wp.out = q[0]; wp.out_count = qn[0];
-    hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, ctx->sc, sp, wp);
+    hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, sc, sp, wp);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2286,7 +2352,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
     // k_tail takes over as soon as few enough paths remain instead of up to 8 passes later
     // (each of those last passes costs ~0.3-1 ms of mostly idle machine).
     int B = IZPI_PASS_BATCH;
-    const bool pass_log = getenv("IZPI_PASS_LOG") != nullptr;  // diagnostics: per-pass times on stderr
+    const bool pass_log = (tu.flags & IZPI_TUNE_PASS_LOG) != 0;  // diagnostics: per-pass times on stderr
     while (n > 0) {
       for (int b = 0; b < B; b++) {
         wp.in = q[cur]; wp.in_count = qn[cur];
@@ -2294,10 +2360,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         wp.in_park = ctx->d_misc + 6 + cur; wp.out_park = ctx->d_misc + 6 + (1 - cur);
         // (k_trace2 zeroes out_count and out_park, k_shade the dequeue cursor for the next pass)
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
-        launch_trace(ctx, tr, wp, st, ctx->d_spill);
+        launch_trace(ctx, sc, tr, wp, st, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
-        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, sc, sp, wp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
@@ -2321,8 +2387,8 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, ShadeParams& sp, WaveP
         wp.in = q[cur]; wp.in_count = qn[cur];
         HIP_TRY(hipEventRecord(ctx->ev2, st));
         if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
-        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
-        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, ctx->sc, sp, wp);
+        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp);
+        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev3, st));
         HIP_TRY(hipEventSynchronize(ctx->ev3));
@@ -2381,6 +2447,7 @@ int apply_post(izpi_ctx* ctx, const izpi_render_req* req, double* canvas_dev) {
 }
 
 int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
+  if (ctx->fault_inject == 2) { ctx->err = "injected render fault (izpi_gpu_debug_fault)"; return IZPI_ERR_DEVICE; }
   if (!ctx->have_scene) { ctx->err = "render before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
   if (req->sampler != IZPI_SAMPLER_COLOUR && req->sampler != IZPI_SAMPLER_SPECTRAL) { ctx->err = "unsupported sampler"; return IZPI_ERR_UNSUPPORTED; }
@@ -2405,16 +2472,25 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (num_pixels64 > (1ull << 30)) { ctx->err = "too many pixels in one request"; return IZPI_ERR_INVALID; }
   const uint32_t num_pixels = (uint32_t)num_pixels64;
   if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
-  // Sizing against the HBM this context may use: what is free plus its own workspace
-  // (which a later frame reuses), so that every frame of a renderer sizes alike.
+  const izpi_render_tuning& tu = tuning_of(req);
+  // this render's view of the scene: the traversal shortcuts the tuning switches off
+  DevScene sc = ctx->sc;
+  if (tu.flags & IZPI_TUNE_NO_LEAF_SHORTCUT) sc.leaf_shortcut = 0;
+  if (tu.flags & IZPI_TUNE_SCALAR_SLAB) sc.nan_free_bounds = 0;
+  Tracer tr;
+  int trc = make_tracer(ctx, tu, &tr);
+  if (trc) return trc;
+  // Sizing against the HBM this context may use: what is free plus the render buffers it
+  // holds and would release (a later frame reuses them, so every frame of a renderer sizes
+  // alike), shared evenly by the contexts of one process on this device.
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-  const uint64_t avail = free_b ? (uint64_t)free_b + workspace_bytes(ctx) : 0;
+  const uint64_t avail = free_b ? ((uint64_t)free_b + render_buffer_bytes(ctx)) / std::max(1u, ctx->dev_share) : 0;
   // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
   // sample order. One chunk per request when it fits in 1/4 of the HBM (C3: 12.9 GB of
   // 288 GB), so the wavefront drains once per frame instead of once per chunk.
   uint64_t max_units = std::max<uint64_t>(64ull << 20, (avail / 4) / (3 * sizeof(double)));
-  if (const char* e = getenv("IZPI_CHUNK_UNITS")) max_units = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  if (tu.chunk_units) max_units = tu.chunk_units;
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
   // blocks (ShadeParams::rec_pool). Colour records are 48 B (24 B compact), spectral 32 B.
@@ -2429,7 +2505,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // (C5 256 spp first frame 8854 -> 8130 ms; 92 GB of workspace, less than a pool twice the
   // size would take).
   uint32_t rec_dense = spectral ? 32u : 8u;
-  if (const char* e = getenv("IZPI_REC_DENSE")) rec_dense = (uint32_t)std::max(1, atoi(e));
+  if (tu.rec_dense) rec_dense = tu.rec_dense;
   rec_dense = std::min(rec_dense, max_depth);
   const uint32_t rec_pool = max_depth - rec_dense;
   // PathCold (wavelength, dielectric point) is read only by the spectral sampler and glass
@@ -2441,7 +2517,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // too: 371 ms at 40M, 349 ms at 250M); C5 at 64 spp 120M slots: -6%; C4 100M: -3%.
   // The state stays within half of the HBM (below).
   uint64_t slot_cap = 256ull << 20;
-  if (const char* e = getenv("IZPI_SLOTS")) slot_cap = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
+  if (tu.slots) slot_cap = std::max<uint64_t>(1024, tu.slots);
   const uint64_t per_slot = 2 * (sizeof(RayOD) + sizeof(uint32_t) + (ctx->sc.tri_only ? 0 : sizeof(double)) + sizeof(PathHot) +
                                  sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(HitSt)) +
                             (uint64_t)rec_dense * D * sizeof(double);
@@ -2452,7 +2528,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // still parks more than 1/64 of its rays doubles the pool for the renderer's next frame.
   uint32_t pool_div = (spectral || !ctx->basic_materials) ? 4u : 16u;
   pool_div = std::max(1u, pool_div >> std::min(ctx->pool_grow, 4u));
-  if (const char* e = getenv("IZPI_POOL_DIV")) pool_div = (uint32_t)std::max(1, atoi(e));
+  if (tu.pool_div) pool_div = tu.pool_div;
   const uint64_t per_block = (uint64_t)rec_pool * D * sizeof(double) + sizeof(uint32_t);
   // The wavefront state within half of the HBM. The overflow pool rounds up to a power of
   // two per ring, up to twice slots / pool_div blocks: counted at that worst case (C4 at
@@ -2465,21 +2541,28 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
     pool_blocks = POOL_SHARDS * 16;
     while (pool_blocks < slots / pool_div && pool_blocks < (1u << 30)) pool_blocks <<= 1;
   }
-  if ((rc = grow(ctx, (void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * 3 * sizeof(double)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_recs, &ctx->recs_cap, (size_t)rec_dense * D * slots * sizeof(double)))) return rc;
-  if (rec_pool) {
-    if ((rc = grow(ctx, (void**)&ctx->d_pool, &ctx->pool_cap, (size_t)pool_blocks * rec_pool * D * sizeof(double)))) return rc;
-    if ((rc = grow(ctx, (void**)&ctx->d_ring, &ctx->ring_cap, (size_t)pool_blocks * sizeof(uint32_t)))) return rc;
-  }
-  if ((rc = grow(ctx, (void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)))) return rc;
-  if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
   const bool need_time = !ctx->sc.tri_only;  // only sphere tests read the ray time
-  if ((rc = grow(ctx, (void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, nullptr))))
-    return rc;
+  // The render buffers this frame needs. When one of them must grow, all are released
+  // before any is allocated, so a frame never holds an old buffer next to a new one (the
+  // sizing above counted every one of them as available).
+  const auto t_alloc0 = std::chrono::steady_clock::now();
+  RenderBuf need[] = {
+      {(void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * 3 * sizeof(double)},
+      {(void**)&ctx->d_recs, &ctx->recs_cap, (size_t)rec_dense * D * slots * sizeof(double)},
+      {(void**)&ctx->d_pool, &ctx->pool_cap, rec_pool ? (size_t)pool_blocks * rec_pool * D * sizeof(double) : 0},
+      {(void**)&ctx->d_ring, &ctx->ring_cap, rec_pool ? (size_t)pool_blocks * sizeof(uint32_t) : 0},
+      {(void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)},
+      {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, nullptr)},
+      {(void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes},
+  };
+  if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0])))) return rc;
+  if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
+  const size_t nbg = req->num_bg_spd;
+  if (nbg && (!req->bg_spd_wavelengths || !req->bg_spd_values)) { ctx->err = "num_bg_spd without the SPD arrays"; return IZPI_ERR_INVALID; }
+  if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
+  const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count();
   WaveBuf bufs[2];
   carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, bufs);
-  const size_t nbg = req->num_bg_spd;
-  if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
   hipStream_t st = ctx->stream;
   HIP_TRY(hipMemcpyAsync(ctx->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   if (nbg) {
@@ -2501,7 +2584,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.rec_dense = rec_dense; sp.rec_pool = rec_pool;
   sp.pool_shift = 0;
   while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
-  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = ctx->sc.mat_const; sp.head = ctx->d_misc;
+  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = ctx->d_misc;
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
@@ -2519,7 +2602,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   float trace_ms = 0, shade_ms = 0, tail_ms = 0;
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
-#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches)
+#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sc, tr, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches)
   // the smallest compiled material set holding the scene's material kinds
   const uint32_t ms = ctx->matset;
   const int set = ms == 0 ? MATSET_BASIC : (ms & ~(uint32_t)MATSET_SURF) == 0 ? MATSET_SURF : MATSET_FULL;
@@ -2555,6 +2638,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.workspace_bytes = workspace_bytes(ctx);
   s.scene_bytes = ctx->scene_bytes;
   s.slots = slots; s.rec_dense = rec_dense; s.pool_blocks = pool_blocks; s.chunk_spp = chunk;
+  s.alloc_ms = alloc_ms;
   if (rec_pool && s.parks * 64 > s.rays && pool_blocks < slots) ctx->pool_grow++;
 #ifdef IZPI_SHADE_CLOCKS
   fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu (wave cycles)\n", cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL],
@@ -2691,7 +2775,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_pool, ctx->d_ring, ctx->d_pool_ctr, ctx->d_running, ctx->d_out,
                   ctx->d_tiles, ctx->d_utiles, ctx->d_bg, ctx->d_misc, ctx->d_counters, ctx->d_state,
                   ctx->d_spill, ctx->d_post, ctx->d_share,
-                  ctx->d_gather};
+                  ctx->d_gather, ctx->d_status};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb[i]) (void)hipEventDestroy(ctx->evb[i]);
@@ -2952,7 +3036,6 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   for (uint32_t i = 0; i < d->num_materials; i++)
     if (d->materials[i].kind == IZPI_MAT_DIELECTRIC) sc.no_pathlen = 0;
   sc.leaf_shortcut = leaf_shortcut;
-  if (getenv("IZPI_NO_LEAF_SHORTCUT")) sc.leaf_shortcut = 0;
   sc.nan_free_bounds = 1;
   for (const GInner& g : inner) {
     const float* f = g.mnx;  // the 24 bounds are contiguous
@@ -2960,7 +3043,6 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   }
   for (const GLeaf& L : leaves)  // leaf re-tests run through the same 4-slot test
     for (int i = 0; i < 3; i++) if (L.mn[i] != L.mn[i] || L.mx[i] != L.mx[i]) sc.nan_free_bounds = 0;
-  if (getenv("IZPI_NO_FAST_SLAB")) sc.nan_free_bounds = 0;
   sc.cam = d->camera;
   // traversal stack bound (see host_scene.cpp stack_bound)
   {
@@ -3108,13 +3190,14 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (!ctx->have_scene) { ctx->err = "no scene"; return IZPI_ERR_NO_SCENE; }
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
+  DevBufs tmp;  // freed on every return
   double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; HitSt* hh;
-  HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 8 * sizeof(double)));
-  HIP_TRY(hipMalloc((void**)&dh, (size_t)n * sizeof(izpi_hit)));
-  HIP_TRY(hipMalloc((void**)&rr, (size_t)n * sizeof(RayOD)));
-  HIP_TRY(hipMalloc((void**)&kk, (size_t)n * sizeof(uint32_t)));
-  HIP_TRY(hipMalloc((void**)&tm, (size_t)n * sizeof(double2)));
-  HIP_TRY(hipMalloc((void**)&hh, (size_t)n * sizeof(HitSt)));
+  HIP_TRY(tmp.alloc(&dr, (size_t)n * 8));
+  HIP_TRY(tmp.alloc(&dh, n));
+  HIP_TRY(tmp.alloc(&rr, n));
+  HIP_TRY(tmp.alloc(&kk, n));
+  HIP_TRY(tmp.alloc(&tm, n));
+  HIP_TRY(tmp.alloc(&hh, n));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
@@ -3123,15 +3206,15 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh;
   wp.in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
-  int rc = make_tracer(ctx, &tr);
+  int rc = make_tracer(ctx, kDefaultTuning, &tr);
   if (rc) return rc;
-  launch_trace(ctx, tr, wp, ctx->stream, ctx->d_spill);
+  if ((rc = grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes))) return rc;
+  launch_trace(ctx, ctx->sc, tr, wp, ctx->stream, ctx->d_spill);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, n, dh);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));
-  (void)hipFree(dr); (void)hipFree(dh); (void)hipFree(rr); (void)hipFree(kk); (void)hipFree(tm); (void)hipFree(hh);
   return IZPI_OK;
 }
 
@@ -3194,6 +3277,11 @@ int izpi_gpu_multi_open(const int* devices, uint32_t num_devices, izpi_multi** o
       return rc;
     }
     m->ctx.push_back(c);
+  }
+  // contexts on one device split its HBM when they size their workspaces
+  for (izpi_ctx* c : m->ctx) {
+    c->dev_share = 0;
+    for (izpi_ctx* o : m->ctx) c->dev_share += o->device == c->device ? 1u : 0u;
   }
   // device 0 receives every share: let it read/write peers directly over xGMI
   for (uint32_t i = 1; i < num_devices; i++) {
@@ -3308,6 +3396,9 @@ int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint
   if (!id || nranks == 0 || rank >= nranks) { ctx->err = "comm_init: bad arguments"; return IZPI_ERR_INVALID; }
   HIP_TRY(hipSetDevice(ctx->device));
   if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+  // the status word of izpi_gpu_render_rank's agreement steps, allocated here so that a
+  // render never fails to reach them for want of it
+  if (!ctx->d_status) HIP_TRY(hipMalloc((void**)&ctx->d_status, 2 * sizeof(int32_t)));
   ncclUniqueId u;
   memcpy(u.internal, id, IZPI_COMM_ID_BYTES);
   const ncclResult_t r = ncclCommInitRank(&ctx->comm, (int)nranks, u, (int)rank);
@@ -3321,28 +3412,86 @@ int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint
   return IZPI_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Agreement step of a multi-rank render: every rank contributes (status << 16 | rank) and
+// all receive the maximum, i.e. the worst status and the highest rank that had it
+// (ncclAllReduce(max), rccl.h). Returns non-zero only if the collective itself failed.
+int agree_status(izpi_ctx* ctx, int local, int* worst_status, uint32_t* worst_rank) {
+  const int32_t word = (int32_t)((uint32_t)std::min(local, 0x7FFF) << 16 | (ctx->comm_rank & 0xFFFFu));
+  int32_t* h = (int32_t*)ctx->h_count + 6;  // pinned
+  h[0] = word;
+  HIP_TRY(hipMemcpyAsync(ctx->d_status, h, sizeof(word), hipMemcpyHostToDevice, ctx->stream));
+  const ncclResult_t r = ncclAllReduce(ctx->d_status, ctx->d_status + 1, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
+  if (r != ncclSuccess) { ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r); return IZPI_ERR_HIP; }
+  HIP_TRY(hipMemcpyAsync(h + 1, ctx->d_status + 1, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  const int32_t out = h[1];
+  *worst_status = (int)((uint32_t)out >> 16);
+  *worst_rank = (uint32_t)out & 0xFFFFu;
+  return IZPI_OK;
+}
+
+// A rank whose own step succeeded returns IZPI_ERR_PEER when another rank's failed.
+int peer_failure(izpi_ctx* ctx, int worst, uint32_t worst_rank, const char* when) {
+  ctx->err = "rank " + std::to_string(worst_rank) + " failed " + when + " (status " + std::to_string(worst) + ")";
+  return IZPI_ERR_PEER;
+}
+}  // namespace
+
+extern "C" {
+
+// Every rank runs the same sequence of collectives whatever fails locally, so no rank is
+// left waiting in one (render/remote.go:40-55 logs a failed remote tile; here every rank
+// learns the worst status):
+//   1. local checks and buffers (share block; gather buffer on rank 0), then agree: if any
+//      rank failed, all return before rendering;
+//   2. render the share (a failed share posts a zeroed block), ncclGather to rank 0, agree
+//      again: if any rank failed, all return it and rank 0 does not assemble;
+//   3. rank 0 assembles and post-processes (a failure there is rank 0's alone).
 int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats) {
   if (!ctx) return IZPI_ERR_INVALID;
-  if (!ctx->comm) { ctx->err = "render_rank before izpi_gpu_comm_init"; return IZPI_ERR_INVALID; }
-  if (ctx->comm_rank == 0 && !out_dev) { ctx->err = "rank 0 needs an output canvas"; return IZPI_ERR_INVALID; }
-  if (req && req->post != IZPI_POST_NONE && req->num_tiles != 0) { ctx->err = "post-processing needs a whole-frame request"; return IZPI_ERR_INVALID; }
-  HIP_TRY(hipSetDevice(ctx->device));
-  Shares sh;
-  int rc = make_shares(ctx, req, ctx->comm_size, sh);
-  if (rc) return rc;
-  // a failed share still joins the gather (the other ranks wait in it), then reports
-  const int rrc = render_share(ctx, req, sh, ctx->comm_rank);
-  if (!ctx->d_share || ctx->share_cap < sh.block * sizeof(double)) return rrc ? rrc : IZPI_ERR_HIP;
+  // without a communicator no collective can run: every rank in this state returns here
+  if (!ctx->comm || !ctx->d_status) { ctx->err = "render_rank before izpi_gpu_comm_init"; return IZPI_ERR_INVALID; }
+  memset(&ctx->last, 0, sizeof(ctx->last));
   if (stats) *stats = ctx->last;
-  if (ctx->comm_rank == 0 &&
-      (rc = grow(ctx, (void**)&ctx->d_gather, &ctx->gather_cap, (size_t)ctx->comm_size * sh.block * sizeof(double)))) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  // ---- 1
+  Shares sh;
+  int prc = IZPI_OK;
+  if (ctx->comm_rank == 0 && !out_dev) { ctx->err = "rank 0 needs an output canvas"; prc = IZPI_ERR_INVALID; }
+  else if (req && req->post != IZPI_POST_NONE && req->num_tiles != 0) { ctx->err = "post-processing needs a whole-frame request"; prc = IZPI_ERR_INVALID; }
+  if (!prc) prc = make_shares(ctx, req, ctx->comm_size, sh);
+  if (!prc) prc = grow(ctx, (void**)&ctx->d_share, &ctx->share_cap, sh.block * sizeof(double));
+  if (!prc && ctx->comm_rank == 0) prc = grow(ctx, (void**)&ctx->d_gather, &ctx->gather_cap, (size_t)ctx->comm_size * sh.block * sizeof(double));
+  if (prc == IZPI_OK && ctx->fault_inject == 1) { ctx->err = "injected fault before rendering"; prc = IZPI_ERR_DEVICE; }
+  int worst = 0;
+  uint32_t wr = 0;
+  int rc = agree_status(ctx, prc, &worst, &wr);
+  if (rc) return rc;
+  if (prc) return prc;
+  if (worst) return peer_failure(ctx, worst, wr, "before rendering");
+  // ---- 2
+  const int rrc = render_share(ctx, req, sh, ctx->comm_rank);
+  if (stats) *stats = ctx->last;
+  if (rrc) (void)hipMemsetAsync(ctx->d_share, 0, sh.block * sizeof(double), ctx->stream);
   // ncclGather (rccl.h:745): block r of the root's buffer = rank r's packed share
   const ncclResult_t r = ncclGather(ctx->d_share, ctx->comm_rank == 0 ? ctx->d_gather : nullptr, sh.block, ncclFloat64, 0,
                                     ctx->comm, ctx->stream);
   if (r != ncclSuccess) { ctx->err = std::string("ncclGather: ") + ncclGetErrorString(r); return IZPI_ERR_HIP; }
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if ((rc = agree_status(ctx, rrc, &worst, &wr))) return rc;
   if (rrc) return rrc;
+  if (worst) return peer_failure(ctx, worst, wr, "while rendering its share");
+  // ---- 3
   if (ctx->comm_rank == 0 && (rc = assemble(ctx, req, sh, out_dev))) return rc;
+  return IZPI_OK;
+}
+
+int izpi_gpu_debug_fault(izpi_ctx* ctx, int where) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  ctx->fault_inject = where;
   return IZPI_OK;
 }
 

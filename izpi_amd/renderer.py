@@ -18,7 +18,6 @@ are gathered to device 0, which scatters them into the canvas. Two forms:
 Per pixel-sample RNG streams make the image independent of the partition.
 """
 import ctypes as C
-import os
 
 import numpy as np
 
@@ -39,8 +38,8 @@ def _check(rc, ctx, what):
 
 def build_bvh4(ctx, boxes, leaf_max=4, method=None):
     """izpi_gpu_build_bvh4 on context `ctx` over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
-    if method is None:  # IZPI_BVH_METHOD=lbvh|ploc overrides the default (experiments)
-        method = {"lbvh": N.BVH_LBVH, "ploc": N.BVH_PLOC}.get(os.environ.get("IZPI_BVH_METHOD", ""), GPU_BVH_METHOD)
+    if method is None:
+        method = GPU_BVH_METHOD
     boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
     n = len(boxes)
     nodes = np.zeros((max(1, 2 * n), 128), np.uint8)
@@ -55,8 +54,9 @@ def build_bvh4(ctx, boxes, leaf_max=4, method=None):
 
 
 def make_request(width, height, spp, max_depth, sampler, background, seed, exposure, bg_spd=None, tiles=None,
-                 layout=N.OUT_CANVAS, post=N.POST_NONE):
-    """izpi_render_req for Render (the arrays it points to are kept alive on `req._keep`)."""
+                 layout=N.OUT_CANVAS, post=N.POST_NONE, tuning=None):
+    """izpi_render_req for Render (the arrays it points to are kept alive on `req._keep`).
+    tuning: an N.RenderTuning (launch settings; None = the library's defaults)."""
     req = N.RenderReq()
     req.post = post
     req.exposure = exposure
@@ -79,6 +79,9 @@ def make_request(width, height, spp, max_depth, sampler, background, seed, expos
         req.num_bg_spd = wl.size
         req.bg_spd_wavelengths = wl.ctypes.data_as(C.POINTER(C.c_double))
         req.bg_spd_values = val.ctypes.data_as(C.POINTER(C.c_double))
+    if tuning is not None:
+        keep.append(tuning)
+        req.tuning = C.pointer(tuning)
     req._keep = keep
     return req
 
@@ -95,10 +98,12 @@ def common_tiles(width, height):
 class GPURenderer:
     def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
                  spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference",
-                 bvh_leaf_max=None):
+                 bvh_leaf_max=None, tuning=None):
         """bvh="reference": hitable.NewBVH4's tree, rebuilt bit for bit on the host (the
         parity default); bvh="gpu": the GPU linear BVH4 builder (izpi_gpu_build_bvh4),
-        same node format, different topology."""
+        same node format, different topology. tuning: an
+        N.RenderTuning for every request (None = library defaults)."""
+        self.tuning = tuning
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
@@ -138,7 +143,7 @@ class GPURenderer:
     def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None, post=N.POST_NONE):
         return make_request(self.width, self.height, self.spp if spp is None else int(spp), self.max_depth,
                             self.sampler, self.background, self.seed, self.exposure, (self._bg_wl, self._bg_val),
-                            tiles, layout, post)
+                            tiles, layout, post, self.tuning)
 
     # --------------------------------------------------------------- render
     @property
@@ -246,7 +251,8 @@ class MultiGPURenderer:
 
     def __init__(self, scene, width, height, spp, devices, max_depth=50, sampler=N.SAMPLER_COLOUR,
                  background=(0.0, 0.0, 0.0), spectral_background=None, seed=12345, bvh_seed=12345, bvh="gpu",
-                 bvh_leaf_max=None):
+                 bvh_leaf_max=None, tuning=None):
+        self.tuning = tuning
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
@@ -289,7 +295,7 @@ class MultiGPURenderer:
         to_host=False (the canvas stays on device 0: the timing form). self.stats is the
         list of per-device stats."""
         req = make_request(self.width, self.height, self.spp, self.max_depth, self.sampler, self.background,
-                           self.seed, self.exposure, self._bg, None, N.OUT_CANVAS, post)
+                           self.seed, self.exposure, self._bg, None, N.OUT_CANVAS, post, self.tuning)
         G = len(self.devices)
         st = (N.RenderStats * G)()
         if to_host and canvas is None:

@@ -1,4 +1,4 @@
-"""The Go shim's exact C call sequence (integration/go/render/gpu/renderer_gpu.go:90-235,
+"""The Go shim's exact C call sequence (integration/go/render/gpu/renderer_gpu.go:101-283,
 replayed by integration/c/go_shim_replay.c) on proto.Marshal-form wire bytes of a scene
 file: parse_binary -> set_image -> scene_to_input -> build_scene_ex(SKIP_BVH) ->
 build_bvh4 -> set_bvh -> upload -> render with Render's post flags. The canvas must equal
@@ -24,7 +24,7 @@ def test_replay_binary_links_and_reports_usage():
     assert out.returncode == 1 and "usage" in out.stderr
 
 
-def _replay(tmp_path, text, png, devices):
+def _replay(tmp_path, text, png, devices, extra=()):
     izpi = tmp_path / "scene.izpi"
     izpi.write_bytes(ingest.ProtoScene(text.encode()).to_wire())
     raw = tmp_path / "canvas.f64"
@@ -33,9 +33,11 @@ def _replay(tmp_path, text, png, devices):
         cmd.append("--png-pipeline")
     if devices:
         cmd += ["--devices", ",".join(map(str, devices))]
+    cmd += list(extra)
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    return json.loads(out.stdout.strip().splitlines()[-1]), np.fromfile(raw, np.float64).reshape(40, 40, 4), izpi
+    data = np.fromfile(raw, np.float64)
+    return json.loads(out.stdout.strip().splitlines()[-1]), (data if extra else data.reshape(40, 40, 4)), izpi
 
 
 @pytest.mark.gpu
@@ -51,3 +53,46 @@ def test_go_shim_call_sequence_bitwise(gpu, tmp_path, which, png, devices):
     want = r.render(post=post)
     r.close()
     assert got.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_go_shim_spectral_black_background_bitwise(gpu, tmp_path, devices):
+    """Leader mode passes colours.SpectralBlack (75 zeros, leader.go:142) as the spectral
+    background: the shim holds it in C.malloc memory (cgo pointer rules) and the render
+    equals the Python host's with the same background."""
+    info, got, izpi = _replay(tmp_path, EXAMPLE.read_text(), False, devices, ["--bg-spd"])
+    assert info["bg_spd"] == 75
+    got = got.reshape(40, 40, 4)
+    s = ingest.ProtoScene.from_file(izpi)
+    wl = 380.0 + 5.0 * np.arange(75)
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", spectral_background=(wl, np.zeros(75)))
+    want = r.render(post=N.POST_SPECTRAL)
+    r.close()
+    assert got.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["spectral", "rgb"])
+def test_go_shim_render_tiles_bitwise(gpu, tmp_path, which):
+    """RenderTiles (the worker's RenderTile, worker/render.go:17-75): the frame's first
+    tiles packed row by row from y0, alpha 1, no post-processing, equal to the same pixels
+    of the Python host's whole-frame canvas (row H - y, rgb.go:41)."""
+    from izpi_amd.renderer import common_tiles
+    text = EXAMPLE.read_text() if which == "spectral" else configs.cornell_rgb_pbtxt(1.0)
+    info, got, izpi = _replay(tmp_path, text, False, None, ["--tiles", "3"])
+    assert info["tiles"] == 3
+    s = ingest.ProtoScene.from_file(izpi)
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu")
+    canvas = r.render()  # raw XYZ / RGB, no post
+    r.close()
+    want = []
+    for x0, y0, x1, y1 in common_tiles(40, 40)[:3]:
+        for y in range(y0, y1 + 1):
+            row = 40 - y
+            want.append(canvas[row, x0:x1 + 1] if row < 40 else np.full((x1 - x0 + 1, 4), np.nan))
+    want = np.concatenate(want).reshape(-1)
+    known = ~np.isnan(want)  # sample row 0 lands on canvas row H, which the canvas drops (A9)
+    assert got.size == want.size
+    assert got[known].tobytes() == want[known].tobytes()
+    assert np.all(got.reshape(-1, 4)[:, 3] == 1.0)

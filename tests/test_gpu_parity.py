@@ -148,13 +148,12 @@ def test_render_dragon_small_bitwise(gpu):
     r.close()
 
 
-@pytest.mark.parametrize("tail", ["default", "0"])
-def test_render_spectral_glass_bitwise(gpu, tail, monkeypatch):
+@pytest.mark.parametrize("tail", ["default", "none"])
+def test_render_spectral_glass_bitwise(gpu, tail):
     """Dielectric spheres: path-length rays, sphere tests; with and without k_tail."""
-    if tail != "default":
-        monkeypatch.setenv("IZPI_TAIL", tail)
+    tu = N.tuning(flags=N.TUNE_NO_TAIL) if tail == "none" else None
     scene = configs.cornell_glass_spectral()
-    r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL)
+    r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL, tuning=tu)
     img = r.render()
     ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_SPECTRAL)
     assert_parity(img, ref, r.stats, ostats)
@@ -201,18 +200,18 @@ def test_tiles_packed_and_unpack(gpu):
 
 
 @pytest.mark.parametrize("name", ["C4", "C3"])
-def test_queue_keeps_every_slot_while_units_remain(gpu, name, monkeypatch, capfd):
+def test_queue_keeps_every_slot_while_units_remain(gpu, name, capfd):
     """While work units remain, every finished path's record slot starts a new unit, so the
     queue stays at its first-fill length. (Round 2 regression: a block-iteration with no
     finished path marked its block "units exhausted" for the rest of the pass; on C4 the
     queue of 42M entries collapsed to one iteration per block and the frame took 3304
     passes instead of ~100. Images were still bit-exact, only slower.)"""
-    monkeypatch.setenv("IZPI_PASS_LOG", "1")
-    monkeypatch.setenv("IZPI_SLOTS", "600000")  # several shading iterations per block, units >> slots
+    # several shading iterations per block, units >> slots
+    tu = N.tuning(flags=N.TUNE_PASS_LOG, slots=600000)
     cfg = configs.configs()[name]
     scene = cfg.build() if name == "C4" else configs.cornell_dragon(1.0, n=60)
     W, H, spp = (192, 108, 64) if name == "C4" else (128, 128, 64)
-    r = GPURenderer(scene, W, H, spp)
+    r = GPURenderer(scene, W, H, spp, tuning=tu)
     r.render()
     units = W * H * spp
     log = capfd.readouterr().err
@@ -228,53 +227,49 @@ def test_queue_keeps_every_slot_while_units_remain(gpu, name, monkeypatch, capfd
     r.close()
 
 
-@pytest.mark.parametrize("env", [{"IZPI_PRIM_W": "1"},
-                                 {"IZPI_PRIM_W": "100000"}, {"IZPI_SLOTS": "3000", "IZPI_CHUNK_UNITS": "5000"},
-                                 {"IZPI_NO_LEAF_SHORTCUT": "1"}, {"IZPI_TRACE_CHUNK": "1", "IZPI_REFILL_MIN": "1"},
-                                 {"IZPI_TRACE_DIST": "0"},
-                                 {"IZPI_TAIL": "0"}, {"IZPI_TAIL": "0", "IZPI_SLOTS": "3000"},
-                                 {"IZPI_TRACE_NO_TRI": "1"},
-                                 {"IZPI_REC_DENSE": "1", "IZPI_POOL_DIV": "100000"},
-                                 {"IZPI_REC_DENSE": "2", "IZPI_POOL_DIV": "100000", "IZPI_TAIL": "0"},
-                                 {"IZPI_REC_DENSE": "50"}])
-def test_kernel_variants_bitwise(gpu, env, monkeypatch):
+@pytest.mark.parametrize("tune", [{"prim_weight": 1},
+                                  {"prim_weight": 100000}, {"slots": 3000, "chunk_units": 5000},
+                                  {"flags": N.TUNE_NO_LEAF_SHORTCUT}, {"trace_chunk": 1, "refill_min": 1},
+                                  {"flags": N.TUNE_NO_DIST},
+                                  {"flags": N.TUNE_NO_TAIL}, {"flags": N.TUNE_NO_TAIL, "slots": 3000},
+                                  {"tail_paths": 100},
+                                  {"flags": N.TUNE_GENERAL_TRACE},
+                                  {"rec_dense": 1, "pool_div": 100000},
+                                  {"rec_dense": 2, "pool_div": 100000, "flags": N.TUNE_NO_TAIL},
+                                  {"rec_dense": 50}])
+def test_kernel_variants_bitwise(gpu, tune):
     """Traversal step weights, tiny slot/chunk counts, the sequential-leaf and
     sphere-capable instances, the pass loop without the k_tail finish, and the unwinding
     records' split (dense levels + overflow blocks: a 4096-block pool far below the demand
     parks slots, all-dense needs no pool) are launch knobs only: results and counters
     must not move."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     scene = configs.cornell_dragon(1.0, n=60)
-    r = GPURenderer(scene, 64, 64, 4)
+    r = GPURenderer(scene, 64, 64, 4, tuning=N.tuning(**tune))
     img = r.render()
     ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
     assert_parity(img, ref, r.stats, ostats)
-    if env.get("IZPI_POOL_DIV") == "100000":
+    if tune.get("pool_div") == 100000:
         assert r.stats["pool_blocks"] == 4096 and r.stats["parks"] > 0, r.stats  # the park path ran
     r.close()
 
 
-@pytest.mark.parametrize("env", [{"IZPI_REC_DENSE": "1", "IZPI_POOL_DIV": "100000"},
-                                 {"IZPI_REC_DENSE": "3", "IZPI_POOL_DIV": "100000", "IZPI_TAIL": "0"}])
-def test_record_pool_spectral_glass_bitwise(gpu, env, monkeypatch):
+@pytest.mark.parametrize("tune", [{"rec_dense": 1, "pool_div": 100000},
+                                  {"rec_dense": 3, "pool_div": 100000, "flags": N.TUNE_NO_TAIL}])
+def test_record_pool_spectral_glass_bitwise(gpu, tune):
     """Overflow records under the spectral sampler with dielectrics: path-length rays,
     parked slots and 32-B records."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     scene = configs.cornell_glass_spectral()
-    r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL)
+    r = GPURenderer(scene, 48, 48, 8, sampler=N.SAMPLER_SPECTRAL, tuning=N.tuning(**tune))
     img = r.render()
     ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_SPECTRAL)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
 
 
-def test_slow_slab_path_bitwise(gpu, monkeypatch):
+def test_slow_slab_path_bitwise(gpu):
     """The NaN-free packed slab (slab4_fast) and the scalar twin give the same image."""
-    monkeypatch.setenv("IZPI_NO_FAST_SLAB", "1")
     scene = configs.cornell_dragon(1.0, n=60)
-    r = GPURenderer(scene, 64, 64, 4)
+    r = GPURenderer(scene, 64, 64, 4, tuning=N.tuning(flags=N.TUNE_SCALAR_SLAB))
     img = r.render()
     ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
     assert_parity(img, ref, r.stats, ostats)
@@ -334,6 +329,30 @@ def test_full_size_c3_tiles_full_spp_bitwise(gpu):
     r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp)
     img = r.render(tiles=tiles)
     ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, cfg.spp, N.SAMPLER_COLOUR, tiles=tiles)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
+
+
+@pytest.mark.parametrize("name,ntiles,tune", [
+    ("C2", 4, None),
+    ("C4", 2, None),
+    # C5 in 5 chunks of per-sample results (the multi-chunk path C5's full frame takes)
+    ("C5", 1, {"chunk_units": 1 << 20}),
+])
+@pytest.mark.timeout(400)
+def test_full_spp_centre_tiles_bitwise(gpu, name, ntiles, tune):
+    """BASELINE.json's configs at their FULL spp (C2 256, C4 1024, C5 4096) on the frame's
+    first tiles in spiral order (the centre, where the dragon / glass is), against the oracle
+    (render/rgb.go:12-57, render/spectral.go:71-106): bit-identical canvases, equal counters."""
+    cfg = configs.configs()[name]
+    scene = cfg.build()
+    tiles = common_tiles(cfg.width, cfg.height)[:ntiles]
+    r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp, sampler=cfg.sampler,
+                    tuning=N.tuning(**tune) if tune else None)
+    img = r.render(tiles=tiles)
+    if tune and "chunk_units" in tune:
+        assert r.stats["chunk_spp"] < cfg.spp, r.stats  # several chunks ran
+    ref, ostats = oracle_canvas(scene, cfg.width, cfg.height, cfg.spp, cfg.sampler, tiles=tiles)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
 
@@ -550,6 +569,69 @@ def test_render_rank_rccl_world1_bitwise(gpu):
     ref, ostats = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
     assert_parity(canvas.cpu().numpy(), ref, r.stats, ostats)
     r.close()
+
+
+def test_render_rank_failures_return_without_hanging(gpu):
+    """izpi_gpu_render_rank's failure paths at world size 1 (every collective still runs:
+    the agreement steps and the gather) return the failing status, then the context renders
+    normally again (render/remote.go:40-55 only logs a failed remote tile; here the caller
+    gets the status)."""
+    import ctypes as C
+    import torch
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 64, 64, 4)
+    L = N.lib()
+    cid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    assert L.izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    canvas = torch.zeros((64, 64, 4), dtype=torch.float64, device="cuda:0")
+    req = r.request()
+    st = N.RenderStats()
+    # rank 0 without an output canvas: fails its local checks, before rendering
+    assert L.izpi_gpu_render_rank(r.ctx, C.byref(req), None, C.byref(st)) == N.IZPI_ERR_INVALID
+    for where, want in ((1, N.IZPI_ERR_DEVICE), (2, N.IZPI_ERR_DEVICE)):
+        assert L.izpi_gpu_debug_fault(r.ctx, where) == 0
+        rc = L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st))
+        assert rc == want, (where, rc, L.izpi_gpu_last_error(r.ctx))
+        assert b"inject" in L.izpi_gpu_last_error(r.ctx)
+    assert L.izpi_gpu_debug_fault(r.ctx, 0) == 0
+    r.render_rank(canvas.data_ptr())
+    torch.cuda.synchronize()
+    ref, _ = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(canvas.cpu().numpy(), ref)
+    r.close()
+
+
+def test_multi_render_device_failure_is_reported(gpu):
+    """izpi_gpu_multi_render with one failing device (a render fault injected on context 1,
+    then a context without a scene): the call returns that device's status and names it,
+    every device thread is joined, and the next frame renders bit-exact."""
+    from izpi_amd.renderer import MultiGPURenderer
+    L = N.lib()
+    scene = configs.cornell_rgb()
+    r = MultiGPURenderer(scene, 64, 64, 4, [0, 0], bvh="reference")
+    ctx1 = L.izpi_gpu_multi_context(r.m, 1)
+    assert L.izpi_gpu_debug_fault(ctx1, 2) == 0
+    with pytest.raises(RuntimeError, match=r"status 5\): device 1: injected"):
+        r.render()
+    assert L.izpi_gpu_debug_fault(ctx1, 0) == 0
+    img = r.render()
+    ref, _ = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(img, ref)
+    r.close()
+    # a device whose scene upload never happened
+    m = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.izpi_gpu_multi_open(devs, 2, C.byref(m)) == 0
+    one = GPURenderer(scene, 64, 64, 4)
+    assert L.izpi_gpu_upload_scene(L.izpi_gpu_multi_context(m, 0), C.byref(one.host.desc)) == 0
+    req = one.request()
+    canvas = np.zeros((64, 64, 4))
+    rc = L.izpi_gpu_multi_render(m, C.byref(req), canvas.ctypes.data_as(C.c_void_p), None)
+    assert rc == N.IZPI_ERR_NO_SCENE, rc
+    assert b"device 1" in L.izpi_gpu_multi_last_error(m)
+    L.izpi_gpu_multi_close(m)
+    one.close()
 
 
 def test_cli_renders_like_the_python_host(gpu, tmp_path):

@@ -134,12 +134,10 @@ def textured_lambert_box():
     return s
 
 
-@pytest.mark.parametrize("env", [{}, {"IZPI_REC_DENSE": "2", "IZPI_POOL_DIV": "100000"}])
-def test_textured_lambert_bitwise(gpu, env, monkeypatch):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("tune", [{}, {"rec_dense": 2, "pool_div": 100000}])
+def test_textured_lambert_bitwise(gpu, tune):
     scene = textured_lambert_box()
-    r = GPURenderer(scene, 48, 48, 8)
+    r = GPURenderer(scene, 48, 48, 8, tuning=N.tuning(**tune) if tune else None)
     img = r.render()
     ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
     assert_parity(img, ref, r.stats, ostats)
