@@ -8,6 +8,7 @@ It is compiled with ``-ffp-contract=off`` and without fast-math so that every
 ``a*b+c`` rounds twice on host and device alike (Go on amd64 emits no FMA).
 """
 import os
+import shutil
 import subprocess
 import sys
 from pathlib import Path
@@ -25,6 +26,13 @@ DEPS = SOURCES + [CSRC / "izpi_dev.h", CSRC / "gomath.h", CSRC / "cie_tables.h",
                   ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h", ROOT / "include" / "izpi_types.h"]
 
 
+def _tmp_name(target):
+    """A per-process name next to `target`: two processes building at once (pytest beside
+    bench.py, ranks of a launcher without torchrun) never write one file; os.replace then
+    swaps the finished file in, so readers never see a partial one."""
+    return target.with_name("%s.tmp%d" % (target.name, os.getpid()))
+
+
 def _stale(target, deps):
     if not target.exists():
         return True
@@ -40,11 +48,13 @@ def build_cli(force=False, verbose=True):
     """izpi-render: the C++ host (izpi_amd/csrc/izpi_render.cpp) linked to the library."""
     if not force and not _stale(CLI, [CLI_SRC, LIB, ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h"]):
         return CLI
-    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-o", str(CLI), str(CLI_SRC), "-L" + str(LIBDIR),
+    tmp = _tmp_name(CLI)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-o", str(tmp), str(CLI_SRC), "-L" + str(LIBDIR),
            "-lizpi_gpu", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    os.replace(tmp, CLI)
     return CLI
 
 
@@ -59,11 +69,13 @@ def build_replay(force=False, verbose=True):
     """go_shim_replay: the Go shim's C call sequence in C (integration/c), for the tests."""
     if not force and not _stale(REPLAY, [REPLAY_SRC, LIB, ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h"]):
         return REPLAY
-    cmd = [os.environ.get("CC", "gcc"), "-O2", "-std=c99", "-Wall", "-I" + str(ROOT / "include"), "-o", str(REPLAY),
+    tmp = _tmp_name(REPLAY)
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-std=c99", "-Wall", "-I" + str(ROOT / "include"), "-o", str(tmp),
            str(REPLAY_SRC), "-L" + str(LIBDIR), "-lizpi_gpu", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    os.replace(tmp, REPLAY)
     return REPLAY
 
 
@@ -73,7 +85,7 @@ def build_gpu(force=False, verbose=True):
         build_replay(force, verbose)
         return LIB
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    objdir = LIBDIR / "obj"
+    objdir = LIBDIR / ("obj.%d" % os.getpid())  # per process: concurrent builds never share an object file
     objdir.mkdir(exist_ok=True)
     # one hipcc per source, in parallel (izpi_gpu.hip dominates), then one link
     from concurrent.futures import ThreadPoolExecutor
@@ -85,9 +97,10 @@ def build_gpu(force=False, verbose=True):
         subprocess.run(cmd, check=True)
     with ThreadPoolExecutor(len(cmds)) as ex:
         list(ex.map(run, cmds))
-    tmp = LIB.with_suffix(".so.tmp%d" % os.getpid())  # os.replace below: readers never see a partial file
+    tmp = _tmp_name(LIB)
     run([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), *LINK])
     os.replace(tmp, LIB)
+    shutil.rmtree(objdir, ignore_errors=True)
     build_cli(True, verbose)
     build_replay(True, verbose)
     return LIB

@@ -67,6 +67,25 @@ struct alignas(16) GLight {
   uint32_t kind, index;
 };
 
+// An image texture's texels in their device storage form (izpi_gpu_upload_scene repacks
+// each IMAGE texture): RGBA = 4 doubles per texel as uploaded, GRAY = 1 double per texel
+// for a texture whose every texel has R, G and B bit-identical (a roughness or metalness
+// map): the lookup returns the same three values from an 8-B read instead of a 32-B one.
+enum { TEXF_RGBA = 0, TEXF_GRAY = 1, TEXF_OTHER = 2, TEXF_NONE = 3 };
+// One texture slot of a material (DevScene::mat_tex), resolved at upload so that a hit
+// reads its material's textures with one dependent load less (material -> texels instead
+// of material -> texture record -> texels): off = first texel (doubles into
+// DevScene::texels), w, hf = height | format << 30. TEXF_OTHER: a non-image texture, off =
+// its index into DevScene::textures; TEXF_NONE: no texture (-1).
+struct alignas(16) TexSlot {
+  uint64_t off;
+  uint32_t w, hf;
+};
+// Slots 0..3: albedo, normal map, roughness, metalness (the PBR set, pbr.go:20-56).
+struct alignas(64) MatTex {
+  TexSlot s[4];
+};
+
 struct DevScene {
   const GInner* inner;
   const GLeaf* leaves;
@@ -83,6 +102,7 @@ struct DevScene {
   const izpi_texture* textures;
   const uint32_t* mat_flags;    // per material: bit0 needs hit-record UVs (image textures)
   const double4* mat_const;     // per material: its constant RGB albedo / emit texture value (GShade cflags bit0)
+  const MatTex* mat_tex;        // per material: its RGB texture slots
   const double* texels;
   const double* spd_wl;
   const double* spd_val;

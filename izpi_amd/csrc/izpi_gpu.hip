@@ -72,25 +72,44 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
        CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
-       CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_PARK, CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
+       CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_PARK, CNT_SCLK_MAT, CNT_SCLK_FIN, CNT_SCLK_MIX, CNT_SCLK_LPDF,
+       CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 
 // ======================================================= textures / spectra
-// texture.Constant / texture.ImageTxt (constant.go:20, image.go:73-101)
+// ImageTxt.Value (image.go:73-101): the nearest texel of a w x h image at (u, v), from
+// its device storage form (TEXF_RGBA or TEXF_GRAY, see TexSlot).
+IZPI_DEV V3 image_rgb(const double* texels, uint64_t off, uint32_t w, uint32_t h, uint32_t fmt, double u, double v) {
+  int64_t i = go_int(u * (double)w);
+  int64_t j = go_int((1 - v) * ((double)h - 0.001));
+  if (i < 0) i = 0;
+  if (j < 0) j = 0;
+  if (i > (int64_t)w - 1) i = (int64_t)w - 1;
+  if (j > (int64_t)h - 1) j = (int64_t)h - 1;
+  const uint64_t k = (uint64_t)j * w + (uint64_t)i;
+  if (fmt == TEXF_GRAY) {
+    const double g = texels[off + k];
+    return mk(g, g, g);
+  }
+  const double* px = texels + off + k * 4;
+  const double2 rg = *reinterpret_cast<const double2*>(px);  // 32-B aligned texel: one 16-B load + one 8-B load
+  return mk(rg.x, rg.y, px[2]);
+}
+// texture.Constant / texture.ImageTxt (constant.go:20, image.go:73-101); the device copy
+// of an IMAGE texture has pad0 = its storage format
 IZPI_DEV V3 tex_rgb(const DevScene& sc, int32_t id, double u, double v) {
   const izpi_texture& t = sc.textures[id];
-  if (t.kind == IZPI_TEX_IMAGE) {
-    int64_t i = go_int(u * (double)t.width);
-    int64_t j = go_int((1 - v) * ((double)t.height - 0.001));
-    if (i < 0) i = 0;
-    if (j < 0) j = 0;
-    if (i > (int64_t)t.width - 1) i = (int64_t)t.width - 1;
-    if (j > (int64_t)t.height - 1) j = (int64_t)t.height - 1;
-    const double* px = sc.texels + t.texel_offset + ((uint64_t)j * t.width + (uint64_t)i) * 4;
-    return mk(px[0], px[1], px[2]);
-  }
+  if (t.kind == IZPI_TEX_IMAGE) return image_rgb(sc.texels, t.texel_offset, t.width, t.height, t.pad0, u, v);
   return mk(t.value[0], t.value[1], t.value[2]);
 }
+// A material's texture slot (MatTex): images straight from their texels, other textures
+// through their record
+IZPI_DEV V3 slot_rgb(const DevScene& sc, const TexSlot& s, double u, double v) {
+  const uint32_t fmt = s.hf >> 30;
+  if (fmt <= TEXF_GRAY) return image_rgb(sc.texels, s.off, s.w, s.hf & 0x3FFFFFFFu, fmt, u, v);
+  return tex_rgb(sc, (int32_t)s.off, u, v);
+}
+IZPI_DEV bool slot_set(const TexSlot& s) { return (s.hf >> 30) != TEXF_NONE; }
 // First interval [wl[i], wl[i+1]] of a NON-DECREASING table that holds w, for
 // n >= 2 and wl[0] <= w <= wl[n-1]: i = (first j >= 1 with wl[j] >= w) - 1, which is the interval
 // the reference's linear scan stops at (spectral.go:151-181, spectral_constant.go:88-106):
@@ -834,6 +853,8 @@ struct HitRec {
   double t, u, v;
   V3 p, n;
   uint32_t mat;
+  bool nraw_ok;  // nraw holds the normal map's texel at (u, v), already read for a PBR triangle
+  V3 nraw;
 };
 // `uvp` is the hit record, whose (u, v): read only for UV-textured triangles and for spheres.
 IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, const GShade& gs, V3 o, V3 d, double time,
@@ -841,10 +862,12 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
   h.mat = gs_mat(gs);
+  h.nraw_ok = false;
   if (IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
     const uint32_t ti = IZPI_PRIM_INDEX(gs.ref);
     V3 n = mk(gs.n[0], gs.n[1], gs.n[2]);
-    if (want_uv) {  // (u,v) are read only by image textures and normal maps
+    h.u = 0; h.v = 0;
+    if (want_uv) {  // (u,v) are read only by image textures
       const double eps = 1e-8;
       double u = uvp->u, v = uvp->v;
       double w = 1.0 - u - v;
@@ -853,17 +876,19 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
       const double* uv = sc.tri_uv + 6 * (size_t)ti;  // u0,v0,u1,v1,u2,v2
       h.u = w * uv[0] + u * uv[2] + v * uv[4];
       h.v = w * uv[1] + u * uv[3] + v * uv[5];
-      const izpi_material& m = sc.materials[h.mat];
-      if (m.kind == IZPI_MAT_PBR && m.normal_tex >= 0) {  // Material.NormalMap() != nil
-        V3 nts = tex_rgb(sc, m.normal_tex, h.u, h.v);
+    }
+    if (gs_kind(gs) == IZPI_MAT_PBR) {
+      const TexSlot ns = sc.mat_tex[h.mat].s[1];
+      if (slot_set(ns)) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
+        V3 nts = slot_rgb(sc, ns, h.u, h.v);
+        h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
+        h.nraw_ok = true;
         nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
         V3 tg = ld3(sc.tri_tangent + 3 * (size_t)ti), bt = ld3(sc.tri_bitangent + 3 * (size_t)ti);
         V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
                    tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
         n = sdiv(nn, length(nn));
       }
-    } else {
-      h.u = 0; h.v = 0;
     }
     h.n = n;
   } else {
@@ -1396,6 +1421,36 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
 }
 
 
+#ifdef IZPI_SHADE_CLOCKS
+// Timing builds only: wave cycles per section of shade_item, accumulated in LDS by the
+// first active lane of the wave that runs the section (so divergent sections count the
+// wave's time once), added to the CNT_SCLK_* counters at the end of the kernel.
+enum { SCLK_MAT = 0, SCLK_FIN, SCLK_MIX, SCLK_LPDF, SCLK_N };
+IZPI_DEV unsigned long long* sclk_lds() {
+  __shared__ unsigned long long c[4][SCLK_N];
+  return &c[(threadIdx.x >> 6) & 3][0];
+}
+IZPI_DEV void sclk_add(int sec, uint64_t dt) {
+  const uint64_t act = __ballot(1);
+  if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)act) - 1)) sclk_lds()[sec] += dt;
+}
+IZPI_DEV void sclk_flush(unsigned long long* counters) {
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < SCLK_N; k++) atomicAdd(counters + CNT_SCLK_MAT + k, sclk_lds()[k]);
+}
+IZPI_DEV void sclk_zero() {
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < SCLK_N; k++) sclk_lds()[k] = 0;
+  __syncthreads();
+}
+#define SCLK_T(v) const uint64_t v = __builtin_readcyclecounter()
+#define SCLK_ADD(sec, t0) sclk_add(sec, __builtin_readcyclecounter() - (t0))
+#else
+#define SCLK_T(v) (void)0
+#define SCLK_ADD(sec, t0) (void)0
+#endif
+
 // One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
 // one bounce deep (colour.go:33-65, sampler/spectral.go:47-80). Sets `push` when the path
 // has a ray to trace next and `done` when its sample finished.
@@ -1407,6 +1462,7 @@ template <int SAMPLER, int MATSET>
 IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
                          PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt, uint32_t& c_ls) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
+  SCLK_T(sc0);
   {
     const RayOD rh = in.ray[i];
     for (int k = 0; k < 3; k++) { R.o[k] = rh.o[k]; R.d[k] = rh.d[k]; }
@@ -1526,13 +1582,19 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       }
       case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
         if constexpr (!ms_has(MATSET, MS_PBR)) { atomicOr(sp.error, 2u); terminal = true; break; }
+        // the four texture slots in one 64-B record; every lookup below is issued before
+        // the first of them is used
+        const MatTex& mt = sc.mat_tex[h.mat];
+        const TexSlot s_alb = mt.s[0], s_nrm = mt.s[1], s_rgh = mt.s[2], s_met = mt.s[3];
         double alb_s = 0;
-        if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+        if (COLOUR) att = slot_rgb(sc, s_alb, h.u, h.v);
         else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
-        else { V3 c = tex_rgb(sc, m.albedo_tex, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
+        else { V3 c = slot_rgb(sc, s_alb, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
+        V3 rough = slot_set(s_rgh) ? slot_rgb(sc, s_rgh, h.u, h.v) : mk(0.5, 0.5, 0.5);
+        V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v) : mk(0.0, 0.0, 0.0);
         V3 normal = h.n;
-        if (m.normal_tex >= 0) {
-          V3 nuv = tex_rgb(sc, m.normal_tex, h.u, h.v);
+        if (slot_set(s_nrm)) {
+          V3 nuv = h.nraw_ok ? h.nraw : slot_rgb(sc, s_nrm, h.u, h.v);
           V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
           V3 nn0 = h.n;
           V3 t = cross(nn0, mk(0, 1, 0));
@@ -1544,12 +1606,10 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
                      t.z * tn.x + b.z * tn.y + nn0.z * tn.z);
           normal = sdiv(nn, length(nn));
         }
-        V3 rough = m.roughness_tex >= 0 ? tex_rgb(sc, m.roughness_tex, h.u, h.v) : mk(0.5, 0.5, 0.5);
-        V3 metal = m.metalness_tex >= 0 ? tex_rgb(sc, m.metalness_tex, h.u, h.v) : mk(0.0, 0.0, 0.0);
         double rv = (rough.x + rough.y + rough.z) / 3.0;
         double mv = (metal.x + metal.y + metal.z) / 3.0;
-        Onb uvw;
-        uvw.build(normal);
+        cos_onb.build(normal);  // the scatter's ONB and the sampler's Cosine(normal) pdf: one build (onb.go:38-67)
+        const Onb& uvw = cos_onb;
         V3 reflected = reflect(unit(rd), normal);
         double cosTheta = gm::abs(dot(unit(rd), normal));
         double fresnel = 0.04 + (1.0 - 0.04) * gm::pow(1.0 - cosTheta, 5.0);
@@ -1565,7 +1625,6 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
           spec = false;
           have_pdf = true;  // the sampler ignores this ray and samples the mixture pdf
         }
-        cos_onb.build(normal);
         if (!COLOUR) att.x = spec ? alb_s * 1.5 : alb_s;
         break;
       }
@@ -1575,12 +1634,16 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       }
     }
   }
+  SCLK_ADD(SCLK_MAT, sc0);
   if (!push) {
     if (terminal) {
+      SCLK_T(sc1);
       finish<SAMPLER, MATSET>(sp, P, L);
+      SCLK_ADD(SCLK_FIN, sc1);
       done = true;
       fblk = P.blk;
     } else {
+      SCLK_T(sc2);
       if (have_pdf) {
         // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:48-51, mixture.go:17-33)
         V3 dir;
@@ -1595,12 +1658,15 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         if (sc_cos < 0) sc_cos = 0;
         const double spdf = zero_spdf ? 0.0 : sc_cos / 3.141592653589793;  // Isotropic.ScatteringPDF is 0
         rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, spdf, rec_mat);
+        SCLK_T(sc3);
         const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
+        SCLK_ADD(SCLK_LPDF, sc3);
         rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
         next_d = dir;
       } else {
         rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, true, att, 0, rec_mat);
       }
+      SCLK_ADD(SCLK_MIX, sc2);
       P.depth++;
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
@@ -1689,6 +1755,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   const uint32_t stride = gridDim.x * 256;
 #ifdef IZPI_SHADE_CLOCKS
   uint64_t k_item = 0, k_ref = 0, k_push = 0;
+  sclk_zero();
 #endif
   // Block-uniform trip count: the unit and queue reservations are block-wide.
   for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
@@ -1747,6 +1814,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     atomicAdd(sp.counters + CNT_SCLK_REFILL, (unsigned long long)k_ref);
     atomicAdd(sp.counters + CNT_SCLK_PUSH, (unsigned long long)k_push);
   }
+  sclk_flush(sp.counters);
 #endif
   if (c_park && wp.out_park) *wp.out_park = 1u;  // the next k_trace2 must read kind words
   unsigned long long vals[3] = {c_lt, c_ls, c_park};
@@ -2641,8 +2709,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.alloc_ms = alloc_ms;
   if (rec_pool && s.parks * 64 > s.rays && pool_blocks < slots) ctx->pool_grow++;
 #ifdef IZPI_SHADE_CLOCKS
-  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu (wave cycles)\n", cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL],
-          cnt[CNT_SCLK_PUSH]);
+  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu mat %llu finish %llu mix %llu lpdf %llu (wave cycles)\n",
+          cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL], cnt[CNT_SCLK_PUSH], cnt[CNT_SCLK_MAT], cnt[CNT_SCLK_FIN],
+          cnt[CNT_SCLK_MIX], cnt[CNT_SCLK_LPDF]);
 #endif
 #ifdef IZPI_TRACE_CLOCKS
   fprintf(stderr, "IZPI_TRACE_CLOCKS refill %llu node %llu prim %llu advance %llu (wave cycles)\n", cnt[CNT_CLK_REFILL],
@@ -3022,13 +3091,55 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       if (!(std::fabs((wl[i] - wl[0]) * scale - (double)i) <= 0.5)) uniform = false;
     if (uniform) { t.pad0 = 2; t.value[0] = wl[0]; t.value[1] = scale; }
   }
+  // texels in their device storage form (TexSlot): every image texture gets its own run,
+  // RGBA runs 32-B aligned; a texture whose R, G and B are bit-identical in every texel is
+  // stored as one double per texel
+  std::vector<double> texels;
+  std::vector<uint32_t> tex_fmt(d->num_textures, TEXF_OTHER);
+  for (uint32_t i = 0; i < d->num_textures; i++) {
+    izpi_texture& t = texs[i];
+    if (t.kind != IZPI_TEX_IMAGE && t.kind != IZPI_TEX_SPECTRAL_IMAGE) continue;
+    const double* src = d->texels + t.texel_offset;
+    const uint64_t np = (uint64_t)t.width * t.height;
+    bool gray = t.kind == IZPI_TEX_IMAGE;
+    for (uint64_t k = 0; k < np && gray; k++)
+      gray = memcmp(src + 4 * k, src + 4 * k + 1, 8) == 0 && memcmp(src + 4 * k, src + 4 * k + 2, 8) == 0;
+    texels.resize((texels.size() + 3) & ~(size_t)3);
+    t.texel_offset = texels.size();
+    if (gray) {
+      for (uint64_t k = 0; k < np; k++) texels.push_back(src[4 * k]);
+    } else {
+      texels.insert(texels.end(), src, src + 4 * np);
+    }
+    if (t.kind == IZPI_TEX_IMAGE) t.pad0 = tex_fmt[i] = gray ? TEXF_GRAY : TEXF_RGBA;
+  }
+  // the materials' texture slots (albedo, normal, roughness, metalness)
+  std::vector<MatTex> mtex(std::max<uint32_t>(1, d->num_materials));
+  for (uint32_t i = 0; i < d->num_materials; i++) {
+    const izpi_material& m = d->materials[i];
+    const int32_t ids[4] = {m.albedo_tex, m.normal_tex, m.roughness_tex, m.metalness_tex};
+    for (int k = 0; k < 4; k++) {
+      TexSlot& sl = mtex[i].s[k];
+      const int32_t id = ids[k];
+      if (id < 0) { sl.off = 0; sl.w = 0; sl.hf = (uint32_t)TEXF_NONE << 30; continue; }
+      const izpi_texture& t = texs[id];
+      if (tex_fmt[id] <= TEXF_GRAY && t.height < (1u << 30)) {
+        sl.off = t.texel_offset; sl.w = t.width; sl.hf = t.height | tex_fmt[id] << 30;
+      } else {
+        sl.off = (uint64_t)id; sl.w = 0; sl.hf = (uint32_t)TEXF_OTHER << 30;
+      }
+    }
+  }
+  MatTex* dmt;
+  UP(mtex.data(), mtex.size(), &dmt);
   UP(texs.data(), d->num_textures, &dtx);
-  UP(d->texels, d->num_texels, &dtex);
+  if (texels.empty()) texels.push_back(0.0);
+  UP(texels.data(), texels.size(), &dtex);
   UP(d->spd_wavelengths, d->num_spd, &dswl);
   UP(d->spd_values, d->num_spd, &dsv);
   sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tri_normal = dn; sc.tri_uv = duv; sc.tri_tangent = dtg;
   sc.tri_bitangent = dbt; sc.tri_mat = dtm; sc.sph_mat = dsm; sc.lights = dlt; sc.materials = dm;
-  sc.mat_flags = dmf; sc.mat_const = dmc; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
+  sc.mat_flags = dmf; sc.mat_const = dmc; sc.mat_tex = dmt; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
   sc.tri_only = d->num_spheres == 0 ? 1u : 0u;
@@ -3222,17 +3333,17 @@ int izpi_gpu_ray_aabb4(izpi_ctx* ctx, const float* boxes, const float* rays, uin
   if (!ctx || !boxes || !rays || !masks) return IZPI_ERR_INVALID;
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
+  DevBufs tmp;  // freed on every return
   float *db, *dr; uint8_t* dm;
-  HIP_TRY(hipMalloc((void**)&db, (size_t)n * 24 * sizeof(float)));
-  HIP_TRY(hipMalloc((void**)&dr, (size_t)n * 7 * sizeof(float)));
-  HIP_TRY(hipMalloc((void**)&dm, n));
+  HIP_TRY(tmp.alloc(&db, (size_t)n * 24));
+  HIP_TRY(tmp.alloc(&dr, (size_t)n * 7));
+  HIP_TRY(tmp.alloc(&dm, n));
   HIP_TRY(hipMemcpy(db, boxes, (size_t)n * 24 * sizeof(float), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 7 * sizeof(float), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_aabb4, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, db, dr, n, dm);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(masks, dm, n, hipMemcpyDeviceToHost));
-  (void)hipFree(db); (void)hipFree(dr); (void)hipFree(dm);
   return IZPI_OK;
 }
 
@@ -3246,20 +3357,19 @@ int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uin
       if (!(y[i] >= 0 && y[i] < (double)ctx->num_textures)) { ctx->err = "texture number out of range"; return IZPI_ERR_INVALID; }
   }
   HIP_TRY(hipSetDevice(ctx->device));
+  DevBufs tmp;  // freed on every return
   double *dx, *dy = nullptr, *dout;
-  HIP_TRY(hipMalloc((void**)&dx, (size_t)n * sizeof(double)));
-  HIP_TRY(hipMalloc((void**)&dout, (size_t)n * sizeof(double)));
+  HIP_TRY(tmp.alloc(&dx, n));
+  HIP_TRY(tmp.alloc(&dout, n));
   HIP_TRY(hipMemcpy(dx, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
   if (y) {
-    HIP_TRY(hipMalloc((void**)&dy, (size_t)n * sizeof(double)));
+    HIP_TRY(tmp.alloc(&dy, n));
     HIP_TRY(hipMemcpy(dy, y, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
   }
   hipLaunchKernelGGL(k_gomath, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, op, dx, dy, n, dout);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dout, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
-  (void)hipFree(dx); (void)hipFree(dout);
-  if (dy) (void)hipFree(dy);
   return IZPI_OK;
 }
 

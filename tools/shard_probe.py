@@ -1,9 +1,10 @@
 """Per-rank render time of a W-way tile shard on ONE GPU (strong-scaling probe).
 
 python tools/shard_probe.py --config C3 --worlds 1,2,4,8
-For each W, renders rank 0's and rank W-1's tiles (packed layout, device memory) and
-prints ms, passes and the implied efficiency T(1) / (W * max rank time), i.e. the
-scaling the multi-GPU bench would see without the gather."""
+For each W, renders every rank's tiles (packed layout, device memory) and prints ms,
+passes and the implied efficiency T(1) / (W * max rank time), i.e. the scaling the
+multi-GPU bench would see without the gather, split into the share imbalance
+(max / mean rank time) and the per-share overhead (W * mean / T(1))."""
 import argparse
 import sys
 import time
@@ -29,8 +30,8 @@ def main():
     all_tiles = common_tiles(cfg.width, cfg.height)
     t1 = None
     for w in [int(x) for x in a.worlds.split(",")]:
-        worst = 0.0
-        for rank in sorted({0, w - 1}):
+        worst, times = 0.0, []
+        for rank in range(w):
             mine = sharding.shard_tiles(all_tiles, rank, w)
             buf = torch.zeros(sharding.packed_len(all_tiles, w), dtype=torch.float64, device="cuda")
             r.render_device(buf.data_ptr(), tiles=mine, layout=N.OUT_PACKED)  # warm
@@ -40,11 +41,14 @@ def main():
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t) * 1e3
             worst = max(worst, ms)
+            times.append(ms)
             print("W=%d rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f tail %.1f, %d passes)" %
                   (w, rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["tail_ms"], st["launches"]), flush=True)
         if t1 is None:
             t1 = worst
-        print("W=%d implied efficiency %.3f" % (w, t1 / (w * worst)), flush=True)
+        mean = sum(times) / len(times)
+        print("W=%d implied efficiency %.3f (imbalance max/mean %.3f, overhead W*mean/T1 %.3f)" %
+              (w, t1 / (w * worst), worst / mean, w * mean / t1), flush=True)
 
 
 if __name__ == "__main__":
