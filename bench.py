@@ -332,6 +332,10 @@ def main():
     post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
     if mode != "threads":
         torch.cuda.set_device(local)
+    # torch's own HIP context starts lazily with its first tensor: start it here, so that
+    # detail.first_frame_ms is the renderer's first frame (what leader.go:155-158 sees)
+    for d in ([local] if mode != "threads" else range(n_gpus)):
+        torch.zeros(1, device="cuda:%d" % d)
 
     def sync_all():
         if mode == "threads":

@@ -89,6 +89,19 @@ uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint3
 uint32_t izpi_host_share_tiles(const uint32_t* tiles, uint32_t num_tiles, uint32_t share, uint32_t num_shares,
                                uint32_t* out);
 
+/* Doubles per padded share block of a packed multi-GPU gather: ceil(num_tiles /
+ * num_shares) * tile_w * tile_h * 4 (every share's block has this size). */
+uint64_t izpi_host_share_block(uint32_t num_tiles, uint32_t tile_w, uint32_t tile_h, uint32_t num_shares);
+
+/* What the root of izpi_gpu_multi_render / izpi_gpu_render_rank does after the gather,
+ * on the host: block r of `gathered` (izpi_host_share_block doubles each) holds share r's
+ * tiles packed (IZPI_OUT_PACKED); every pixel is scattered to canvas row height - y
+ * (render/rgb.go:41; sample row y = 0 has no canvas row). The same index rule as the
+ * device's k_unpack. Replaces the framebuffer assembly of renderer.go:172-211 (workers
+ * write their tiles into the shared canvas). Tiles must be equal-sized and in bounds. */
+int izpi_host_assemble_shares(uint32_t width, uint32_t height, const uint32_t* tiles, uint32_t num_tiles,
+                              uint32_t num_shares, const double* gathered, double* canvas);
+
 /* The Go-math routines of izpi_amd/csrc/gomath.h evaluated on the host (same op
  * codes as izpi_gpu_gomath); used by the parity tests. */
 double izpi_host_gomath(int op, double x, double y);

@@ -1026,8 +1026,9 @@ struct ShadeParams {
 };
 
 // Unwinding records, one per bounce, laid out [slot][depth] so that a finishing path
-// reads its records as one contiguous run (48 B per level for Colour: flag, att xyz, s, p;
-// 32 B for Spectral: flag, att, s, p). A [depth][field][slot] layout made every field
+// reads its records as one contiguous run (40 B per level for Colour: att xyz, s, p;
+// 24 B for Spectral: att, s, p; a specular level marks s, see REC_SPEC_BITS). A
+// [depth][field][slot] layout made every field
 // of every level a separate scattered 64-B sector read (measured: 44% of C5 shading).
 // Only the first rec_dense levels are stored per slot. Few paths go deeper (C3: ~3% of
 // the paths in flight at depth >= 8), so the deeper levels live in overflow blocks of
@@ -1038,7 +1039,7 @@ struct ShadeParams {
 // footprint small; MATSET_CONST is MATSET_BASIC for scenes whose albedos are all
 // constant RGB textures (Colour sampler): a bounce's attenuation is then its material's
 // constant, so its unwinding record holds the material instead of the colour (24 B
-// instead of 48 B); MATSET_SURF adds Metal and PBR, MATSET_FULL Dielectric and Isotropic
+// instead of 40 B); MATSET_SURF adds Metal and PBR, MATSET_FULL Dielectric and Isotropic
 // too. The host picks the variant from the scene's materials (results are identical).
 // A MATSET is a set of feature bits: only the material branches it holds are compiled in.
 // The host runs the smallest instance holding the scene's material kinds: MATSET_SURF for
@@ -1060,9 +1061,14 @@ constexpr bool ms_spec(int matset) { return (matset & (MS_DIEL | MS_METAL | MS_P
 template <int SAMPLER, int MATSET>
 struct RecLayout {
   static constexpr bool COMPACT = SAMPLER == IZPI_SAMPLER_COLOUR && MATSET == MATSET_CONST;
-  static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 4);  // doubles per record
+  static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 5 : 3);  // doubles per record
   static constexpr uint32_t P = D - 1;                                                   // index of p
+  static constexpr uint32_t S = D - 2;                                                   // index of s
 };
+// Records are (att, s, p): att xyz for Colour, att for Spectral. A specular bounce has no
+// s or p and stores s = REC_SPEC_BITS, a signalling-NaN pattern: ScatteringPDF's
+// arithmetic only ever makes quiet NaNs, so no non-specular record carries it.
+constexpr uint64_t REC_SPEC_BITS = 0x7FF4C0DEC0DEC0DEull;
 template <int SAMPLER, int MATSET>
 IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth) {
   constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
@@ -1079,15 +1085,11 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
     rp[1] = s;
     return;
   }
-  double2* r = reinterpret_cast<double2*>(rp);
-  r[0] = make_double2(spec ? 1.0 : 0.0, att.x);
-  if (SAMPLER == IZPI_SAMPLER_COLOUR) {
-    r[1] = make_double2(att.y, att.z);
-    if (!spec) rp[4] = s;
-  } else {
-    if (!spec) rp[2] = s;
-  }
+  rp[0] = att.x;
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) { rp[1] = att.y; rp[2] = att.z; }
+  rp[RecLayout<SAMPLER, MATSET>::S] = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
 }
+IZPI_DEV bool rec_is_spec(double s) { return (uint64_t)__double_as_longlong(s) == REC_SPEC_BITS; }
 
 // Result slot of work unit `unit` (= pixel * chunk_spp + sample). Unit-major: paths of
 // neighbouring units finish close in time and fill whole lines (a sample-major layout
@@ -1110,7 +1112,10 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   // The records are read four levels at a time (one batch of independent loads, then
   // the levels applied in order), so a path of depth d waits ~d/4 memory round trips.
   constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
-  constexpr int RB = 4;
+#ifndef IZPI_FIN_RB
+#define IZPI_FIN_RB 4
+#endif
+  constexpr int RB = IZPI_FIN_RB;
   for (int dd = (int)P.depth - 1; dd >= 0; dd -= RB) {
     double rv[RB][D];
     if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {
@@ -1144,33 +1149,38 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
 #pragma unroll
     for (int j = 0; j < RB; j++) {
       if (dd - j >= 0) {
-        const double2* r2 = reinterpret_cast<const double2*>(rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j)));
+        const double* rp = rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j));
+        if constexpr (D % 2 == 0) {
+          const double2* r2 = reinterpret_cast<const double2*>(rp);
 #pragma unroll
-        for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
+          for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
+        } else {
+#pragma unroll
+          for (uint32_t q = 0; q < D; q++) rv[j][q] = rp[q];
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < RB; j++) {
       if (dd - j < 0) break;
       const double* r = rv[j];
-      const bool spec = r[0] != 0.0;
       if (SAMPLER == IZPI_SAMPLER_COLOUR) {
-        V3 att = mk(r[1], r[2], r[3]);
-        if (spec) {
+        V3 att = mk(r[0], r[1], r[2]);
+        if (rec_is_spec(r[3])) {
           L = mul(att, L);                                   // vec3.Mul(att, Sample(...))
         } else {
-          const double s = r[4], p = r[5];
+          const double s = r[3], p = r[4];
           V3 v1 = smul(L, s);                                // ScalarMul(Sample(...), ScatteringPDF)
           V3 v2 = mul(att, v1);
           V3 v3 = sdiv(v2, p);
           L = mk(0.0 + v3.x, 0.0 + v3.y, 0.0 + v3.z);        // Add(emitted == 0, v3)
         }
       } else {
-        const double att = r[1];
-        if (spec) {
+        const double att = r[0];
+        if (rec_is_spec(r[1])) {
           L.x = att * L.x;
         } else {
-          const double s = r[2], p = r[3];
+          const double s = r[1], p = r[2];
           double v1 = L.x * s;
           double v2 = att * v1;
           double v3 = v2 / p;
@@ -2030,16 +2040,23 @@ __global__ void __launch_bounds__(256) k_postprocess(double* canvas, uint64_t nu
   p[1] = make_double2(c[2], ba.y);
 }
 
+// Packed pixel p (IZPI_OUT_PACKED: tile after tile, the rows of each tile) -> its canvas
+// column x and row H - y (rgb.go:41); false for sample row y = 0, which has no canvas row.
+// k_unpack and izpi_host_assemble_shares share this rule.
+__host__ __device__ inline bool packed_target(const uint32_t* tiles, uint32_t p, uint32_t tile_w, uint32_t tile_h,
+                                              uint32_t height, uint32_t* x, uint32_t* row) {
+  const uint32_t tile_px = tile_w * tile_h;
+  const uint32_t tile = p / tile_px, in_tile = p % tile_px;
+  *x = tiles[4 * tile] + in_tile % tile_w;
+  *row = height - (tiles[4 * tile + 1] + in_tile / tile_w);
+  return *row < height;
+}
 __global__ void k_unpack(const uint32_t* tiles, uint32_t num_pixels, uint32_t tile_w, uint32_t tile_h, uint32_t width,
                          uint32_t height, const double* packed, double* canvas) {
   const uint32_t p = blockIdx.x * 256 + threadIdx.x;
   if (p >= num_pixels) return;
-  const uint32_t tile_px = tile_w * tile_h;
-  const uint32_t tile = p / tile_px, in_tile = p % tile_px;
-  const uint32_t x = tiles[4 * tile] + in_tile % tile_w;
-  const uint32_t y = tiles[4 * tile + 1] + in_tile / tile_w;
-  const uint32_t row = height - y;
-  if (row < height) {
+  uint32_t x, row;
+  if (packed_target(tiles, p, tile_w, tile_h, height, &x, &row)) {
     const double* s = packed + (size_t)p * 4;
     double* o = canvas + ((size_t)row * width + x) * 4;
     o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
@@ -2561,7 +2578,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (tu.chunk_units) max_units = tu.chunk_units;
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
-  // blocks (ShadeParams::rec_pool). Colour records are 48 B (24 B compact), spectral 32 B.
+  // blocks (ShadeParams::rec_pool). Colour records are 40 B (24 B compact), spectral 24 B.
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
   const bool compact = !spectral && ctx->basic_materials && ctx->const_albedo;
   const uint32_t D = spectral  ? RecLayout<IZPI_SAMPLER_SPECTRAL, MATSET_FULL>::D
@@ -2742,6 +2759,8 @@ struct Shares {
   }
 };
 
+size_t share_block(size_t ntiles, uint32_t tw, uint32_t th, uint32_t n) { return ((ntiles + n - 1) / n) * (size_t)tw * th * 4; }
+
 int make_shares(izpi_ctx* ctx, const izpi_render_req* req, uint32_t n, Shares& sh) {
   if (!req || req->width == 0 || req->height == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
   if (req->out_layout != IZPI_OUT_CANVAS) { ctx->err = "multi-GPU renders produce a canvas (IZPI_OUT_CANVAS)"; return IZPI_ERR_INVALID; }
@@ -2754,7 +2773,7 @@ int make_shares(izpi_ctx* ctx, const izpi_render_req* req, uint32_t n, Shares& s
   }
   sh.n = n;
   const size_t ntiles = sh.all.size() / 4;
-  sh.block = ((ntiles + n - 1) / n) * (size_t)tw * th * 4;
+  sh.block = share_block(ntiles, tw, th, n);
   return IZPI_OK;
 }
 
@@ -3596,6 +3615,31 @@ int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_
   if (worst) return peer_failure(ctx, worst, wr, "while rendering its share");
   // ---- 3
   if (ctx->comm_rank == 0 && (rc = assemble(ctx, req, sh, out_dev))) return rc;
+  return IZPI_OK;
+}
+
+uint64_t izpi_host_share_block(uint32_t num_tiles, uint32_t tile_w, uint32_t tile_h, uint32_t num_shares) {
+  return num_shares ? share_block(num_tiles, tile_w, tile_h, num_shares) : 0;
+}
+
+int izpi_host_assemble_shares(uint32_t width, uint32_t height, const uint32_t* tiles, uint32_t num_tiles,
+                              uint32_t num_shares, const double* gathered, double* canvas) {
+  if (!tiles || !gathered || !canvas || num_tiles == 0 || num_shares == 0 || width == 0 || height == 0) return IZPI_ERR_INVALID;
+  izpi_render_req req{};
+  req.width = width; req.height = height;
+  uint32_t tw = 0, th = 0;
+  if (!validate_tiles(&req, tiles, num_tiles, &tw, &th)) return IZPI_ERR_INVALID;
+  const size_t block = share_block(num_tiles, tw, th, num_shares);
+  std::vector<uint32_t> mine(4 * (size_t)num_tiles);
+  for (uint32_t r = 0; r < num_shares; r++) {
+    const uint32_t nt = izpi_host_share_tiles(tiles, num_tiles, r, num_shares, mine.data());
+    const double* packed = gathered + (size_t)r * block;
+    for (uint32_t p = 0; p < nt * tw * th; p++) {
+      uint32_t x, row;
+      if (packed_target(mine.data(), p, tw, th, height, &x, &row))
+        memcpy(canvas + ((size_t)row * width + x) * 4, packed + (size_t)p * 4, 4 * sizeof(double));
+    }
+  }
   return IZPI_OK;
 }
 

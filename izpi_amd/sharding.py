@@ -8,8 +8,8 @@ the partition, so the gathered canvas is bit-identical for any world size.
 Each rank packs its tiles contiguously (IZPI_OUT_PACKED: tile after tile, rows of
 sample y, 4 doubles per pixel). One collective moves them to rank 0: ``dist.gather``
 of equal-sized (padded) packed buffers — over RCCL/xGMI with the "nccl" backend, or
-gloo in the CPU tests. Rank 0 scatters them into the canvas (izpi_gpu_unpack_tiles on
-the GPU; :func:`unpack_into` is the same rule on the host).
+gloo in the CPU tests. Rank 0 scatters them into the canvas (k_unpack on the GPU;
+:func:`assemble` = izpi_host_assemble_shares, the library's host twin of it).
 """
 import numpy as np
 
@@ -33,11 +33,30 @@ def tile_pixels(tiles):
 
 
 def packed_len(all_tiles, world):
-    """Doubles per rank's (padded) packed buffer: max tiles per rank * tile pixels * 4."""
+    """Doubles per rank's (padded) packed buffer: the library's share block
+    (izpi_host_share_block: max tiles per rank * tile pixels * 4)."""
+    from . import _native as N
     t = np.asarray(all_tiles, np.int64)
-    per_tile = int((t[0, 2] - t[0, 0] + 1) * (t[0, 3] - t[0, 1] + 1))
-    max_tiles = (len(t) + world - 1) // world
-    return max_tiles * per_tile * 4
+    return int(N.lib().izpi_host_share_block(len(t), int(t[0, 2] - t[0, 0] + 1), int(t[0, 3] - t[0, 1] + 1), world))
+
+
+def assemble(all_tiles, world, gathered, width, height, canvas=None):
+    """Rank 0's assembly of the gathered share blocks (`world` blocks of packed_len
+    doubles, in rank order) into the canvas: the library's izpi_host_assemble_shares, the
+    host twin of what izpi_gpu_render_rank's root runs on the device (k_unpack)."""
+    from . import _native as N
+    t = np.ascontiguousarray(np.asarray(all_tiles, np.uint32).reshape(-1, 4))
+    g = np.ascontiguousarray(np.asarray(gathered, np.float64).reshape(-1))
+    if g.size != world * packed_len(t, world):
+        raise ValueError("gathered holds %d doubles, expected %d blocks of %d" % (g.size, world, packed_len(t, world)))
+    if canvas is None:
+        canvas = np.zeros((height, width, 4), np.float64)
+    assert canvas.flags.c_contiguous and canvas.dtype == np.float64 and canvas.size == width * height * 4
+    rc = N.lib().izpi_host_assemble_shares(width, height, t.ctypes.data_as(N.c_uint32_p), len(t), world,
+                                           g.ctypes.data_as(N.c_double_p), canvas.ctypes.data_as(N.c_double_p))
+    if rc != 0:
+        raise RuntimeError("izpi_host_assemble_shares: status %d" % rc)
+    return canvas
 
 
 def gather_packed(packed, rank, world, group=None):
@@ -51,7 +70,8 @@ def gather_packed(packed, rank, world, group=None):
 
 
 def unpack_into(canvas, tiles, packed, width, height):
-    """Host twin of k_unpack: packed tile pixels -> canvas rows H - y (rgb.go:41)."""
+    """A Python restatement of k_unpack (packed tile pixels -> canvas rows H - y,
+    rgb.go:41), kept as the independent check of izpi_host_assemble_shares."""
     p = 0
     flat = np.asarray(packed).reshape(-1, 4)
     for x0, y0, x1, y1 in np.asarray(tiles, np.int64):

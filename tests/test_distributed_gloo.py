@@ -1,8 +1,10 @@
-"""Multi-rank path on CPU (gloo, world_size 2 and 3): the product's tile sharding and
-packed-buffer gather (izpi_amd/sharding.py, the same code the RCCL path runs), fed by
-oracle renders of each rank's tiles. The gathered canvas must be bit-identical to a
-single-rank render: per pixel-sample RNG streams make the image partition-independent
-(SURVEY.md §8(e))."""
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): the library's own share rule
+(izpi_host_share_tiles), padded block size (izpi_host_share_block) and root assembly
+(izpi_host_assemble_shares, the host twin of the device's k_unpack step in
+izpi_gpu_render_rank), with the blocks moved by a gloo gather and fed by oracle renders of
+each rank's tiles. The assembled canvas must be bit-identical to a single-rank render:
+per pixel-sample RNG streams make the image partition-independent; a
+Python restatement of the unpack rule cross-checks the library's."""
 import os
 import socket
 
@@ -52,11 +54,14 @@ def _worker(rank, world, port, outdir):
         packed[:part.size] = part
     got = sharding.gather_packed(torch.from_numpy(packed), rank, world)
     if rank == 0:
-        canvas = np.zeros((H, W, 4))
+        blocks = np.concatenate([g.numpy() for g in got])
+        canvas = sharding.assemble(all_tiles, world, blocks, W, H)
+        check = np.zeros((H, W, 4))
         for r in range(world):
             rt = sharding.shard_tiles(all_tiles, r, world)
             if len(rt):
-                sharding.unpack_into(canvas, rt, got[r].numpy()[:sharding.tile_pixels(rt) * 4], W, H)
+                sharding.unpack_into(check, rt, got[r].numpy()[:sharding.tile_pixels(rt) * 4], W, H)
+        assert canvas.tobytes() == check.tobytes()
         np.save(os.path.join(outdir, "canvas_%d.npy" % world), canvas)
     dist.barrier()
     dist.destroy_process_group()

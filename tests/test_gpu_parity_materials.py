@@ -175,3 +175,44 @@ def test_isotropic_bitwise(gpu, sampler):
     ref, ostats = oracle_canvas(scene, 48, 48, 8, sampler)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
+
+
+def pbr_storage_box():
+    """PBR textures in every device storage form: an RGBA image albedo, a gray image
+    roughness (R = G = B in every texel: one double per texel on the device), a metalness
+    image that is gray except in one texel (kept RGBA), and CONSTANT normal maps, which
+    Triangle.Hit's TBN (triangle.go:250-264) and PBR.Scatter (pbr.go:65-91) apply like image
+    ones; a Lambert wall keeps an image albedo next to them."""
+    s = Scene("pbr_storage")
+    res = 40
+    y, x = np.mgrid[0:res, 0:res] / float(res)
+    alb = np.stack([0.2 + 0.6 * x, 0.3 + 0.5 * y, 0.4 + 0.2 * x * y, np.ones_like(x)], -1)
+    g = 0.1 + 0.8 * ((np.floor(x * 5) + np.floor(y * 5)) % 2)
+    rough = np.stack([g, g, g, np.ones_like(x)], -1)
+    m = 0.6 * x
+    metal = np.stack([m, m, m, np.ones_like(x)], -1)
+    metal[7, 11, 2] += 0.25  # one texel with B != R: the whole texture stays RGBA
+    a_id, r_id, m_id = s.image(alb), s.image(rough), s.image(metal)
+    nconst = s.constant((0.55, 0.45, 0.9))
+    mats = configs.rgb_box_materials(s)
+    mats["White"] = s.pbr(a_id, normal=nconst, roughness=r_id, metalness=m_id)
+    mats["Green"] = s.lambert(albedo=a_id)
+    for v0, v1, v2, mname, _ in configs._BOX:
+        P = np.array([v0, v1, v2], np.float64)
+        span = P.max(0) - P.min(0)
+        ax = [i for i in range(3) if span[i] > 0][:2]
+        uv = [(P[k, ax[0]] / 100.0, P[k, ax[1]] / 100.0) for k in range(3)]
+        s.add_triangles([v0], [v1], [v2], mats[mname], uv=[[c for p in uv for c in p]])
+    s.add_sphere((35, 20, 45), 18, s.pbr(s.constant((0.7, 0.5, 0.3)), normal=nconst, roughness=r_id))
+    s.add_sphere((70, 15, 30), 12, s.pbr(a_id, normal=s.constant((0.5, 0.5, 1.0)), metalness=m_id))
+    configs.cornell_camera(s, 1.0)
+    return s
+
+
+def test_pbr_texture_storage_forms_bitwise(gpu):
+    scene = pbr_storage_box()
+    r = GPURenderer(scene, 48, 48, 8)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--bvh", default="gpu")
+    ap.add_argument("--pass-log", action="store_true", help="per-pass trace/shade times and queue lengths on stderr")
     a = ap.parse_args()
     import torch
     from izpi_amd import _native as N
@@ -26,7 +27,8 @@ def main():
     from izpi_amd.renderer import GPURenderer, common_tiles
     cfg = configs.configs()[a.config]
     spp = a.spp or cfg.spp
-    r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, bvh=a.bvh)
+    r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, bvh=a.bvh,
+                    tuning=N.tuning(flags=[N.TUNE_PASS_LOG]) if a.pass_log else None)
     all_tiles = common_tiles(cfg.width, cfg.height)
     t1 = None
     for w in [int(x) for x in a.worlds.split(",")]:

@@ -1,7 +1,7 @@
 """A/B experiments on compile-time variants of the library.
 
     python tools/variants.py build NAME [-DFOO ...]      # here (CPU): izpi_amd/_lib/variants/NAME/libizpi_gpu.so
-    python tools/variants.py run --config C4 --spp 64 --frames 3 base NAME ...   # on the GPU box
+    python tools/variants.py run --config C4 --spp 64 --frames 3 [--tune slots=N ...] base NAME ...   # on the GPU box
 
 `base` is the product library. Each variant renders in a fresh child process (same scene,
 same request) and prints one JSON line per frame: device time, trace / shade / tail ms and
@@ -46,17 +46,30 @@ def child(a):
     from izpi_amd import _native as N
     if a.variant != "base":
         N.LIB_PATH = VDIR / a.variant / "libizpi_gpu.so"
+
+        class OlderLib(N.C.CDLL):  # a variant built from an older checkout may lack newer entry points
+            def __getattr__(self, name):
+                try:
+                    return super().__getattr__(name)
+                except AttributeError:
+                    return N.C.CFUNCTYPE(N.C.c_int)(lambda *args: -1)
+        N.C.CDLL = OlderLib
     from izpi_amd import configs
     from izpi_amd.renderer import GPURenderer
     cfg = configs.configs()[a.config]
     spp = a.spp or cfg.spp
+    tune = {}
+    for kv in a.tune or []:
+        k, v = kv.split("=")
+        tune[k] = int(v)
     r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=0,
-                    bvh="gpu")
+                    bvh="gpu", tuning=N.tuning(**tune) if tune else None)
     post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
     for i in range(a.frames):
         img = r.render(post=post)
         st = r.stats
-        print(json.dumps({"variant": a.variant, "config": a.config, "spp": spp, "frame": i,
+        print(json.dumps({"variant": a.variant, "tune": tune, "config": a.config, "spp": spp, "frame": i,
+                          "slots": st["slots"], "chunk_spp": st["chunk_spp"], "workspace_gb": round(st["workspace_bytes"] / 1e9, 1),
                           "device_ms": round(st["total_ms"], 3), "trace_ms": round(st["kernel_ms"], 3),
                           "shade_ms": round(st["shade_ms"], 3), "tail_ms": round(st["tail_ms"], 3),
                           "launches": st["launches"], "rays": st["rays"],
@@ -69,6 +82,8 @@ def run(a):
         cmd = [sys.executable, __file__, "child", "--config", a.config, "--frames", str(a.frames), "--variant", v]
         if a.spp:
             cmd += ["--spp", str(a.spp)]
+        for kv in a.tune or []:
+            cmd += ["--tune", kv]
         rc = subprocess.run(cmd, timeout=a.timeout).returncode
         if rc != 0:
             sys.exit("variant %s: exit %d" % (v, rc))
@@ -86,12 +101,14 @@ def main():
     r.add_argument("--spp", type=int, default=None)
     r.add_argument("--frames", type=int, default=3)
     r.add_argument("--timeout", type=int, default=300)
+    r.add_argument("--tune", action="append", help="izpi_render_tuning field=value (repeatable)")
     r.add_argument("variants", nargs="+")
     c = sub.add_parser("child")
     c.add_argument("--config", default="C3")
     c.add_argument("--spp", type=int, default=None)
     c.add_argument("--frames", type=int, default=3)
     c.add_argument("--variant", default="base")
+    c.add_argument("--tune", action="append")
     a, rest = p.parse_known_args()
     if a.cmd == "build":
         build(a.name, a.defines + rest, a.src)
