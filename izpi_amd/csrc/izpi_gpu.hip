@@ -75,6 +75,20 @@ enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP,
        CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_PARK, CNT_SCLK_MAT, CNT_SCLK_FIN, CNT_SCLK_MIX, CNT_SCLK_LPDF,
        CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
+// Frame counters without atomics: a render's kernels add their per-wave counts to the
+// wave's own row of `cpart` ([rows][CNT_N], rows = 4 x the largest grid, zeroed per frame)
+// with a plain load and store by lane 0 (the waves of a launch own distinct rows; launches
+// run one after another), and k_cpart_reduce folds the rows into the counters at the end of
+// the frame. Per-wave atomics on the one line of counters made every launch end in a burst
+// of ~36k serialised atomics when all waves finish together: a ~0.4 ms floor per k_trace2
+// pass, 4 ms of a 45-ms eighth-of-C3 share. Without `cpart` (component entries) the
+// counts go to the counters by atomics as before.
+IZPI_DEV void count_add(unsigned long long* cpart, unsigned long long* counters, int k, unsigned long long v) {
+  if (v == 0) return;
+  if (cpart) cpart[(size_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * CNT_N + k] += v;
+  else atomicAdd(counters + k, v);
+}
+
 
 // ======================================================= textures / spectra
 // ImageTxt.Value (image.go:73-101): the nearest texel of a w x h image at (u, v), from
@@ -338,6 +352,7 @@ struct WaveParams {
   const uint32_t* in_park;    // nonzero: the pass that wrote `in` parked entries (k_trace2 reads kind words), or null
   uint32_t* out_park;         // set by k_shade when it parks an entry of `out` (zeroed by k_trace2)
   uint32_t hit_uv;            // k_shade may read a hit's (u, v): spheres (the root) or (u,v)-reading textures
+  unsigned long long* cpart;  // per-wave counter rows (count_add), or null
 };
 IZPI_DEV double ray_tmin(const WaveBuf& b, uint32_t i, uint32_t kind) {
   return b.tminmax ? b.tminmax[i].x : (kind_of(kind) == RAY_PATHLEN ? 0.0 : 0.001);
@@ -486,6 +501,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // dequeue atomic on the one counter word (~88/us chip-wide).
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t chunk = min(tchunk, max(16u, (n + nwaves - 1u) / nwaves));
+  // the root node's 112 B in LDS: a new ray's first visit reads it there (fused refill)
+  __shared__ float4 lds_root[7];
+  if (sc.root >= 0 && threadIdx.x < 7) lds_root[threadIdx.x] = reinterpret_cast<const float4*>(sc.inner + sc.root)[threadIdx.x];
+  __syncthreads();
   if ((uint64_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk >= n) return;
   uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
   uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
@@ -500,7 +519,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int clean_from = 0;     // stack entries at positions >= clean_from were pushed after the last accepted hit
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
-  uint32_t c_pos = 0, c_end = 0;  // wave-private range [c_pos, c_end) of the input queue
+  // wave-private range [c_pos, c_end) of the input queue; the first one is the wave's own
+  uint32_t c_pos = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk);  // (uniform: SGPR)
+  uint32_t c_end = c_pos + chunk < n ? c_pos + chunk : n;
+  bool fresh = false;     // the lane took a new entry whose ray the next node step loads and decodes
+#ifndef IZPI_NO_FUSED_REFILL
+  const bool root_inner = sc.root >= 0;  // the fused refill (below) visits an inner root from LDS
+#else
+  const bool root_inner = false;         // A/B builds: the separate refill round trip of round 2
+#endif
 #ifdef IZPI_TRACE_CLOCKS
   uint64_t k_refill = 0, k_node = 0, k_prim = 0, k_adv = 0, k0 = 0, k1 = 0;
 #define IZPI_CLK(v) (v) = __builtin_readcyclecounter()
@@ -514,10 +541,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint32_t nidle = (uint32_t)__popcll(idle);
       if (!exhausted && (nidle >= refill_min || idle == ~0ull) && c_pos >= c_end) {
         // the wave's private range of the queue is used up: take the next `chunk`
-        // entries with one atomic (a single head word saturates near 88 dequeues/us)
+        // entries with one atomic (a single head word saturates near 88 dequeues/us).
+        // Every wave's first chunk is its own (chunk w, set before the loop), without an
+        // atomic: a pass of at most nwaves chunks (the tail passes) dequeues without any.
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(wp.trace_next, chunk);
-        b = __builtin_amdgcn_readfirstlane(b);
+        b = __builtin_amdgcn_readfirstlane(b) + nwaves * chunk;
         if (b >= n) exhausted = true;
         c_pos = b;
         c_end = b + chunk < n ? b + chunk : n;
@@ -529,7 +558,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         bool main_ray = false;
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
         const uint32_t my = base + rank;
-        if (!busy && rank < take) {
+        if (root_inner) {
+          // Fused refill: the new lanes only take their entries here. Their rays are loaded
+          // by the next node step's own loads (in place of a node: the root's data is in
+          // LDS), so the refill costs no memory round trip of its own and the root visit
+          // none either (the step decodes the rays, then tests them against the root).
+          if (!busy && rank < take) {
+            qi = my;
+            fresh = true;
+            busy = true;
+            in_prim = false;
+            cur = sc.root;
+            sp = 0; low = 0; clean_from = 0;
+            bprim = -1;
+          }
+        } else if (!busy && rank < take) {
           const uint32_t k = read_kind ? wp.in.kind[my] : (uint32_t)RAY_MAIN;
           // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
           const RayOD& r = wp.in.ray[my];
@@ -549,10 +592,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (!busy) wp.in.hit[my] = HitSt{0.0, -1, 0u, 0.0, 0.0};
           }
         }
-        c_rays += (uint64_t)__popcll(__ballot(main_ray));
-        // drain the new rays' loads here: left pending they make the compiler wait for
-        // vmcnt(0) at the loop head, i.e. for every hit-record store, on every iteration
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        if (!root_inner) {
+          c_rays += (uint64_t)__popcll(__ballot(main_ray));
+          // drain the new rays' loads here: left pending they make the compiler wait for
+          // vmcnt(0) at the loop head, i.e. for every hit-record store, on every iteration
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
       } else if (exhausted && idle == ~0ull) {
         break;
       }
@@ -568,7 +613,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     IZPI_CLK(k1); k_refill += k1 - k0; k0 = k1;
     const bool clk_prim = n_prim * prim_w >= n_node * 16u;
 #endif
-    if (n_prim * prim_w >= n_node * 16u) {
+    const bool any_fresh = __ballot(fresh) != 0;
+    if (!any_fresh && n_prim * prim_w >= n_node * 16u) {
       if constexpr (DIST) {
         // ---- distributed primitive step: every pending test of the PRIM lanes' leaves
         // (up to 64) runs on its own lane, then each owner accepts its leaf's results in
@@ -701,10 +747,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       c_pstep++;
       }
     } else {
-      c_nodes += n_node;
       c_nstep++;
       // ---- node step: visit `cur` (bvh4.go:87-146)
-      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
       if (__ballot(busy && !in_prim && sp + 3 - low > S) != 0) {
         // ring too full for this step's three writes: spill the oldest entries (rare)
         if (busy && !in_prim) {
@@ -714,29 +758,68 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
         }
       }
+      // An inner node (4-slot box test) and a leaf's slot-0 re-test (A10) run as ONE
+      // code path: a leaf lane's 32-B GLeaf box lands in slot 0 (selects below), its
+      // slots 1-3 are invalid. Mixed waves (nearly every node step) then issue one set
+      // of loads and wait once, instead of running the two branches one after the other.
+      // A fresh lane (fused refill) loads its 48-B ray record with the same loads (its
+      // last four read past the record, inside the state allocation; unused) and visits
+      // the root from the LDS copy.
+      const bool is_leaf = ref_is_leaf(cur);
+      float4 q0 = make_float4(0, 0, 0, 0), q1 = q0, mnz_ = q0, mxx_ = q0, mxy_ = q0, mxz_ = q0;
+      int4 ch_ = make_int4(-1, -1, -1, -1);
+      uint32_t fk = RAY_MAIN;
       if (busy && !in_prim) {
-        const float tm = (float)tmax;
-        // An inner node (4-slot box test) and a leaf's slot-0 re-test (A10) run as ONE
-        // code path: a leaf lane's 32-B GLeaf box lands in slot 0 (selects below), its
-        // slots 1-3 are invalid. Mixed waves (nearly every node step) then issue one set
-        // of loads and wait once, instead of running the two branches one after the other.
-        const bool is_leaf = ref_is_leaf(cur);
-        const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
-                                                                   : (const void*)(sc.inner + cur));
+        const float4* lp = reinterpret_cast<const float4*>(
+            fresh ? (const void*)(wp.in.ray + qi)
+                  : (is_leaf ? (const void*)(sc.leaves + leaf_start(cur)) : (const void*)(sc.inner + cur)));
         // leaf lanes read their last five loads from the root node (a cached valid address;
         // the values are not used)
-        const float4* np = is_leaf ? reinterpret_cast<const float4*>(sc.inner) : lp;
-        const float4 q0 = lp[0], q1 = lp[1];
-        const float4 mnz_ = np[2], mxx_ = np[3], mxy_ = np[4], mxz_ = np[5];
-        const int4 ch_ = *reinterpret_cast<const int4*>(np + 6);
+        const float4* np = (is_leaf && !fresh) ? reinterpret_cast<const float4*>(sc.inner) : lp;
+        q0 = lp[0]; q1 = lp[1];
+        mnz_ = np[2]; mxx_ = np[3]; mxy_ = np[4]; mxz_ = np[5];
+        ch_ = *reinterpret_cast<const int4*>(np + 6);
+        if (fresh && read_kind) fk = wp.in.kind[qi];
+      }
+      if (any_fresh) {
+        bool main_ray = false;
+        if (fresh) {
+          // RayOD = o[3], d[3] as doubles: (q0.xy) (q0.zw) (q1.xy) | (q1.zw) (mnz_.xy) (mnz_.zw)
+          auto dbl = [](float lo, float hi) { return __hiloint2double(__float_as_int(hi), __float_as_int(lo)); };
+          const double o0 = dbl(q0.x, q0.y), o1 = dbl(q0.z, q0.w), o2 = dbl(q1.x, q1.y);
+          const double d0 = dbl(q1.z, q1.w), d1 = dbl(mnz_.x, mnz_.y), d2 = dbl(mnz_.z, mnz_.w);
+          // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
+          if (!(fk & (RAY_PARKED | RAY_DEAD)) && (uint64_t)__double_as_longlong(o0) != DEAD_BITS) {
+            lkind = fk;
+            tmax = ray_tmax(wp.in, qi, fk);
+            main_ray = kind_of(fk) == RAY_MAIN;
+            ix = (float)(1.0 / d0); iy = (float)(1.0 / d1); iz = (float)(1.0 / d2);
+            ox = (float)o0; oy = (float)o1; oz = (float)o2;
+            fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
+          } else {
+            busy = false;
+            fresh = false;
+          }
+        }
+        c_rays += (uint64_t)__popcll(__ballot(main_ray));
+      }
+      c_nodes += (uint64_t)__popcll(__ballot(busy && !in_prim));
+      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
+      if (busy && !in_prim) {
+        const float tm = (float)tmax;
         // GLeaf = (mn.x, mn.y, mn.z, mx.x), (mx.y, mx.z, start, count)
-        const float4 mnx = q0;
-        const float4 mny = make_float4(is_leaf ? q0.y : q1.x, q1.y, q1.z, q1.w);
-        const float4 mnz = make_float4(is_leaf ? q0.z : mnz_.x, mnz_.y, mnz_.z, mnz_.w);
-        const float4 mxx = make_float4(is_leaf ? q0.w : mxx_.x, mxx_.y, mxx_.z, mxx_.w);
-        const float4 mxy = make_float4(is_leaf ? q1.x : mxy_.x, mxy_.y, mxy_.z, mxy_.w);
-        const float4 mxz = make_float4(is_leaf ? q1.y : mxz_.x, mxz_.y, mxz_.z, mxz_.w);
-        const int4 ch = make_int4(is_leaf ? cur : ch_.x, ch_.y, ch_.z, ch_.w);
+        float4 mnx = q0;
+        float4 mny = make_float4(is_leaf ? q0.y : q1.x, q1.y, q1.z, q1.w);
+        float4 mnz = make_float4(is_leaf ? q0.z : mnz_.x, mnz_.y, mnz_.z, mnz_.w);
+        float4 mxx = make_float4(is_leaf ? q0.w : mxx_.x, mxx_.y, mxx_.z, mxx_.w);
+        float4 mxy = make_float4(is_leaf ? q1.x : mxy_.x, mxy_.y, mxy_.z, mxy_.w);
+        float4 mxz = make_float4(is_leaf ? q1.y : mxz_.x, mxz_.y, mxz_.z, mxz_.w);
+        int4 ch = make_int4(is_leaf ? cur : ch_.x, ch_.y, ch_.z, ch_.w);
+        if (any_fresh && fresh) {
+          mnx = lds_root[0]; mny = lds_root[1]; mnz = lds_root[2]; mxx = lds_root[3]; mxy = lds_root[4]; mxz = lds_root[5];
+          const float4 c = lds_root[6];
+          ch = make_int4(__float_as_int(c.x), __float_as_int(c.y), __float_as_int(c.z), __float_as_int(c.w));
+        }
         uint32_t hm;
         if (wave_fast) {
           hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
@@ -782,6 +865,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         sp += np_;
         advance = !enter;
       }
+      fresh = false;
     }
 #ifdef IZPI_TRACE_CLOCKS
     IZPI_CLK(k1); if (clk_prim) k_prim += k1 - k0; else k_node += k1 - k0; k0 = k1;
@@ -838,13 +922,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 #endif
   if (lane == 0) {
-    if (c_rays) atomicAdd(counters + CNT_RAYS, (unsigned long long)c_rays);
-    if (c_nodes) atomicAdd(counters + CNT_NODES, (unsigned long long)c_nodes);
-    if (c_tri) atomicAdd(counters + CNT_TRI, (unsigned long long)c_tri);
-    if (c_sph) atomicAdd(counters + CNT_SPH, (unsigned long long)c_sph);
-    atomicAdd(counters + CNT_NSTEP, (unsigned long long)c_nstep);
-    atomicAdd(counters + CNT_PSTEP, (unsigned long long)c_pstep);
-    atomicAdd(counters + CNT_SHORT, (unsigned long long)c_short);
+    count_add(wp.cpart, counters, CNT_RAYS, c_rays);
+    count_add(wp.cpart, counters, CNT_NODES, c_nodes);
+    count_add(wp.cpart, counters, CNT_TRI, c_tri);
+    count_add(wp.cpart, counters, CNT_SPH, c_sph);
+    count_add(wp.cpart, counters, CNT_NSTEP, c_nstep);
+    count_add(wp.cpart, counters, CNT_PSTEP, c_pstep);
+    count_add(wp.cpart, counters, CNT_SHORT, c_short);
   }
 }
 
@@ -930,6 +1014,9 @@ IZPI_DEV double lights_pdf(const DevScene& sc, V3 o, V3 v, uint32_t& c_lt, uint3
       }
     } else {
       c_ls++;
+#ifdef IZPI_EXP_NO_SPHERE_LPDF  // timing experiment only (wrong radiance, same paths): the sphere terms' cost
+      continue;
+#endif
       double t; int root;
       if (sph_intersect_at(ld3(L.cz), L.radius, o, v, 0.001, 1.7976931348623157e308, t, root)) {
         double cosThetaMax = gm::sqrt(1 - L.radius * L.radius / sqlen(sub(ld3(L.c0), o)));
@@ -1022,6 +1109,7 @@ struct ShadeParams {
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
   unsigned long long* counters;
+  unsigned long long* cpart;   // per-wave counter rows (count_add), or null
   uint32_t* error;
 };
 
@@ -1112,10 +1200,13 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   // The records are read four levels at a time (one batch of independent loads, then
   // the levels applied in order), so a path of depth d waits ~d/4 memory round trips.
   constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
+  // levels per batch of record loads: 8 for the Spectral sampler's 24-B records (C5 shade
+  // -2.2% against 4), 4 for Colour (8 made C3's compact records +13%: more live registers)
 #ifndef IZPI_FIN_RB
-#define IZPI_FIN_RB 4
-#endif
+  constexpr int RB = SAMPLER == IZPI_SAMPLER_SPECTRAL ? 8 : 4;
+#else
   constexpr int RB = IZPI_FIN_RB;
+#endif
   for (int dd = (int)P.depth - 1; dd >= 0; dd -= RB) {
     double rv[RB][D];
     if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {
@@ -1832,7 +1923,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   for (int k = 0; k < 3; k++) {
     unsigned long long s = vals[k];
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
-    if (lane == 0 && s) atomicAdd(sp.counters + idx[k], s);
+    if (lane == 0) count_add(sp.cpart, sp.counters, idx[k], s);
   }
 }
 
@@ -1879,8 +1970,24 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
   for (int k = 0; k < 9; k++) {
     unsigned long long v = vals[k];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
-    if (lane == 0 && v) atomicAdd(sp.counters + idx[k], v);
+    if (lane == 0) count_add(sp.cpart, sp.counters, idx[k], v);
   }
+}
+
+constexpr uint32_t CPART_BLOCKS_PER_CU = 16;  // counter rows per CU / 4: above any resident 256-thread grid
+// End of frame: counters[k] += the sum of column k of the per-wave rows (count_add).
+__global__ void __launch_bounds__(256) k_cpart_reduce(const unsigned long long* cpart, uint32_t rows,
+                                                      unsigned long long* counters) {
+  __shared__ unsigned long long red[256];
+  unsigned long long v = 0;
+  for (uint32_t r = threadIdx.x; r < rows; r += 256) v += cpart[(size_t)r * CNT_N + blockIdx.x];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counters[blockIdx.x] += red[0];
 }
 
 // Publish the frees of the last shading pass (k_trace2 does it at its start; k_tail and
@@ -2176,6 +2283,7 @@ struct izpi_ctx {
   double* d_bg = nullptr; size_t bg_cap = 0;
   uint32_t* d_misc = nullptr;              // [0] unit head, [1] error, [2] trace cursor, [3..4] queue counts, [6..7] park flags
   unsigned long long* d_counters = nullptr;
+  unsigned long long* d_cpart = nullptr; size_t cpart_cap = 0;  // per-wave counter rows of a render (count_add)
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
@@ -2231,7 +2339,7 @@ int grow(izpi_ctx* ctx, void** p, size_t* cap, size_t bytes) {
 uint64_t workspace_bytes(const izpi_ctx* ctx) {
   return (uint64_t)ctx->samples_cap + ctx->recs_cap + ctx->pool_cap + ctx->ring_cap + ctx->running_cap + ctx->out_cap +
          ctx->tiles_cap + ctx->utiles_cap + ctx->bg_cap + ctx->state_cap + ctx->spill_cap + ctx->post_cap + ctx->share_cap +
-         ctx->gather_cap;
+         ctx->gather_cap + ctx->cpart_cap;
 }
 
 // Device bytes of the buffers render_impl sizes per frame and may release to re-size
@@ -2404,6 +2512,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   int tail_res = 0;
   if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res)
                       : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
+  if ((uint32_t)std::max({tr.blocks, shade_res, tail_res}) > ctx->num_cus * CPART_BLOCKS_PER_CU) {
+    ctx->err = "grid larger than the counter rows";
+    return IZPI_ERR_INVALID;
+  }
   uint64_t tail_max = (uint64_t)tail_res * 256;
   if (tu.tail_paths) tail_max = tu.tail_paths;
   if (tu.flags & IZPI_TUNE_NO_TAIL) tail_max = 0;
@@ -2645,6 +2757,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const size_t nbg = req->num_bg_spd;
   if (nbg && (!req->bg_spd_wavelengths || !req->bg_spd_values)) { ctx->err = "num_bg_spd without the SPD arrays"; return IZPI_ERR_INVALID; }
   if ((rc = grow(ctx, (void**)&ctx->d_bg, &ctx->bg_cap, (2 * nbg + 1) * sizeof(double)))) return rc;
+  // counter rows: one per wave of the largest grid (run_chunks checks the grids against it)
+  const uint32_t cpart_rows = ctx->num_cus * CPART_BLOCKS_PER_CU * 4u;
+  if ((rc = grow(ctx, (void**)&ctx->d_cpart, &ctx->cpart_cap, (size_t)cpart_rows * CNT_N * sizeof(unsigned long long)))) return rc;
   const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count();
   WaveBuf bufs[2];
   carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, bufs);
@@ -2656,6 +2771,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   }
   HIP_TRY(hipMemsetAsync(ctx->d_running, 0, (size_t)num_pixels * 3 * sizeof(double), st));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(ctx->d_cpart, 0, (size_t)cpart_rows * CNT_N * sizeof(unsigned long long), st));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), st));
 
   ShadeParams sp{};
@@ -2672,13 +2788,14 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = ctx->d_misc;
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
-  sp.counters = ctx->d_counters; sp.error = ctx->d_misc + 1;
+  sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = ctx->d_misc + 1;
   WaveParams wp{};
   wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
   // kind words other than plain main rays: path-length rays, parked entries
   wp.read_kind = !ctx->sc.no_pathlen ? 1u : 0u;  // parked entries: wp.in_park, per pass
   wp.hit_uv = (!ctx->sc.tri_only || ctx->any_uv) ? 1u : 0u;
   wp.pool_ctr = sp.pool_ctr;
+  wp.cpart = ctx->d_cpart;
   AccumParams ap{};
   ap.num_pixels = num_pixels; ap.spp = req->spp; ap.width = req->width; ap.height = req->height;
   ap.tile_w = tw; ap.tile_h = th; ap.sampler = req->sampler; ap.out_layout = req->out_layout;
@@ -2702,6 +2819,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
                               : IZPI_RUN(IZPI_SAMPLER_SPECTRAL, MATSET_FULL);
 #undef IZPI_RUN
   if (rc) return rc;
+  hipLaunchKernelGGL(k_cpart_reduce, dim3(CNT_N), dim3(256), 0, st, ctx->d_cpart, cpart_rows, ctx->d_counters);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev1, st));
   if ((rc = apply_post(ctx, req, out_dev))) return rc;
   HIP_TRY(hipEventSynchronize(ctx->ev1));
@@ -2863,7 +2982,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_pool, ctx->d_ring, ctx->d_pool_ctr, ctx->d_running, ctx->d_out,
                   ctx->d_tiles, ctx->d_utiles, ctx->d_bg, ctx->d_misc, ctx->d_counters, ctx->d_state,
                   ctx->d_spill, ctx->d_post, ctx->d_share,
-                  ctx->d_gather, ctx->d_status};
+                  ctx->d_gather, ctx->d_status, ctx->d_cpart};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb[i]) (void)hipEventDestroy(ctx->evb[i]);
@@ -3324,7 +3443,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; HitSt* hh;
   HIP_TRY(tmp.alloc(&dr, (size_t)n * 8));
   HIP_TRY(tmp.alloc(&dh, n));
-  HIP_TRY(tmp.alloc(&rr, n));
+  HIP_TRY(tmp.alloc(&rr, (size_t)n + 2));  // + 2: k_trace2's fused refill reads up to 64 B past a ray record
   HIP_TRY(tmp.alloc(&kk, n));
   HIP_TRY(tmp.alloc(&tm, n));
   HIP_TRY(tmp.alloc(&hh, n));
