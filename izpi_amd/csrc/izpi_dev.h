@@ -58,6 +58,14 @@ struct alignas(32) GShade {
 __host__ __device__ inline uint32_t gs_mat(const GShade& g) { return g.mk >> 8; }
 __host__ __device__ inline uint32_t gs_kind(const GShade& g) { return (g.mk >> 2) & 63u; }
 __host__ __device__ inline uint32_t gs_cflags(const GShade& g) { return g.mk & 3u; }
+// Texture-space data of a triangle, in BVH leaf order next to GShade (a hit's primitive
+// indexes it directly, so it loads in parallel with GShade instead of after it): the
+// vertex UVs (triangle.go:61-134) and the tangent / bitangent of the normal map's TBN
+// (triangle.go:250-264). Uploaded only for scenes with image textures or normal maps.
+struct alignas(16) GTriTex {
+  double uv[6];     // u0, v0, u1, v1, u2, v2
+  double tg[3], bt[3];
+};
 // Light record (Scene.Lights entry, transport order): everything PDFValue/Random read.
 struct alignas(16) GLight {
   double v0[3], v1[3], v2[3], e1[3], e2[3], n[3];  // triangle
@@ -91,16 +99,10 @@ struct DevScene {
   const GLeaf* leaves;
   const GPrim* prims;
   const GShade* shade;          // [num_prims], leaf order
-  const double* tri_normal;     // [nt][3]
-  const double* tri_uv;         // [nt][6]
-  const double* tri_tangent;    // [nt][3]
-  const double* tri_bitangent;  // [nt][3]
-  const uint32_t* tri_mat;
-  const uint32_t* sph_mat;
+  const GTriTex* tritex;        // [num_prims], leaf order: triangle UVs and tangent frame (textured scenes only, else null)
   const GLight* lights;
   const izpi_material* materials;
   const izpi_texture* textures;
-  const uint32_t* mat_flags;    // per material: bit0 needs hit-record UVs (image textures)
   const double4* mat_const;     // per material: its constant RGB albedo / emit texture value (GShade cflags bit0)
   const MatTex* mat_tex;        // per material: its RGB texture slots
   const double* texels;

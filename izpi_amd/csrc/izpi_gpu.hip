@@ -124,6 +124,17 @@ IZPI_DEV V3 slot_rgb(const DevScene& sc, const TexSlot& s, double u, double v) {
   return tex_rgb(sc, (int32_t)s.off, u, v);
 }
 IZPI_DEV bool slot_set(const TexSlot& s) { return (s.hf >> 30) != TEXF_NONE; }
+// The materials' texture slots staged in LDS next to their constants (mc_stage): a PBR
+// hit reads its slots with an LDS read instead of a dependent L2 load.
+constexpr uint32_t MT_LDS = 64;
+IZPI_DEV MatTex* mt_lds() {
+  __shared__ MatTex t[MT_LDS];
+  return t;
+}
+// Slot k of material m: from LDS when staged (`staged`), else from DevScene::mat_tex.
+IZPI_DEV TexSlot mat_slot(const DevScene& sc, bool staged, uint32_t m, int k) {
+  return staged ? mt_lds()[m].s[k] : sc.mat_tex[m].s[k];
+}
 // First interval [wl[i], wl[i+1]] of a NON-DECREASING table that holds w, for
 // n >= 2 and wl[0] <= w <= wl[n-1]: i = (first j >= 1 with wl[j] >= w) - 1, which is the interval
 // the reference's linear scan stops at (spectral.go:151-181, spectral_constant.go:88-106):
@@ -501,10 +512,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // dequeue atomic on the one counter word (~88/us chip-wide).
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t chunk = min(tchunk, max(16u, (n + nwaves - 1u) / nwaves));
-  // the root node's 112 B in LDS: a new ray's first visit reads it there (fused refill)
-  __shared__ float4 lds_root[7];
-  if (sc.root >= 0 && threadIdx.x < 7) lds_root[threadIdx.x] = reinterpret_cast<const float4*>(sc.inner + sc.root)[threadIdx.x];
-  __syncthreads();
   if ((uint64_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk >= n) return;
   uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
   uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
@@ -522,12 +529,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // wave-private range [c_pos, c_end) of the input queue; the first one is the wave's own
   uint32_t c_pos = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk);  // (uniform: SGPR)
   uint32_t c_end = c_pos + chunk < n ? c_pos + chunk : n;
-  bool fresh = false;     // the lane took a new entry whose ray the next node step loads and decodes
-#ifndef IZPI_NO_FUSED_REFILL
-  const bool root_inner = sc.root >= 0;  // the fused refill (below) visits an inner root from LDS
-#else
-  const bool root_inner = false;         // A/B builds: the separate refill round trip of round 2
-#endif
 #ifdef IZPI_TRACE_CLOCKS
   uint64_t k_refill = 0, k_node = 0, k_prim = 0, k_adv = 0, k0 = 0, k1 = 0;
 #define IZPI_CLK(v) (v) = __builtin_readcyclecounter()
@@ -558,21 +559,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         bool main_ray = false;
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
         const uint32_t my = base + rank;
-        if (root_inner) {
-          // Fused refill: the new lanes only take their entries here. Their rays are loaded
-          // by the next node step's own loads (in place of a node: the root's data is in
-          // LDS), so the refill costs no memory round trip of its own and the root visit
-          // none either (the step decodes the rays, then tests them against the root).
-          if (!busy && rank < take) {
-            qi = my;
-            fresh = true;
-            busy = true;
-            in_prim = false;
-            cur = sc.root;
-            sp = 0; low = 0; clean_from = 0;
-            bprim = -1;
-          }
-        } else if (!busy && rank < take) {
+        if (!busy && rank < take) {
           const uint32_t k = read_kind ? wp.in.kind[my] : (uint32_t)RAY_MAIN;
           // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
           const RayOD& r = wp.in.ray[my];
@@ -592,12 +579,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (!busy) wp.in.hit[my] = HitSt{0.0, -1, 0u, 0.0, 0.0};
           }
         }
-        if (!root_inner) {
-          c_rays += (uint64_t)__popcll(__ballot(main_ray));
-          // drain the new rays' loads here: left pending they make the compiler wait for
-          // vmcnt(0) at the loop head, i.e. for every hit-record store, on every iteration
-          __builtin_amdgcn_s_waitcnt(0x0F70);
-        }
+        c_rays += (uint64_t)__popcll(__ballot(main_ray));
+        // drain the new rays' loads here: left pending they make the compiler wait for
+        // vmcnt(0) at the loop head, i.e. for every hit-record store, on every iteration
+        __builtin_amdgcn_s_waitcnt(0x0F70);
       } else if (exhausted && idle == ~0ull) {
         break;
       }
@@ -613,8 +598,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     IZPI_CLK(k1); k_refill += k1 - k0; k0 = k1;
     const bool clk_prim = n_prim * prim_w >= n_node * 16u;
 #endif
-    const bool any_fresh = __ballot(fresh) != 0;
-    if (!any_fresh && n_prim * prim_w >= n_node * 16u) {
+    if (n_prim * prim_w >= n_node * 16u) {
       if constexpr (DIST) {
         // ---- distributed primitive step: every pending test of the PRIM lanes' leaves
         // (up to 64) runs on its own lane, then each owner accepts its leaf's results in
@@ -747,8 +731,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       c_pstep++;
       }
     } else {
+      c_nodes += n_node;
       c_nstep++;
       // ---- node step: visit `cur` (bvh4.go:87-146)
+      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
       if (__ballot(busy && !in_prim && sp + 3 - low > S) != 0) {
         // ring too full for this step's three writes: spill the oldest entries (rare)
         if (busy && !in_prim) {
@@ -758,68 +744,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
         }
       }
-      // An inner node (4-slot box test) and a leaf's slot-0 re-test (A10) run as ONE
-      // code path: a leaf lane's 32-B GLeaf box lands in slot 0 (selects below), its
-      // slots 1-3 are invalid. Mixed waves (nearly every node step) then issue one set
-      // of loads and wait once, instead of running the two branches one after the other.
-      // A fresh lane (fused refill) loads its 48-B ray record with the same loads (its
-      // last four read past the record, inside the state allocation; unused) and visits
-      // the root from the LDS copy.
-      const bool is_leaf = ref_is_leaf(cur);
-      float4 q0 = make_float4(0, 0, 0, 0), q1 = q0, mnz_ = q0, mxx_ = q0, mxy_ = q0, mxz_ = q0;
-      int4 ch_ = make_int4(-1, -1, -1, -1);
-      uint32_t fk = RAY_MAIN;
-      if (busy && !in_prim) {
-        const float4* lp = reinterpret_cast<const float4*>(
-            fresh ? (const void*)(wp.in.ray + qi)
-                  : (is_leaf ? (const void*)(sc.leaves + leaf_start(cur)) : (const void*)(sc.inner + cur)));
-        // leaf lanes read their last five loads from the root node (a cached valid address;
-        // the values are not used)
-        const float4* np = (is_leaf && !fresh) ? reinterpret_cast<const float4*>(sc.inner) : lp;
-        q0 = lp[0]; q1 = lp[1];
-        mnz_ = np[2]; mxx_ = np[3]; mxy_ = np[4]; mxz_ = np[5];
-        ch_ = *reinterpret_cast<const int4*>(np + 6);
-        if (fresh && read_kind) fk = wp.in.kind[qi];
-      }
-      if (any_fresh) {
-        bool main_ray = false;
-        if (fresh) {
-          // RayOD = o[3], d[3] as doubles: (q0.xy) (q0.zw) (q1.xy) | (q1.zw) (mnz_.xy) (mnz_.zw)
-          auto dbl = [](float lo, float hi) { return __hiloint2double(__float_as_int(hi), __float_as_int(lo)); };
-          const double o0 = dbl(q0.x, q0.y), o1 = dbl(q0.z, q0.w), o2 = dbl(q1.x, q1.y);
-          const double d0 = dbl(q1.z, q1.w), d1 = dbl(mnz_.x, mnz_.y), d2 = dbl(mnz_.z, mnz_.w);
-          // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
-          if (!(fk & (RAY_PARKED | RAY_DEAD)) && (uint64_t)__double_as_longlong(o0) != DEAD_BITS) {
-            lkind = fk;
-            tmax = ray_tmax(wp.in, qi, fk);
-            main_ray = kind_of(fk) == RAY_MAIN;
-            ix = (float)(1.0 / d0); iy = (float)(1.0 / d1); iz = (float)(1.0 / d2);
-            ox = (float)o0; oy = (float)o1; oz = (float)o2;
-            fast = sc.nan_free_bounds && ray_fast_ok(ox, oy, oz, ix, iy, iz);
-          } else {
-            busy = false;
-            fresh = false;
-          }
-        }
-        c_rays += (uint64_t)__popcll(__ballot(main_ray));
-      }
-      c_nodes += (uint64_t)__popcll(__ballot(busy && !in_prim));
-      const bool wave_fast = __ballot(busy && !in_prim && !fast) == 0;
       if (busy && !in_prim) {
         const float tm = (float)tmax;
+        // An inner node (4-slot box test) and a leaf's slot-0 re-test (A10) run as ONE
+        // code path: a leaf lane's 32-B GLeaf box lands in slot 0 (selects below), its
+        // slots 1-3 are invalid. Mixed waves (nearly every node step) then issue one set
+        // of loads and wait once, instead of running the two branches one after the other.
+        const bool is_leaf = ref_is_leaf(cur);
+        const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
+                                                                   : (const void*)(sc.inner + cur));
+        // leaf lanes read their last five loads from the root node (a cached valid address;
+        // the values are not used)
+        const float4* np = is_leaf ? reinterpret_cast<const float4*>(sc.inner) : lp;
+        const float4 q0 = lp[0], q1 = lp[1];
+        const float4 mnz_ = np[2], mxx_ = np[3], mxy_ = np[4], mxz_ = np[5];
+        const int4 ch_ = *reinterpret_cast<const int4*>(np + 6);
         // GLeaf = (mn.x, mn.y, mn.z, mx.x), (mx.y, mx.z, start, count)
-        float4 mnx = q0;
-        float4 mny = make_float4(is_leaf ? q0.y : q1.x, q1.y, q1.z, q1.w);
-        float4 mnz = make_float4(is_leaf ? q0.z : mnz_.x, mnz_.y, mnz_.z, mnz_.w);
-        float4 mxx = make_float4(is_leaf ? q0.w : mxx_.x, mxx_.y, mxx_.z, mxx_.w);
-        float4 mxy = make_float4(is_leaf ? q1.x : mxy_.x, mxy_.y, mxy_.z, mxy_.w);
-        float4 mxz = make_float4(is_leaf ? q1.y : mxz_.x, mxz_.y, mxz_.z, mxz_.w);
-        int4 ch = make_int4(is_leaf ? cur : ch_.x, ch_.y, ch_.z, ch_.w);
-        if (any_fresh && fresh) {
-          mnx = lds_root[0]; mny = lds_root[1]; mnz = lds_root[2]; mxx = lds_root[3]; mxy = lds_root[4]; mxz = lds_root[5];
-          const float4 c = lds_root[6];
-          ch = make_int4(__float_as_int(c.x), __float_as_int(c.y), __float_as_int(c.z), __float_as_int(c.w));
-        }
+        const float4 mnx = q0;
+        const float4 mny = make_float4(is_leaf ? q0.y : q1.x, q1.y, q1.z, q1.w);
+        const float4 mnz = make_float4(is_leaf ? q0.z : mnz_.x, mnz_.y, mnz_.z, mnz_.w);
+        const float4 mxx = make_float4(is_leaf ? q0.w : mxx_.x, mxx_.y, mxx_.z, mxx_.w);
+        const float4 mxy = make_float4(is_leaf ? q1.x : mxy_.x, mxy_.y, mxy_.z, mxy_.w);
+        const float4 mxz = make_float4(is_leaf ? q1.y : mxz_.x, mxz_.y, mxz_.z, mxz_.w);
+        const int4 ch = make_int4(is_leaf ? cur : ch_.x, ch_.y, ch_.z, ch_.w);
         uint32_t hm;
         if (wave_fast) {
           hm = slab4_fast(mnx, mny, mnz, mxx, mxy, mxz, ox, oy, oz, ix, iy, iz, tm);
@@ -865,7 +812,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         sp += np_;
         advance = !enter;
       }
-      fresh = false;
     }
 #ifdef IZPI_TRACE_CLOCKS
     IZPI_CLK(k1); if (clk_prim) k_prim += k1 - k0; else k_node += k1 - k0; k0 = k1;
@@ -942,33 +888,33 @@ struct HitRec {
 };
 // `uvp` is the hit record, whose (u, v): read only for UV-textured triangles and for spheres.
 IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, const GShade& gs, V3 o, V3 d, double time,
-                         bool want_uv, HitRec& h) {
+                         bool want_uv, HitRec& h, bool mt_staged = false) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
   h.mat = gs_mat(gs);
   h.nraw_ok = false;
   if (IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
-    const uint32_t ti = IZPI_PRIM_INDEX(gs.ref);
     V3 n = mk(gs.n[0], gs.n[1], gs.n[2]);
     h.u = 0; h.v = 0;
-    if (want_uv) {  // (u,v) are read only by image textures
+    if (want_uv && sc.tritex) {  // (u,v) are read only by image textures
       const double eps = 1e-8;
       double u = uvp->u, v = uvp->v;
       double w = 1.0 - u - v;
       double sum = u + v + w;
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
-      const double* uv = sc.tri_uv + 6 * (size_t)ti;  // u0,v0,u1,v1,u2,v2
+      const double* uv = sc.tritex[c.prim].uv;  // u0,v0,u1,v1,u2,v2
       h.u = w * uv[0] + u * uv[2] + v * uv[4];
       h.v = w * uv[1] + u * uv[3] + v * uv[5];
     }
     if (gs_kind(gs) == IZPI_MAT_PBR) {
-      const TexSlot ns = sc.mat_tex[h.mat].s[1];
+      const TexSlot ns = mat_slot(sc, mt_staged, h.mat, 1);
       if (slot_set(ns)) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
         V3 nts = slot_rgb(sc, ns, h.u, h.v);
         h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
         h.nraw_ok = true;
         nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
-        V3 tg = ld3(sc.tri_tangent + 3 * (size_t)ti), bt = ld3(sc.tri_bitangent + 3 * (size_t)ti);
+        const GTriTex& tt = sc.tritex[c.prim];
+        V3 tg = ld3(tt.tg), bt = ld3(tt.bt);
         V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
                    tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
         n = sdiv(nn, length(nn));
@@ -1105,6 +1051,7 @@ struct ShadeParams {
   double* recs;                // [slots][rec_dense][D] unwinding records
   double* pool;                // [blocks][rec_pool][D] overflow unwinding records
   const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
+  uint32_t num_mc, mc_in_lds;  // materials; mat_const staged in LDS (num_mc <= MC_LDS, mc_stage)
   uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
@@ -1179,6 +1126,24 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
 }
 IZPI_DEV bool rec_is_spec(double s) { return (uint64_t)__double_as_longlong(s) == REC_SPEC_BITS; }
 
+// The materials' constant RGB values (DevScene::mat_const) and texture slots (mt_lds)
+// staged in LDS by k_shade and k_tail when there are at most MC_LDS materials: the compact
+// records' unwinding (finish) and constant-albedo hits read them with an LDS read instead
+// of a dependent L2 load.
+constexpr uint32_t MC_LDS = MT_LDS;
+IZPI_DEV double4* mc_lds() {
+  __shared__ double4 c[MC_LDS];
+  return c;
+}
+IZPI_DEV void mc_stage(const DevScene& sc, const ShadeParams& sp) {
+  if (sp.mc_in_lds) {
+    if (threadIdx.x < sp.num_mc) mc_lds()[threadIdx.x] = sp.mat_const[threadIdx.x];
+    for (uint32_t t = threadIdx.x; t < 4 * sp.num_mc; t += blockDim.x) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
+  }
+  __syncthreads();
+}
+IZPI_DEV double4 mat_const_of(const ShadeParams& sp, uint32_t m) { return sp.mc_in_lds ? mc_lds()[m] : sp.mat_const[m]; }
+
 // Result slot of work unit `unit` (= pixel * chunk_spp + sample). Unit-major: paths of
 // neighbouring units finish close in time and fill whole lines (a sample-major layout
 // made k_accumulate coalesced but cost k_shade 16% in scattered partial-line stores).
@@ -1222,7 +1187,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
 #pragma unroll
       for (int j = 0; j < RB; j++) {
         if (dd - j >= 0) {
-          const double4 c = sp.mat_const[(uint32_t)rv[j][0]];
+          const double4 c = mat_const_of(sp, (uint32_t)rv[j][0]);
           cv[j][0] = c.x; cv[j][1] = c.y; cv[j][2] = c.z;
         }
       }
@@ -1610,7 +1575,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h);
+    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, sp.mc_in_lds != 0);
     hit_n = h.n;
     rec_mat = h.mat;
     next_o = h.p;
@@ -1619,7 +1584,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
     const izpi_material& m = sc.materials[h.mat];
     const bool cconst = COLOUR && (gs_cflags(gs) & 1u) != 0;
     V3 cval = mk(0, 0, 0);
-    if (cconst) { const double4 c4 = sc.mat_const[h.mat]; cval = mk(c4.x, c4.y, c4.z); }
+    if (cconst) { const double4 c4 = mat_const_of(sp, h.mat); cval = mk(c4.x, c4.y, c4.z); }
     switch (gs_kind(gs)) {
       case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
         if (dot(h.n, rd) < 0.0) {
@@ -1683,10 +1648,11 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       }
       case IZPI_MAT_PBR: {  // pbr.go:59-155 / 158-263
         if constexpr (!ms_has(MATSET, MS_PBR)) { atomicOr(sp.error, 2u); terminal = true; break; }
-        // the four texture slots in one 64-B record; every lookup below is issued before
-        // the first of them is used
-        const MatTex& mt = sc.mat_tex[h.mat];
-        const TexSlot s_alb = mt.s[0], s_nrm = mt.s[1], s_rgh = mt.s[2], s_met = mt.s[3];
+        // the four texture slots (LDS, or one 64-B record); every lookup below is issued
+        // before the first of them is used
+        const bool stg = sp.mc_in_lds != 0;
+        const TexSlot s_alb = mat_slot(sc, stg, h.mat, 0), s_nrm = mat_slot(sc, stg, h.mat, 1),
+                      s_rgh = mat_slot(sc, stg, h.mat, 2), s_met = mat_slot(sc, stg, h.mat, 3);
         double alb_s = 0;
         if (COLOUR) att = slot_rgb(sc, s_alb, h.u, h.v);
         else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
@@ -1847,6 +1813,7 @@ template <int SAMPLER, int MATSET>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  mc_stage(sc, sp);
   uint32_t parity = 0;  // block_reserve2 LDS buffer set
   const uint32_t n = *wp.in_count;
   // this pass's k_trace2 is done with its dequeue cursor: reset it for the next pass's
@@ -1934,6 +1901,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 // Same per-ray code paths, results and counters as k_trace + k_shade.
 template <int SAMPLER, int MATSET, int STACK>
 __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  mc_stage(sc, sp);
   __shared__ int32_t lds_stack[STACK * 256];
   int32_t* stk = lds_stack + threadIdx.x;
   const uint32_t n = *wp.in_count;
@@ -2265,6 +2233,7 @@ struct izpi_ctx {
   // scene
   bool have_scene = false;
   uint32_t num_textures = 0;     // of the uploaded scene (izpi_gpu_gomath texture lookups)
+  uint32_t num_materials = 0;    // of the uploaded scene
   DevScene sc{};
   uint32_t stack_needed = 0;
   uint32_t num_prims = 0;
@@ -2683,10 +2652,13 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
   const uint64_t avail = free_b ? ((uint64_t)free_b + render_buffer_bytes(ctx)) / std::max(1u, ctx->dev_share) : 0;
+  // The render workspace stays within 9/16 of the HBM (~160 GB of 288): per-sample results
+  // within 1/8, the wavefront state in the rest.
   // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
-  // sample order. One chunk per request when it fits in 1/4 of the HBM (C3: 12.9 GB of
-  // 288 GB), so the wavefront drains once per frame instead of once per chunk.
-  uint64_t max_units = std::max<uint64_t>(64ull << 20, (avail / 4) / (3 * sizeof(double)));
+  // sample order. One chunk per request when it fits in 1/8 of the HBM (C3: 12.9 GB of
+  // 288 GB), so the wavefront drains once per frame instead of once per chunk (C4 at 1024
+  // spp: 2 chunks, C5 at 4096 spp: 12; a chunk's drain costs a few ms).
+  uint64_t max_units = std::max<uint64_t>(64ull << 20, (avail / 8) / (3 * sizeof(double)));
   if (tu.chunk_units) max_units = tu.chunk_units;
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
@@ -2727,11 +2699,16 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   pool_div = std::max(1u, pool_div >> std::min(ctx->pool_grow, 4u));
   if (tu.pool_div) pool_div = tu.pool_div;
   const uint64_t per_block = (uint64_t)rec_pool * D * sizeof(double) + sizeof(uint32_t);
-  // The wavefront state within half of the HBM. The overflow pool rounds up to a power of
-  // two per ring, up to twice slots / pool_div blocks: counted at that worst case (C4 at
-  // 256M slots otherwise took 271 GB of the 288).
+  // The wavefront state in the rest of the workspace budget. The overflow pool rounds up
+  // to a power of two per ring, up to twice slots / pool_div blocks: counted at that worst
+  // case (C4 at 256M slots otherwise took 271 GB of the 288). C3 keeps its 256M slots
+  // (135 GB); C5 at 128 spp ran 1.4% faster at 64M slots than at 118M (less state, better
+  // cache and TLB reach in k_shade), so the smaller budget costs the deep-path scenes nothing.
+  const uint64_t samples_bytes = (uint64_t)num_pixels * chunk * 3 * sizeof(double);
+  const uint64_t budget = avail / 16 * 9;
   if (avail > 0)
-    slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (avail / 2) / (per_slot + 2 * per_block / pool_div + 1)));
+    slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (budget > samples_bytes ? budget - samples_bytes : 0) /
+                                                                          (per_slot + 2 * per_block / pool_div + 1)));
   const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);
   uint32_t pool_blocks = 0;
   if (rec_pool) {  // POOL_SHARDS rings of a power of two each, at least 16 blocks per ring
@@ -2786,6 +2763,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.pool_shift = 0;
   while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = ctx->d_misc;
+  sp.num_mc = ctx->num_materials; sp.mc_in_lds = ctx->num_materials <= MC_LDS ? 1u : 0u;
+#ifdef IZPI_NO_MC_LDS
+  sp.mc_in_lds = 0;  // A/B builds
+#endif
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = ctx->d_misc + 1;
@@ -3179,23 +3160,35 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   // ---- upload
   DevScene& sc = ctx->sc;
   memset(&sc, 0, sizeof(sc));
-  GInner* di; GLeaf* dl; GPrim* dp; GShade* dsh; GLight* dlt;
-  double *dn, *duv, *dtg, *dbt, *dtex, *dswl, *dsv;
-  uint32_t *dtm, *dsm, *dmf;
+  GInner* di; GLeaf* dl; GPrim* dp; GShade* dsh; GLight* dlt; GTriTex* dtt = nullptr;
+  double *dtex, *dswl, *dsv;
   izpi_material* dm; izpi_texture* dtx;
   UP(inner.data(), inner.size(), &di);
   UP(leaves.data(), leaves.size(), &dl);
   UP(prims.data(), prims.size(), &dp);
   UP(shade.data(), shade.size(), &dsh);
-  UP(d->tri_normal, 3 * (size_t)nt, &dn);
-  UP(d->tri_uv, 6 * (size_t)nt, &duv);
-  UP(d->tri_tangent, 3 * (size_t)nt, &dtg);
-  UP(d->tri_bitangent, 3 * (size_t)nt, &dbt);
-  UP(d->tri_mat, nt, &dtm);
-  UP(d->sph_mat, ns, &dsm);
+  for (uint32_t i = 0; i < d->num_materials; i++)
+    if (d->materials[i].kind == IZPI_MAT_PBR && d->materials[i].normal_tex >= 0 && nt && (!d->tri_tangent || !d->tri_bitangent)) {
+      ctx->err = "a PBR normal map needs the triangles' tangents and bitangents";
+      return IZPI_ERR_INVALID;
+    }
+  // triangle UVs and tangent frames in leaf order (shading reads them for image textures
+  // and normal maps; izpi_gpu_trace's hit records carry the UVs)
+  if (d->num_prims && (d->tri_uv || d->tri_tangent || d->tri_bitangent)) {
+    std::vector<GTriTex> tt(d->num_prims);
+    for (uint32_t k = 0; k < d->num_prims; k++) {
+      memset(&tt[k], 0, sizeof(GTriTex));
+      const uint32_t r = d->prim_ref[k];
+      if (IZPI_PRIM_KIND(r) != IZPI_PRIM_TRIANGLE) continue;
+      const size_t ti = IZPI_PRIM_INDEX(r);
+      if (d->tri_uv) memcpy(tt[k].uv, d->tri_uv + 6 * ti, 48);
+      if (d->tri_tangent) memcpy(tt[k].tg, d->tri_tangent + 3 * ti, 24);
+      if (d->tri_bitangent) memcpy(tt[k].bt, d->tri_bitangent + 3 * ti, 24);
+    }
+    UP(tt.data(), tt.size(), &dtt);
+  }
   UP(lights.data(), lights.size(), &dlt);
   UP(d->materials, d->num_materials, &dm);
-  UP(mflags.data(), mflags.size(), &dmf);
   double4* dmc;
   UP(mconst.data(), mconst.size(), &dmc);
   for (uint32_t i = 0; i < d->num_textures; i++) {
@@ -3275,9 +3268,8 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(texels.data(), texels.size(), &dtex);
   UP(d->spd_wavelengths, d->num_spd, &dswl);
   UP(d->spd_values, d->num_spd, &dsv);
-  sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tri_normal = dn; sc.tri_uv = duv; sc.tri_tangent = dtg;
-  sc.tri_bitangent = dbt; sc.tri_mat = dtm; sc.sph_mat = dsm; sc.lights = dlt; sc.materials = dm;
-  sc.mat_flags = dmf; sc.mat_const = dmc; sc.mat_tex = dmt; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
+  sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tritex = dtt; sc.lights = dlt; sc.materials = dm;
+  sc.mat_const = dmc; sc.mat_tex = dmt; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
   sc.tri_only = d->num_spheres == 0 ? 1u : 0u;
@@ -3313,6 +3305,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   }
   ctx->have_scene = true;
   ctx->num_textures = d->num_textures;
+  ctx->num_materials = d->num_materials;
   return IZPI_OK;
 }
 
@@ -3443,7 +3436,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; HitSt* hh;
   HIP_TRY(tmp.alloc(&dr, (size_t)n * 8));
   HIP_TRY(tmp.alloc(&dh, n));
-  HIP_TRY(tmp.alloc(&rr, (size_t)n + 2));  // + 2: k_trace2's fused refill reads up to 64 B past a ray record
+  HIP_TRY(tmp.alloc(&rr, n));
   HIP_TRY(tmp.alloc(&kk, n));
   HIP_TRY(tmp.alloc(&tm, n));
   HIP_TRY(tmp.alloc(&hh, n));
