@@ -194,14 +194,14 @@ def traffic_summary(pmc):
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(cfg, scene, budget_s, spp, bvh):
+def cpu_baseline(cfg, scene, budget_s, spp, bvh, leaf_max):
     """Oracle render of a bounded sample of the same frame (tiles spread over the frame,
     full spp when it fits the budget), timed on the CPUs this process may use, on the tree
     the GPU figure uses (like for like) and on izpi's own NewBVH4 tree; half the budget each."""
     import ctypes as C
     import numpy as np
     from izpi_amd import _native as N
-    from izpi_amd.renderer import GPU_BVH_LEAF_MAX, GPU_BVH_METHOD, common_tiles
+    from izpi_amd.renderer import GPU_BVH_METHOD, common_tiles
     from oracle import oracle as O
     cpus = host_cpus()
     threads = cpus["usable"]
@@ -236,7 +236,7 @@ def cpu_baseline(cfg, scene, budget_s, spp, bvh):
     ref_value, ref_sample = measure(o, budget_s / 2)
     value, sample, tree = ref_value, ref_sample, "izpi's own NewBVH4 tree"
     if bvh == "gpu":  # the GPU-built tree, restated on the CPU node for node (oracle.lbvh4)
-        nodes, order = O.lbvh4(o.prim_boxes(), GPU_BVH_LEAF_MAX, GPU_BVH_METHOD)
+        nodes, order = O.lbvh4(o.prim_boxes(), leaf_max, GPU_BVH_METHOD)
         o.set_bvh(nodes, order)
         value, sample = measure(o, budget_s / 2)
         tree = "the GPU-built PLOC tree (the tree of `value`)"
@@ -404,6 +404,7 @@ def main():
             elapsed = float(e.item())
         last = r.stats[0] if mode == "threads" else r.stats
         info = {"triangles": int(r.host.desc.num_tris), "nodes": int(r.host.desc.num_nodes),
+                "leaf_max": getattr(r, "bvh_leaf_max", None),
                 "build_ms": r.bvh_build_ms if bvh == "gpu" else r.host.build_ms, "setup_s": setup,
                 "first_frame_ms": first_ms, "first_frame_alloc_ms": first_alloc_ms, "workspace_gb": (last or {}).get("workspace_bytes", 0) / 1e9,
                 "scene_gb": (last or {}).get("scene_bytes", 0) / 1e9, "slots": (last or {}).get("slots"),
@@ -488,7 +489,7 @@ def main():
         roof["pmc_error"] = pmc["error"]
     cpu = None
     if mode == "single" and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, scene, args.cpu_seconds, spp, args.bvh)
+        cpu = cpu_baseline(cfg, scene, args.cpu_seconds, spp, args.bvh, info.get("leaf_max"))
         # like for like: the GPU and the CPU oracle on the same tree
         cpu["gpu_speedup"] = value / cpu["value"]
         if ref_check and cpu.get("value_reference_tree"):
@@ -510,7 +511,7 @@ def main():
         "data": "synthetic (deterministic Cornell box + 817k-triangle displaced cube-sphere dragon)",
         "config": {"workload": cfg.name, "width": cfg.width, "height": cfg.height, "spp": spp,
                    "max_depth": cfg.max_depth, "triangles": info["triangles"],
-                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "parallelism": "tiles%d" % n_gpus, "mode": mode,
+                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "bvh_leaf_max": info["leaf_max"], "parallelism": "tiles%d" % n_gpus, "mode": mode,
                    "samples_per_step": samples_per_step},
         "roofline": roof,
         "cpu_baseline": cpu,

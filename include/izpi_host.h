@@ -89,6 +89,11 @@ uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint3
 uint32_t izpi_host_share_tiles(const uint32_t* tiles, uint32_t num_tiles, uint32_t share, uint32_t num_shares,
                                uint32_t* out);
 
+/* Primitives per leaf for izpi_gpu_build_bvh4 on this scene: 3, or 2 when spheres are at
+ * least a quarter of the primitives (a sphere test costs more than a node visit; C5 at
+ * 32 spp: -2.9% per frame with 2). The Python host, the C replay and the Go shim all use it. */
+uint32_t izpi_host_bvh_leaf_max(const izpi_scene_desc* desc);
+
 /* Doubles per padded share block of a packed multi-GPU gather: ceil(num_tiles /
  * num_shares) * tile_w * tile_h * 4 (every share's block has this size). */
 uint64_t izpi_host_share_block(uint32_t num_tiles, uint32_t tile_w, uint32_t tile_h, uint32_t num_shares);

@@ -7,7 +7,7 @@
  *   2. izpi_scene_set_image per loaded image texture      (here: none / a flat test texture)
  *   3. izpi_scene_to_input(aspect = W/H, bvh seed 12345) -> izpi_host_build_scene_ex(SKIP_BVH)
  *   4. izpi_gpu_open / izpi_gpu_multi_open (Options.Devices), izpi_host_scene_prim_boxes,
- *      izpi_gpu_build_bvh4(leaf 3, PLOC) -> izpi_host_scene_set_bvh
+ *      izpi_gpu_build_bvh4(leaf izpi_host_bvh_leaf_max, PLOC) -> izpi_host_scene_set_bvh
  *   5. izpi_gpu_upload_scene / izpi_gpu_multi_upload_scene, the whole-frame request:
  *      sampler from the scene's colour representation, IZPI_POST_SPECTRAL for the
  *      spectral sampler, IZPI_POST_GAMMA_CLAMP with --png-pipeline, exposure = camera's;
@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
     uint32_t num_nodes = 0;
     double ms = 0;
     if (izpi_host_scene_prim_boxes(host, boxes)) return fail("izpi_host_scene_prim_boxes", izpi_host_last_error());
-    if (izpi_gpu_build_bvh4(ctx, boxes, np, 3, IZPI_BVH_PLOC, nodes, 2 * np, &num_nodes, order, &ms))
+    if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC, nodes, 2 * np, &num_nodes, order, &ms))
       return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
     if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
     free(boxes); free(nodes); free(order);

@@ -197,7 +197,7 @@ EXPORTS = [
     "izpi_gpu_multi_size", "izpi_gpu_multi_context", "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render",
     "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
-    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_share_block", "izpi_host_assemble_shares", "izpi_host_gomath", "izpi_abi_struct_size",
+    "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_share_block", "izpi_host_assemble_shares", "izpi_host_bvh_leaf_max", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_serialize", "izpi_scene_info", "izpi_scene_image_file",
     "izpi_scene_set_image", "izpi_scene_add_triangles", "izpi_scene_background", "izpi_scene_to_input",
     "izpi_scene_material_name", "izpi_scene_free", "izpi_light_source", "izpi_light_source_name",
@@ -269,6 +269,8 @@ def lib():
     L.izpi_host_tiles.restype = C.c_uint32
     L.izpi_host_share_tiles.argtypes = [c_uint32_p, C.c_uint32, C.c_uint32, C.c_uint32, c_uint32_p]
     L.izpi_host_share_tiles.restype = C.c_uint32
+    L.izpi_host_bvh_leaf_max.argtypes = [C.POINTER(SceneDesc)]
+    L.izpi_host_bvh_leaf_max.restype = C.c_uint32
     L.izpi_host_share_block.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.izpi_host_share_block.restype = C.c_uint64
     L.izpi_host_assemble_shares.argtypes = [C.c_uint32, C.c_uint32, c_uint32_p, C.c_uint32, C.c_uint32, c_double_p,

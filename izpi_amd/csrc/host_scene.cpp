@@ -560,6 +560,11 @@ uint32_t izpi_host_tiles(uint32_t width, uint32_t height, uint32_t* tiles, uint3
   return n < max_tiles ? n : max_tiles;
 }
 
+uint32_t izpi_host_bvh_leaf_max(const izpi_scene_desc* desc) {
+  const uint64_t np = desc ? (uint64_t)desc->num_tris + desc->num_spheres : 0;
+  return np > 0 && 4ull * desc->num_spheres >= np ? 2u : 3u;
+}
+
 uint32_t izpi_host_share_tiles(const uint32_t* tiles, uint32_t num_tiles, uint32_t share, uint32_t num_shares,
                                uint32_t* out) {
   if (!tiles || !out || num_shares == 0) return 0;

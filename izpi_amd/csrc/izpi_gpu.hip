@@ -2234,6 +2234,14 @@ struct izpi_ctx {
   bool have_scene = false;
   uint32_t num_textures = 0;     // of the uploaded scene (izpi_gpu_gomath texture lookups)
   uint32_t num_materials = 0;    // of the uploaded scene
+  // The workspace sizing of the last render and what it was decided for (render_impl): a
+  // request of the same shape reuses it, so frames of one renderer never re-size (sizing
+  // from the free HBM of each frame made C4 reallocate its 148 GB every frame, 2 s each).
+  struct Sizing {
+    uint64_t key[8];
+    uint32_t chunk, slots, pool_blocks, pool_div;
+  } sizing{};
+  bool sizing_valid = false;
   DevScene sc{};
   uint32_t stack_needed = 0;
   uint32_t num_prims = 0;
@@ -2649,8 +2657,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // Sizing against the HBM this context may use: what is free plus the render buffers it
   // holds and would release (a later frame reuses them, so every frame of a renderer sizes
   // alike), shared evenly by the contexts of one process on this device.
+  const uint64_t size_key[8] = {num_pixels, req->spp, req->sampler, req->max_depth, ctx->pool_grow,
+                                ((uint64_t)tu.slots << 32) | tu.chunk_units, ((uint64_t)tu.rec_dense << 32) | tu.pool_div, 0};
+  const bool reuse = ctx->sizing_valid && memcmp(size_key, ctx->sizing.key, sizeof(size_key)) == 0;
   size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  if (!reuse && hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
   const uint64_t avail = free_b ? ((uint64_t)free_b + render_buffer_bytes(ctx)) / std::max(1u, ctx->dev_share) : 0;
   // The render workspace stays within 9/16 of the HBM (~160 GB of 288): per-sample results
   // within 1/8, the wavefront state in the rest.
@@ -2660,7 +2671,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // spp: 2 chunks, C5 at 4096 spp: 12; a chunk's drain costs a few ms).
   uint64_t max_units = std::max<uint64_t>(64ull << 20, (avail / 8) / (3 * sizeof(double)));
   if (tu.chunk_units) max_units = tu.chunk_units;
-  const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
+  const uint32_t chunk = reuse ? ctx->sizing.chunk : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
   // blocks (ShadeParams::rec_pool). Colour records are 40 B (24 B compact), spectral 24 B.
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
@@ -2698,6 +2709,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   uint32_t pool_div = (spectral || !ctx->basic_materials) ? 4u : 16u;
   pool_div = std::max(1u, pool_div >> std::min(ctx->pool_grow, 4u));
   if (tu.pool_div) pool_div = tu.pool_div;
+  if (reuse) pool_div = ctx->sizing.pool_div;
   const uint64_t per_block = (uint64_t)rec_pool * D * sizeof(double) + sizeof(uint32_t);
   // The wavefront state in the rest of the workspace budget. The overflow pool rounds up
   // to a power of two per ring, up to twice slots / pool_div blocks: counted at that worst
@@ -2709,12 +2721,15 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (avail > 0)
     slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (budget > samples_bytes ? budget - samples_bytes : 0) /
                                                                           (per_slot + 2 * per_block / pool_div + 1)));
-  const uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);
+  const uint32_t slots = reuse ? ctx->sizing.slots : (uint32_t)std::min<uint64_t>((uint64_t)num_pixels * chunk, slot_cap);
   uint32_t pool_blocks = 0;
   if (rec_pool) {  // POOL_SHARDS rings of a power of two each, at least 16 blocks per ring
     pool_blocks = POOL_SHARDS * 16;
     while (pool_blocks < slots / pool_div && pool_blocks < (1u << 30)) pool_blocks <<= 1;
   }
+  memcpy(ctx->sizing.key, size_key, sizeof(size_key));
+  ctx->sizing.chunk = chunk; ctx->sizing.slots = slots; ctx->sizing.pool_blocks = pool_blocks; ctx->sizing.pool_div = pool_div;
+  ctx->sizing_valid = true;
   const bool need_time = !ctx->sc.tri_only;  // only sphere tests read the ray time
   // The render buffers this frame needs. When one of them must grow, all are released
   // before any is allocated, so a frame never holds an old buffer next to a new one (the
@@ -2729,7 +2744,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
       {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, nullptr)},
       {(void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes},
   };
-  if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0])))) return rc;
+  if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0])))) {
+    ctx->sizing_valid = false;
+    return rc;
+  }
   if ((rc = grow(ctx, (void**)&ctx->d_tiles, &ctx->tiles_cap, tiles.size() * sizeof(uint32_t)))) return rc;
   const size_t nbg = req->num_bg_spd;
   if (nbg && (!req->bg_spd_wavelengths || !req->bg_spd_values)) { ctx->err = "num_bg_spd without the SPD arrays"; return IZPI_ERR_INVALID; }
@@ -3304,6 +3322,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     ctx->num_prims = d->num_prims;
   }
   ctx->have_scene = true;
+  ctx->sizing_valid = false;  // per-slot sizes depend on the scene
   ctx->num_textures = d->num_textures;
   ctx->num_materials = d->num_materials;
   return IZPI_OK;

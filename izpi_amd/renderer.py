@@ -30,6 +30,16 @@ GPU_BVH_METHOD = N.BVH_PLOC
 GPU_BVH_LEAF_MAX = 3  # measured on C3: 3 -> 1146, 2 -> 1137, 4 -> 1065 Msamples/s
 
 
+def gpu_leaf_max(desc):
+    """Primitives per leaf of the GPU-built tree for a scene (izpi_scene_desc), by the
+    library's rule (izpi_host_bvh_leaf_max, shared with the Go shim): 3, or 2 when
+    spheres are at least a quarter of the primitives. A sphere test (square root and two
+    f64 divisions) costs more than a node visit, so sphere-heavy scenes want smaller leaves:
+    C5 (10 spheres of 22 primitives) at 32 spp 876.7 -> 851.6 ms per frame with 2 (1: 931),
+    C4 (2 of 16) 194.9 -> 196.8 ms, C3 (no spheres) best at 3 (profiles/r3c/c5_leaf.log)."""
+    return int(N.lib().izpi_host_bvh_leaf_max(C.byref(desc)))
+
+
 def _check(rc, ctx, what):
     if rc != 0:
         msg = N.lib().izpi_gpu_last_error(ctx).decode() if ctx else ""
@@ -128,9 +138,10 @@ class GPURenderer:
             raise RuntimeError("izpi_gpu_open(%d) failed: no HIP device?" % self.device)
         self.ctx = ctx
         self.bvh_build_ms = None
+        self.bvh_leaf_max = (bvh_leaf_max or gpu_leaf_max(self.host.desc)) if bvh == "gpu" else None
         if bvh == "gpu" and host_scene is None:
             nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes(),
-                                                              bvh_leaf_max or GPU_BVH_LEAF_MAX)
+                                                              self.bvh_leaf_max)
             self.host.set_bvh(nodes, order)
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None
@@ -274,9 +285,10 @@ class MultiGPURenderer:
             raise RuntimeError("izpi_gpu_multi_open(%s) failed (status %d)" % (self.devices, rc))
         self.m = m
         self.bvh_build_ms = None
+        self.bvh_leaf_max = (bvh_leaf_max or gpu_leaf_max(self.host.desc)) if bvh == "gpu" else None
         if bvh == "gpu":
             nodes, order, self.bvh_build_ms = build_bvh4(L.izpi_gpu_multi_context(m, 0), self.host.prim_boxes(),
-                                                         bvh_leaf_max or GPU_BVH_LEAF_MAX)
+                                                         self.bvh_leaf_max)
             self.host.set_bvh(nodes, order)
         self._check(L.izpi_gpu_multi_upload_scene(m, C.byref(self.host.desc)), "izpi_gpu_multi_upload_scene")
         self.stats = None
