@@ -381,6 +381,7 @@ def main():
             t = time.perf_counter()
             sts = step()
             sync_all()
+            print("bench: warmup frame %d: %.1f ms" % (i, (time.perf_counter() - t) * 1e3), file=sys.stderr, flush=True)
             if i == 0:
                 first_ms = (time.perf_counter() - t) * 1e3
                 # host time of the workspace allocation inside that frame (hipMalloc of fresh
@@ -391,9 +392,11 @@ def main():
         sync_all()
         t1 = time.perf_counter()
         agg = {k: 0.0 for k in STAT_KEYS}
-        for _ in range(steps):
+        for k in range(steps):
             for st in step():
                 add_stats(agg, st)
+            if rank == 0 and (k + 1) % max(1, steps // 4) == 0:  # progress (long frames: C5 takes ~2 min)
+                print("bench: %d of %d timed frames issued" % (k + 1, steps), file=sys.stderr, flush=True)
         sync_all()
         if dist is not None:
             dist.barrier()

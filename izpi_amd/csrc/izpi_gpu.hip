@@ -69,6 +69,10 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
 }
 
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
+#ifndef IZPI_MISC_STRIDE
+#define IZPI_MISC_STRIDE 64
+#endif
+constexpr int MISC_STRIDE = IZPI_MISC_STRIDE;  // words between the fields of izpi_ctx::d_misc (misc()); 1 in A/B builds only
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
        CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
@@ -943,20 +947,48 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
 // ================================================================ lights
 // HitableSlice.PDFValue over Scene.Lights (hitable_slice.go:98-105) with
 // Triangle.PDFValue (triangle.go:271-280) / Sphere.PDFValue (sphere.go:129-137).
-IZPI_DEV double lights_pdf(const DevScene& sc, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
+// What PDFValue reads of light i, 16 doubles: a triangle's v0, e1, e2, n, area; a
+// sphere's center(0), radius, c0; [15] = kind. Staged in LDS by k_shade / k_tail (lt_lds,
+// at most LT_LDS lights): the light loop then reads LDS broadcasts instead of one
+// dependent global load per light (the compiler cannot use scalar loads for the GLight
+// records, which it cannot prove unwritten).
+constexpr uint32_t LT_LDS = 64;
+IZPI_DEV double* lt_lds() {
+  __shared__ double l[LT_LDS * 16];
+  return l;
+}
+IZPI_DEV void light_pack(const GLight& L, uint32_t k, double* out) {  // k = 0..15
+  double v = 0;
+  if (L.kind == IZPI_PRIM_TRIANGLE) {
+    v = k < 3 ? L.v0[k] : k < 6 ? L.e1[k - 3] : k < 9 ? L.e2[k - 6] : k < 12 ? L.n[k - 9] : k == 12 ? L.area : 0.0;
+  } else {
+    v = k < 3 ? L.cz[k] : k == 3 ? L.radius : k < 7 ? L.c0[k - 4] : 0.0;
+  }
+  if (k == 15) v = (double)L.kind;
+  out[k] = v;
+}
+// HitableSlice.PDFValue over Scene.Lights (hitable_slice.go:98-105) from the packed
+// records (LDS when staged, else `glob`, packed the same way on the fly).
+IZPI_DEV double lights_pdf(const DevScene& sc, const double* lds, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
   const double weight = 1.0 / (double)sc.num_lights;
   double sum = 0;
   for (uint32_t i = 0; i < sc.num_lights; i++) {
-    const GLight& L = sc.lights[i];
+    double r[16];
+    if (lds) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) r[k] = lds[i * 16 + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) light_pack(sc.lights[i], k, r);
+    }
     double pdf = 0;
-    if (L.kind == IZPI_PRIM_TRIANGLE) {
+    if (r[15] == (double)IZPI_PRIM_TRIANGLE) {
       c_lt++;
-      const double a[9] = {L.v0[0], L.v0[1], L.v0[2], L.e1[0], L.e1[1], L.e1[2], L.e2[0], L.e2[1], L.e2[2]};
       double t, u, w;
-      if (tri_intersect(a, o, v, 0.001, 1.7976931348623157e308, t, u, w)) {
+      if (tri_intersect(r, o, v, 0.001, 1.7976931348623157e308, t, u, w)) {  // r[0..8] = v0, e1, e2
         double dist2 = t * t * sqlen(v);
-        double cosine = gm::abs(dot(v, sdiv(ld3(L.n), length(v))));
-        pdf = dist2 / (cosine * L.area);
+        double cosine = gm::abs(dot(v, sdiv(mk(r[9], r[10], r[11]), length(v))));
+        pdf = dist2 / (cosine * r[12]);
       }
     } else {
       c_ls++;
@@ -964,8 +996,9 @@ IZPI_DEV double lights_pdf(const DevScene& sc, V3 o, V3 v, uint32_t& c_lt, uint3
       continue;
 #endif
       double t; int root;
-      if (sph_intersect_at(ld3(L.cz), L.radius, o, v, 0.001, 1.7976931348623157e308, t, root)) {
-        double cosThetaMax = gm::sqrt(1 - L.radius * L.radius / sqlen(sub(ld3(L.c0), o)));
+      const double radius = r[3];
+      if (sph_intersect_at(mk(r[0], r[1], r[2]), radius, o, v, 0.001, 1.7976931348623157e308, t, root)) {
+        double cosThetaMax = gm::sqrt(1 - radius * radius / sqlen(sub(mk(r[4], r[5], r[6]), o)));
         double solidAngle = 6.283185307179586 * (1 - cosThetaMax);
         pdf = 1 / solidAngle;
       }
@@ -1052,6 +1085,7 @@ struct ShadeParams {
   double* pool;                // [blocks][rec_pool][D] overflow unwinding records
   const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
   uint32_t num_mc, mc_in_lds;  // materials; mat_const staged in LDS (num_mc <= MC_LDS, mc_stage)
+  uint32_t lt_in_lds;          // the lights' PDFValue records staged in LDS (num_lights <= LT_LDS, mc_stage)
   uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
@@ -1140,6 +1174,8 @@ IZPI_DEV void mc_stage(const DevScene& sc, const ShadeParams& sp) {
     if (threadIdx.x < sp.num_mc) mc_lds()[threadIdx.x] = sp.mat_const[threadIdx.x];
     for (uint32_t t = threadIdx.x; t < 4 * sp.num_mc; t += blockDim.x) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
   }
+  if (sp.lt_in_lds)
+    for (uint32_t t = threadIdx.x; t < 16 * sc.num_lights; t += blockDim.x) light_pack(sc.lights[t >> 4], t & 15, lt_lds() + (t & ~15u));
   __syncthreads();
 }
 IZPI_DEV double4 mat_const_of(const ShadeParams& sp, uint32_t m) { return sp.mc_in_lds ? mc_lds()[m] : sp.mat_const[m]; }
@@ -1726,7 +1762,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         const double spdf = zero_spdf ? 0.0 : sc_cos / 3.141592653589793;  // Isotropic.ScatteringPDF is 0
         rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, spdf, rec_mat);
         SCLK_T(sc3);
-        const double pdf_val = 0.5 * lights_pdf(sc, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
+        const double pdf_val = 0.5 * lights_pdf(sc, sp.lt_in_lds ? lt_lds() : nullptr, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         SCLK_ADD(SCLK_LPDF, sc3);
         rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
         next_d = dir;
@@ -2258,7 +2294,7 @@ struct izpi_ctx {
   uint32_t* d_tiles = nullptr; size_t tiles_cap = 0;
   uint32_t* d_utiles = nullptr; size_t utiles_cap = 0;  // tile lists of k_unpack (multi-GPU root)
   double* d_bg = nullptr; size_t bg_cap = 0;
-  uint32_t* d_misc = nullptr;              // [0] unit head, [1] error, [2] trace cursor, [3..4] queue counts, [6..7] park flags
+  uint32_t* d_misc = nullptr;              // words k * MISC_STRIDE (misc()): 0 unit head, 1 error, 2 trace cursor, 3..4 queue counts, 6..7 park flags
   unsigned long long* d_counters = nullptr;
   unsigned long long* d_cpart = nullptr; size_t cpart_cap = 0;  // per-wave counter rows of a render (count_add)
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
@@ -2266,7 +2302,7 @@ struct izpi_ctx {
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
   double* d_share = nullptr; size_t share_cap = 0;    // multi-GPU: this device's packed tiles
   double* d_gather = nullptr; size_t gather_cap = 0;  // multi-GPU root: every device's packed tiles
-  uint32_t* h_count = nullptr;                        // pinned readback of d_misc (unit head, queue lengths)
+  uint32_t* h_count = nullptr;                        // pinned readback of d_misc (unit head, queue lengths; same stride) + scratch
   hipEvent_t ev3 = nullptr;
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
   // RCCL communicator of a multi-process render (izpi_gpu_comm_init), or null
@@ -2285,6 +2321,12 @@ struct izpi_ctx {
 };
 
 namespace {
+
+// The words of d_misc lie MISC_STRIDE words (256 B) apart: the unit head and the queue
+// counts take one returning atomic each per shading block-iteration (~11M per C3 frame),
+// and atomics on one line are served one at a time (a single word saturates near 88 per
+// microsecond, MI355X_MICROARCH.md "dequeue").
+uint32_t* misc(izpi_ctx* ctx, int k) { return ctx->d_misc + (size_t)k * MISC_STRIDE; }
 
 template <typename T>
 int dev_upload(izpi_ctx* ctx, const T* host, size_t count, T** out) {
@@ -2452,7 +2494,7 @@ void launch_trace(izpi_ctx* ctx, const DevScene& sc, const Tracer& t, const Wave
 #define IZPI_T2_LAUNCH(P, T)                                                                                   \
   if (t.p2 == P && t.tri == T) {                                                                               \
     hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T>), g, b, 0, st, sc, wp, ctx->d_counters,          \
-                       ctx->d_misc + 1, spill, stride, t.prim_w, t.tchunk, t.refill_min);                      \
+                       misc(ctx, 1), spill, stride, t.prim_w, t.tchunk, t.refill_min);                        \
     return;                                                                                                    \
   }
   IZPI_T2_LIST(IZPI_T2_LAUNCH)
@@ -2499,7 +2541,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   // k_tail's allocations cannot park: every tail path must find a published block
   if (sp.rec_pool) tail_max = std::min<uint64_t>(tail_max, pool_blocks);
   const WaveBuf q[2] = {wp.in, wp.out};  // the two sides of the state; entry counts in d_misc[3..4]
-  uint32_t* qn[2] = {ctx->d_misc + 3, ctx->d_misc + 4};
+  uint32_t* qn[2] = {misc(ctx, 3), misc(ctx, 4)};
   if (sp.rec_pool)
     hipLaunchKernelGGL(k_pool_init, dim3((pool_blocks + 255) / 256), dim3(256), 0, st, sp.pool_ring, pool_blocks,
                        pool_blocks / POOL_SHARDS, sp.pool_ctr);
@@ -2508,9 +2550,9 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     const uint32_t cs = std::min(chunk, req->spp - s0);
     sp.chunk_spp = cs; sp.s0 = s0; sp.total_units = num_pixels * cs;
     const uint32_t fill = std::min<uint32_t>(sp.slots, sp.total_units);
-    HIP_TRY(hipMemsetD32Async(ctx->d_misc, (int)fill, 1, st));  // unit head: k_start gives slot i unit i
-    HIP_TRY(hipMemsetAsync(ctx->d_misc + 2, 0, 3 * sizeof(uint32_t), st));  // dequeue cursor, queue counts
-    HIP_TRY(hipMemsetAsync(ctx->d_misc + 6, 0, 2 * sizeof(uint32_t), st));  // park flags of the two sides
+    HIP_TRY(hipMemsetD32Async(misc(ctx, 0), (int)fill, 1, st));  // unit head: k_start gives slot i unit i
+    HIP_TRY(hipMemsetAsync(misc(ctx, 2), 0, 3 * MISC_STRIDE * sizeof(uint32_t), st));  // dequeue cursor, queue counts
+    HIP_TRY(hipMemsetAsync(misc(ctx, 6), 0, 2 * MISC_STRIDE * sizeof(uint32_t), st));  // park flags of the two sides
     wp.out = q[0]; wp.out_count = qn[0];
     hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, sc, sp, wp);
     HIP_TRY(hipGetLastError());
@@ -2531,7 +2573,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
       for (int b = 0; b < B; b++) {
         wp.in = q[cur]; wp.in_count = qn[cur];
         wp.out = q[1 - cur]; wp.out_count = qn[1 - cur];
-        wp.in_park = ctx->d_misc + 6 + cur; wp.out_park = ctx->d_misc + 6 + (1 - cur);
+        wp.in_park = misc(ctx, 6 + cur); wp.out_park = misc(ctx, 6 + (1 - cur));
         // (k_trace2 zeroes out_count and out_park, k_shade the dequeue cursor for the next pass)
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
         launch_trace(ctx, sc, tr, wp, st, ctx->d_spill);
@@ -2542,7 +2584,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
       }
-      HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->d_misc, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->d_misc, 8 * MISC_STRIDE * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
       for (int b = 0; b < B; b++) {
         float t_ms = 0, s_ms = 0;
@@ -2553,11 +2595,12 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         if (pass_log) fprintf(stderr, "IZPI_PASS %u trace %.3f shade %.3f\n", *launches, t_ms, s_ms);
         (*launches)++;
       }
-      if (pass_log) fprintf(stderr, "IZPI_BATCH queue %u head %u\n", ctx->h_count[3 + cur], ctx->h_count[0]);
-      n = ctx->h_count[3 + cur];
-      if (ctx->h_count[0] >= sp.total_units) B = 1;
+      const uint32_t head = ctx->h_count[0];
+      n = ctx->h_count[(3 + cur) * MISC_STRIDE];
+      if (pass_log) fprintf(stderr, "IZPI_BATCH queue %u head %u\n", n, head);
+      if (head >= sp.total_units) B = 1;
       // every unit has started: finish the remaining paths in one k_tail launch
-      if (n > 0 && n <= tail_max && ctx->h_count[0] >= sp.total_units) {
+      if (n > 0 && n <= tail_max && head >= sp.total_units) {
         wp.in = q[cur]; wp.in_count = qn[cur];
         HIP_TRY(hipEventRecord(ctx->ev2, st));
         if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
@@ -2767,7 +2810,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   HIP_TRY(hipMemsetAsync(ctx->d_running, 0, (size_t)num_pixels * 3 * sizeof(double), st));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), st));
   HIP_TRY(hipMemsetAsync(ctx->d_cpart, 0, (size_t)cpart_rows * CNT_N * sizeof(unsigned long long), st));
-  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), st));
+  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * MISC_STRIDE * sizeof(uint32_t), st));
 
   ShadeParams sp{};
   sp.width = req->width; sp.height = req->height; sp.max_depth = req->max_depth;
@@ -2780,16 +2823,20 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.rec_dense = rec_dense; sp.rec_pool = rec_pool;
   sp.pool_shift = 0;
   while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
-  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = ctx->d_misc;
+  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = misc(ctx, 0);
   sp.num_mc = ctx->num_materials; sp.mc_in_lds = ctx->num_materials <= MC_LDS ? 1u : 0u;
+  sp.lt_in_lds = sc.num_lights <= LT_LDS ? 1u : 0u;
+#ifdef IZPI_NO_LT_LDS
+  sp.lt_in_lds = 0;  // A/B builds
+#endif
 #ifdef IZPI_NO_MC_LDS
   sp.mc_in_lds = 0;  // A/B builds
 #endif
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
-  sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = ctx->d_misc + 1;
+  sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = misc(ctx, 1);
   WaveParams wp{};
-  wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = ctx->d_misc + 2; wp.slots = slots;
+  wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = misc(ctx, 2); wp.slots = slots;
   // kind words other than plain main rays: path-length rays, parked entries
   wp.read_kind = !ctx->sc.no_pathlen ? 1u : 0u;  // parked entries: wp.in_park, per pass
   wp.hit_uv = (!ctx->sc.tri_only || ctx->any_uv) ? 1u : 0u;
@@ -2826,9 +2873,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   float total_ms = 0;
   HIP_TRY(hipEventElapsedTime(&total_ms, ctx->ev0, ctx->ev1));
   unsigned long long cnt[CNT_N];
-  uint32_t misc[2];
+  uint32_t misc_w[MISC_STRIDE + 1];
   HIP_TRY(hipMemcpy(cnt, ctx->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(misc, ctx->d_misc, sizeof(misc), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(misc_w, misc(ctx, 0), sizeof(misc_w), hipMemcpyDeviceToHost));
   izpi_render_stats& s = ctx->last;
   memset(&s, 0, sizeof(s));
   s.rays = cnt[CNT_RAYS]; s.node_visits = cnt[CNT_NODES]; s.tri_tests = cnt[CNT_TRI]; s.sph_tests = cnt[CNT_SPH];
@@ -2852,9 +2899,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   fprintf(stderr, "IZPI_TRACE_CLOCKS refill %llu node %llu prim %llu advance %llu (wave cycles)\n", cnt[CNT_CLK_REFILL],
           cnt[CNT_CLK_NODE], cnt[CNT_CLK_PRIM], cnt[CNT_CLK_ADV]);
 #endif
-  if (misc[1]) {
-    ctx->err = misc[1] & 1u   ? "device guard: traversal stack overflow"
-               : misc[1] & 2u ? "device guard: unknown material kind"
+  const uint32_t guard = misc_w[MISC_STRIDE];  // the error word
+  if (guard) {
+    ctx->err = guard & 1u   ? "device guard: traversal stack overflow"
+               : guard & 2u ? "device guard: unknown material kind"
                               : "device guard: no overflow record block in k_tail";
     return IZPI_ERR_DEVICE;
   }
@@ -2959,8 +3007,8 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
   ok = ok && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
        hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess &&
        hipEventCreate(&ctx->ev2) == hipSuccess && hipEventCreate(&ctx->ev3) == hipSuccess &&
-       hipHostMalloc((void**)&ctx->h_count, 8 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
-       hipMalloc((void**)&ctx->d_misc, 8 * sizeof(uint32_t)) == hipSuccess &&
+       hipHostMalloc((void**)&ctx->h_count, 9 * MISC_STRIDE * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+       hipMalloc((void**)&ctx->d_misc, 8 * MISC_STRIDE * sizeof(uint32_t)) == hipSuccess &&
        hipMalloc((void**)&ctx->d_pool_ctr, POOL_SHARDS * POOL_CTR_STRIDE * sizeof(unsigned long long)) == hipSuccess &&
        hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) == hipSuccess;
   for (int i = 0; ok && i < 3 * IZPI_PASS_BATCH; i++) ok = hipEventCreate(&ctx->evb[i]) == hipSuccess;
@@ -3460,12 +3508,12 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   HIP_TRY(tmp.alloc(&tm, n));
   HIP_TRY(tmp.alloc(&hh, n));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * sizeof(uint32_t), ctx->stream));
+  HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * MISC_STRIDE * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
-  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, ctx->d_misc + 3);
+  hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, misc(ctx, 3));
   WaveParams wp{};
   wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh;
-  wp.in_count = ctx->d_misc + 3; wp.trace_next = ctx->d_misc + 2; wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
+  wp.in_count = misc(ctx, 3); wp.trace_next = misc(ctx, 2); wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
   int rc = make_tracer(ctx, kDefaultTuning, &tr);
   if (rc) return rc;
@@ -3680,7 +3728,7 @@ namespace {
 // (ncclAllReduce(max), rccl.h). Returns non-zero only if the collective itself failed.
 int agree_status(izpi_ctx* ctx, int local, int* worst_status, uint32_t* worst_rank) {
   const int32_t word = (int32_t)((uint32_t)std::min(local, 0x7FFF) << 16 | (ctx->comm_rank & 0xFFFFu));
-  int32_t* h = (int32_t*)ctx->h_count + 6;  // pinned
+  int32_t* h = (int32_t*)ctx->h_count + 8 * MISC_STRIDE;  // pinned scratch
   h[0] = word;
   HIP_TRY(hipMemcpyAsync(ctx->d_status, h, sizeof(word), hipMemcpyHostToDevice, ctx->stream));
   const ncclResult_t r = ncclAllReduce(ctx->d_status, ctx->d_status + 1, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
