@@ -69,6 +69,13 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
 }
 
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
+#ifndef IZPI_SHADE_THREADS
+#define IZPI_SHADE_THREADS 256
+#endif
+// k_shade's block. Its reservation phase takes one unit-head and one queue atomic per
+// block-iteration; 384-thread blocks (6 waves, 2 per CU) take a third fewer but measured
+// C3 shade 114 -> 161 ms (the barriers of block_reserve2 wait for 6 waves), so 256 stays.
+constexpr uint32_t SHADE_THREADS = IZPI_SHADE_THREADS, SHADE_WAVES = SHADE_THREADS / 64;
 #ifndef IZPI_MISC_STRIDE
 #define IZPI_MISC_STRIDE 64
 #endif
@@ -1465,7 +1472,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
 // whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
 IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
                              uint32_t& pos, uint32_t& parity, bool& exhausted) {
-  __shared__ uint32_t s_p[2][4], s_u[2][4];
+  __shared__ uint32_t s_p[2][SHADE_WAVES], s_u[2][SHADE_WAVES];
   __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2], s_nent[2];
   const uint32_t b = parity;
   parity ^= 1u;
@@ -1479,8 +1486,10 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
     // until this block has seen the unit head run out (`exhausted`, thread 0's register);
     // a lane reserved an entry but denied a unit leaves a dead entry (at most one
     // iteration per block, in the frame's last passes)
-    const uint32_t np = s_p[b][0] + s_p[b][1] + s_p[b][2] + s_p[b][3];
-    const uint32_t nu = exhausted ? 0u : s_u[b][0] + s_u[b][1] + s_u[b][2] + s_u[b][3];
+    uint32_t np = 0, nu = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SHADE_WAVES; k++) { np += s_p[b][k]; nu += s_u[b][k]; }
+    if (exhausted) nu = 0;
     const uint32_t ne = np + nu;
     const uint32_t u0 = nu ? atomicAdd(sp.head, nu) : sp.total_units;
     // (an iteration without finished paths asks for nothing and learns nothing: it must
@@ -1529,8 +1538,8 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
 // wave's time once), added to the CNT_SCLK_* counters at the end of the kernel.
 enum { SCLK_MAT = 0, SCLK_FIN, SCLK_MIX, SCLK_LPDF, SCLK_N };
 IZPI_DEV unsigned long long* sclk_lds() {
-  __shared__ unsigned long long c[4][SCLK_N];
-  return &c[(threadIdx.x >> 6) & 3][0];
+  __shared__ unsigned long long c[16][SCLK_N];
+  return &c[(threadIdx.x >> 6) & 15][0];
 }
 IZPI_DEV void sclk_add(int sec, uint64_t dt) {
   const uint64_t act = __ballot(1);
@@ -1805,7 +1814,7 @@ IZPI_DEV uint32_t pool_alloc(const ShadeParams& sp, bool need) {
   const uint64_t m = __ballot(need);
   if (m == 0) return 0;
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t ring = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (POOL_SHARDS - 1);
+  const uint32_t ring = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (POOL_SHARDS - 1);
   unsigned long long* c = pool_ring_ctr(sp, ring);
   const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
   unsigned long long base = 0, pub = 0;
@@ -1846,7 +1855,7 @@ IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
 #endif
 template <int SAMPLER, int MATSET>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
+__global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   mc_stage(sc, sp);
@@ -1856,13 +1865,13 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *wp.trace_next = 0;
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
-  const uint32_t stride = gridDim.x * 256;
+  const uint32_t stride = gridDim.x * SHADE_THREADS;
 #ifdef IZPI_SHADE_CLOCKS
   uint64_t k_item = 0, k_ref = 0, k_push = 0;
   sclk_zero();
 #endif
   // Block-uniform trip count: the unit and queue reservations are block-wide.
-  for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {
+  for (uint32_t base = blockIdx.x * SHADE_THREADS; base < n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < n;
     bool push = false;      // the path has a ray to trace next (P, R)
@@ -1956,7 +1965,7 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
       if (sp.rec_pool && P.depth >= sp.rec_dense && P.blk == 0) {
         // The host launches k_tail with at most pool blocks paths, all of the free
         // blocks published, so this cannot fail (guarded anyway: no spin on a bug).
-        P.blk = pool_alloc_any(sp, blockIdx.x * 4u + (threadIdx.x >> 6));
+        P.blk = pool_alloc_any(sp, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
         if (P.blk == 0) { atomicOr(sp.error, 4u); break; }
       }
       bool push = false, done = false;
@@ -2431,9 +2440,9 @@ void free_scene(izpi_ctx* ctx) {
 }
 
 template <typename K>
-int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks) {
+int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks, int threads = 256) {
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0));
   if (per_cu < 1) per_cu = 1;
   *blocks = per_cu * ctx->num_cus;
   return IZPI_OK;
@@ -2524,14 +2533,14 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   hipStream_t st = ctx->stream;
   const izpi_render_tuning& tu = tuning_of(req);
   int shade_res = 0;
-  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res);
+  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res, (int)SHADE_THREADS);
   if (rc) return rc;
   // tail kernel: used once every unit has started and at most `tail_max` paths remain
   const bool tail_deep = ctx->stack_needed > 32;
   int tail_res = 0;
   if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res)
                       : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
-  if ((uint32_t)std::max({tr.blocks, shade_res, tail_res}) > ctx->num_cus * CPART_BLOCKS_PER_CU) {
+  if ((uint32_t)std::max({tr.blocks * 4, shade_res * (int)SHADE_WAVES, tail_res * 4}) > ctx->num_cus * CPART_BLOCKS_PER_CU * 4) {
     ctx->err = "grid larger than the counter rows";
     return IZPI_ERR_INVALID;
   }
@@ -2579,7 +2588,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         launch_trace(ctx, sc, tr, wp, st, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
-        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(256), 0, st, sc, sp, wp);
+        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(SHADE_THREADS), 0, st, sc, sp, wp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
@@ -2706,8 +2715,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   size_t free_b = 0, total_b = 0;
   if (!reuse && hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
   const uint64_t avail = free_b ? ((uint64_t)free_b + render_buffer_bytes(ctx)) / std::max(1u, ctx->dev_share) : 0;
-  // The render workspace stays within 9/16 of the HBM (~160 GB of 288): per-sample results
-  // within 1/8, the wavefront state in the rest.
+  // The render workspace stays within 17/32 of the HBM (~152 GB of 288, ~160 GB with the
+  // canvas, post-processing and counter buffers): per-sample results within 1/8, the
+  // wavefront state in the rest.
   // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
   // sample order. One chunk per request when it fits in 1/8 of the HBM (C3: 12.9 GB of
   // 288 GB), so the wavefront drains once per frame instead of once per chunk (C4 at 1024
@@ -2760,7 +2770,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // (135 GB); C5 at 128 spp ran 1.4% faster at 64M slots than at 118M (less state, better
   // cache and TLB reach in k_shade), so the smaller budget costs the deep-path scenes nothing.
   const uint64_t samples_bytes = (uint64_t)num_pixels * chunk * 3 * sizeof(double);
-  const uint64_t budget = avail / 16 * 9;
+  const uint64_t budget = avail / 32 * 17;
   if (avail > 0)
     slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (budget > samples_bytes ? budget - samples_bytes : 0) /
                                                                           (per_slot + 2 * per_block / pool_div + 1)));
