@@ -101,6 +101,64 @@ IZPI_DEV void count_add(unsigned long long* cpart, unsigned long long* counters,
 }
 
 
+// A load from a pointer known to point into LDS (the per-block staged tables): typed in
+// the LDS address space, so it is a ds_read even where the same data is read from global
+// memory on the other side of a branch (an untyped pointer there becomes a flat load).
+template <class T>
+IZPI_DEV T lds_ld(const T* p) {
+  if constexpr (sizeof(T) % 8 == 0 && alignof(T) >= 8) {  // records: word by word (no copy from an LDS lvalue)
+    T r;
+    uint64_t* d = reinterpret_cast<uint64_t*>(&r);
+    const __attribute__((address_space(3))) uint64_t* q = (const __attribute__((address_space(3))) uint64_t*)p;
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof(T) / 8; i++) d[i] = q[i];
+    return r;
+  } else {
+    return *(const __attribute__((address_space(3))) T*)p;
+  }
+}
+
+// Loader of the table lookups below: L = the table is a staged LDS copy.
+template <bool L, class T>
+IZPI_DEV T tld(const T* p) {
+  if constexpr (L) return lds_ld(p);
+  else return *p;
+}
+// The scene's small tables staged in LDS by every k_shade / k_tail block (shade_stage),
+// when they fit (ShadeParams::staged): materials, textures, tabulated SPDs, the background
+// SPD and the CIE tables. Shading then reads them with LDS reads instead of dependent
+// global loads (the compiler cannot use scalar loads for scene arrays it cannot prove
+// unwritten): the light records alone took C3's shading from 128 to 114 ms.
+constexpr uint32_t MAT_LDS = 64, TEX_LDS = 64, SPD_LDS = 384, BG_LDS = 128;
+IZPI_DEV izpi_material* mat_lds() {
+  __shared__ izpi_material m[MAT_LDS];
+  return m;
+}
+IZPI_DEV izpi_texture* tex_lds() {
+  __shared__ izpi_texture t[TEX_LDS];
+  return t;
+}
+IZPI_DEV double* spd_lds() {  // wavelengths [0, SPD_LDS), values [SPD_LDS, 2 SPD_LDS)
+  __shared__ double d[2 * SPD_LDS];
+  return d;
+}
+IZPI_DEV double* bg_lds() {   // the background SPD: wavelengths, then values
+  __shared__ double d[2 * BG_LDS];
+  return d;
+}
+IZPI_DEV double* cie_lds() {  // wavelengths, x, y, z, running sums of y: IZPI_CIE_N each
+  __shared__ double d[5 * IZPI_CIE_N];
+  return d;
+}
+IZPI_DEV izpi_material mat_rec(const DevScene& sc, bool st, uint32_t m) {
+  if (st) return lds_ld(mat_lds() + m);
+  return sc.materials[m];
+}
+IZPI_DEV izpi_texture tex_rec(const DevScene& sc, bool st, int32_t id) {
+  if (st) return lds_ld(tex_lds() + id);
+  return sc.textures[id];
+}
+
 // ======================================================= textures / spectra
 // ImageTxt.Value (image.go:73-101): the nearest texel of a w x h image at (u, v), from
 // its device storage form (TEXF_RGBA or TEXF_GRAY, see TexSlot).
@@ -122,17 +180,17 @@ IZPI_DEV V3 image_rgb(const double* texels, uint64_t off, uint32_t w, uint32_t h
 }
 // texture.Constant / texture.ImageTxt (constant.go:20, image.go:73-101); the device copy
 // of an IMAGE texture has pad0 = its storage format
-IZPI_DEV V3 tex_rgb(const DevScene& sc, int32_t id, double u, double v) {
-  const izpi_texture& t = sc.textures[id];
+IZPI_DEV V3 tex_rgb(const DevScene& sc, int32_t id, double u, double v, bool st = false) {
+  const izpi_texture t = tex_rec(sc, st, id);
   if (t.kind == IZPI_TEX_IMAGE) return image_rgb(sc.texels, t.texel_offset, t.width, t.height, t.pad0, u, v);
   return mk(t.value[0], t.value[1], t.value[2]);
 }
 // A material's texture slot (MatTex): images straight from their texels, other textures
 // through their record
-IZPI_DEV V3 slot_rgb(const DevScene& sc, const TexSlot& s, double u, double v) {
+IZPI_DEV V3 slot_rgb(const DevScene& sc, const TexSlot& s, double u, double v, bool st = false) {
   const uint32_t fmt = s.hf >> 30;
   if (fmt <= TEXF_GRAY) return image_rgb(sc.texels, s.off, s.w, s.hf & 0x3FFFFFFFu, fmt, u, v);
-  return tex_rgb(sc, (int32_t)s.off, u, v);
+  return tex_rgb(sc, (int32_t)s.off, u, v, st);
 }
 IZPI_DEV bool slot_set(const TexSlot& s) { return (s.hf >> 30) != TEXF_NONE; }
 // The materials' texture slots staged in LDS next to their constants (mc_stage): a PBR
@@ -144,17 +202,19 @@ IZPI_DEV MatTex* mt_lds() {
 }
 // Slot k of material m: from LDS when staged (`staged`), else from DevScene::mat_tex.
 IZPI_DEV TexSlot mat_slot(const DevScene& sc, bool staged, uint32_t m, int k) {
-  return staged ? mt_lds()[m].s[k] : sc.mat_tex[m].s[k];
+  if (staged) return lds_ld(&mt_lds()[m].s[k]);
+  return sc.mat_tex[m].s[k];
 }
 // First interval [wl[i], wl[i+1]] of a NON-DECREASING table that holds w, for
 // n >= 2 and wl[0] <= w <= wl[n-1]: i = (first j >= 1 with wl[j] >= w) - 1, which is the interval
 // the reference's linear scan stops at (spectral.go:151-181, spectral_constant.go:88-106):
 // every earlier interval ends below w. ~log2(n) dependent loads instead of up to n.
+template <bool L = false>
 IZPI_DEV uint32_t sorted_interval(const double* wl, uint32_t n, double w) {
   uint32_t lo = 1, hi = n - 1;  // wl[n-1] >= w, so the answer is in [1, n-1]
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (wl[mid] >= w) hi = mid; else lo = mid + 1;
+    if (tld<L>(wl + mid) >= w) hi = mid; else lo = mid + 1;
   }
   return lo - 1;
 }
@@ -200,109 +260,132 @@ IZPI_DEV double tex_spectral_image(const DevScene& sc, const izpi_texture& t, do
 }
 
 // texture.SpectralConstant.Value (spectral_constant.go:65-106); SpectralImage reads (u, v)
-IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda, double u = 0.0, double v = 0.0) {
-  const izpi_texture& t = sc.textures[id];
+// The tabulated SPD lookup of SpectralConstant.Value (spectral_constant.go:88-106) on the
+// table at wl / vl (L: staged in LDS)
+template <bool L>
+IZPI_DEV double tab_value(const double* wl, const double* vl, const izpi_texture& t, double lambda) {
+  const uint32_t n = t.spd_count;
+  if (n == 0) return 0.0;
+  if (lambda < tld<L>(wl)) return tld<L>(vl);
+  if (lambda > tld<L>(wl + n - 1)) return tld<L>(vl + n - 1);
+  if (t.pad0 == 2 && lambda == lambda) {
+    // near-uniform wavelengths (set at upload): the interval's index is guessed from
+    // lambda, its two wavelengths and values load together, and a short walk fixes a
+    // wrong guess, so the result is the scan's interval exactly
+    uint32_t g = 1u + (uint32_t)((lambda - t.value[0]) * t.value[1]);
+    g = g > n - 1 ? n - 1 : g;
+    double w1 = tld<L>(wl + g - 1), w2 = tld<L>(wl + g), v1 = tld<L>(vl + g - 1), v2 = tld<L>(vl + g);
+    if (!((g == 1 || w1 < lambda) && w2 >= lambda)) {
+      while (g > 1 && tld<L>(wl + g - 1) >= lambda) g--;
+      while (tld<L>(wl + g) < lambda) g++;
+      w1 = tld<L>(wl + g - 1); w2 = tld<L>(wl + g); v1 = tld<L>(vl + g - 1); v2 = tld<L>(vl + g);
+    }
+    const double tt = (lambda - w1) / (w2 - w1);
+    return v1 + tt * (v2 - v1);
+  }
+  if (t.pad0 && lambda == lambda) {  // pad0: wavelengths non-decreasing (set at upload)
+    const uint32_t i = sorted_interval<L>(wl, n, lambda);
+    const double w1 = tld<L>(wl + i), w2 = tld<L>(wl + i + 1);
+    const double tt = (lambda - w1) / (w2 - w1);
+    return tld<L>(vl + i) + tt * (tld<L>(vl + i + 1) - tld<L>(vl + i));
+  }
+  for (uint32_t i = 0; i + 1 < n; i++) {
+    double w1 = tld<L>(wl + i), w2 = tld<L>(wl + i + 1);
+    if (lambda >= w1 && lambda <= w2) {
+      double tt = (lambda - w1) / (w2 - w1);
+      return tld<L>(vl + i) + tt * (tld<L>(vl + i + 1) - tld<L>(vl + i));
+    }
+  }
+  return 0.0;
+}
+IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda, double u = 0.0, double v = 0.0, bool st = false) {
+  const izpi_texture t = tex_rec(sc, st, id);
   if (t.kind == IZPI_TEX_SPECTRAL_IMAGE) return tex_spectral_image(sc, t, u, v, lambda);
   if (t.kind == IZPI_TEX_SPECTRAL_TABULATED) {
-    const double* wl = sc.spd_wl + t.spd_offset;
-    const double* vl = sc.spd_val + t.spd_offset;
-    uint32_t n = t.spd_count;
-    if (n == 0) return 0.0;
-    if (lambda < wl[0]) return vl[0];
-    if (lambda > wl[n - 1]) return vl[n - 1];
-    if (t.pad0 == 2 && lambda == lambda) {
-      // near-uniform wavelengths (set at upload): the interval's index is guessed from
-      // lambda, its two wavelengths and values load together, and a short walk fixes a
-      // wrong guess, so the result is the scan's interval exactly
-      uint32_t g = 1u + (uint32_t)((lambda - t.value[0]) * t.value[1]);
-      g = g > n - 1 ? n - 1 : g;
-      double w1 = wl[g - 1], w2 = wl[g], v1 = vl[g - 1], v2 = vl[g];
-      if (!((g == 1 || w1 < lambda) && w2 >= lambda)) {
-        while (g > 1 && wl[g - 1] >= lambda) g--;
-        while (wl[g] < lambda) g++;
-        w1 = wl[g - 1]; w2 = wl[g]; v1 = vl[g - 1]; v2 = vl[g];
-      }
-      const double tt = (lambda - w1) / (w2 - w1);
-      return v1 + tt * (v2 - v1);
-    }
-    if (t.pad0 && lambda == lambda) {  // pad0: wavelengths non-decreasing (set at upload)
-      const uint32_t i = sorted_interval(wl, n, lambda);
-      const double w1 = wl[i], w2 = wl[i + 1];
-      const double tt = (lambda - w1) / (w2 - w1);
-      return vl[i] + tt * (vl[i + 1] - vl[i]);
-    }
-    for (uint32_t i = 0; i + 1 < n; i++) {
-      double w1 = wl[i], w2 = wl[i + 1];
-      if (lambda >= w1 && lambda <= w2) {
-        double tt = (lambda - w1) / (w2 - w1);
-        return vl[i] + tt * (vl[i + 1] - vl[i]);
-      }
-    }
-    return 0.0;
+    if (st) return tab_value<true>(spd_lds() + t.spd_offset, spd_lds() + SPD_LDS + t.spd_offset, t, lambda);
+    return tab_value<false>(sc.spd_wl + t.spd_offset, sc.spd_val + t.spd_offset, t, lambda);
   }
   double exponent = -gm::pow((lambda - t.center) / t.width_nm, 2);
   return t.peak * gm::exp(exponent);
 }
 // SpectralPowerDistribution.Value (spectral.go:151-181)
+template <bool L = false>
 IZPI_DEV double spd_value(const double* wl, const double* vl, uint32_t n, double w, bool sorted = false) {
   if (n == 0) return 0.0;
-  if (w <= wl[0]) return vl[0];
-  if (w >= wl[n - 1]) return vl[n - 1];
+  if (w <= tld<L>(wl)) return tld<L>(vl);
+  if (w >= tld<L>(wl + n - 1)) return tld<L>(vl + n - 1);
   if (sorted && w == w) {  // (NaN falls through to the scan, which matches no interval)
-    const uint32_t i = sorted_interval(wl, n, w);
-    const double w1 = wl[i], w2 = wl[i + 1];
+    const uint32_t i = sorted_interval<L>(wl, n, w);
+    const double w1 = tld<L>(wl + i), w2 = tld<L>(wl + i + 1);
     const double t = (w - w1) / (w2 - w1);
-    return vl[i] + t * (vl[i + 1] - vl[i]);
+    return tld<L>(vl + i) + t * (tld<L>(vl + i + 1) - tld<L>(vl + i));
   }
   for (uint32_t i = 0; i + 1 < n; i++) {
-    double w1 = wl[i], w2 = wl[i + 1];
+    double w1 = tld<L>(wl + i), w2 = tld<L>(wl + i + 1);
     if (w >= w1 && w <= w2) {
       double t = (w - w1) / (w2 - w1);
-      return vl[i] + t * (vl[i + 1] - vl[i]);
+      return tld<L>(vl + i) + t * (tld<L>(vl + i + 1) - tld<L>(vl + i));
     }
   }
   return 0.0;
 }
 // spectral.SampleWavelength (spectral.go:184-224): the scan stops at the first i whose
 // running sum reaches the target (y >= 0, so the sums never decrease): bisected.
+// The CIE tables: __constant__ memory, or the block's LDS copy (L; shade_stage)
+template <bool L>
+struct Cie {
+  IZPI_DEV static const double* wl() { return L ? cie_lds() : c_cie_wl; }
+  IZPI_DEV static const double* x() { return L ? cie_lds() + IZPI_CIE_N : c_cie_x; }
+  IZPI_DEV static const double* y() { return L ? cie_lds() + 2 * IZPI_CIE_N : c_cie_y; }
+  IZPI_DEV static const double* z() { return L ? cie_lds() + 3 * IZPI_CIE_N : c_cie_z; }
+  IZPI_DEV static const double* ycum() { return L ? cie_lds() + 4 * IZPI_CIE_N : c_cie_ycum.v; }
+};
+template <bool L = false>
 IZPI_DEV void sample_wavelength(double random, double& lambda, double& pdf) {
+  using C = Cie<L>;
   const double target = random * IZPI_CIE_Y_INTEGRAL;
-  const double* cum = c_cie_ycum.v;
-  if (!(cum[IZPI_CIE_N - 1] >= target)) {  // the scan ran off the end
+  const double* cum = C::ycum();
+  if (!(tld<L>(cum + IZPI_CIE_N - 1) >= target)) {  // the scan ran off the end
     lambda = 750;
-    pdf = c_cie_y[IZPI_CIE_N - 1] / IZPI_CIE_Y_INTEGRAL;
+    pdf = tld<L>(C::y() + IZPI_CIE_N - 1) / IZPI_CIE_Y_INTEGRAL;
     return;
   }
   uint32_t lo = 0, hi = IZPI_CIE_N - 1;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (cum[mid] >= target) hi = mid; else lo = mid + 1;
+    if (tld<L>(cum + mid) >= target) hi = mid; else lo = mid + 1;
   }
   const uint32_t i = lo;
-  const double y = c_cie_y[i];
+  const double y = tld<L>(C::y() + i);
   if (i > 0) {
-    const double prev = cum[i - 1];
+    const double prev = tld<L>(cum + i - 1);
     const double t = (target - prev) / y;
-    lambda = c_cie_wl[i - 1] + t * (c_cie_wl[i] - c_cie_wl[i - 1]);
-    const double iy = c_cie_y[i - 1] + t * (c_cie_y[i] - c_cie_y[i - 1]);
+    lambda = tld<L>(C::wl() + i - 1) + t * (tld<L>(C::wl() + i) - tld<L>(C::wl() + i - 1));
+    const double iy = tld<L>(C::y() + i - 1) + t * (tld<L>(C::y() + i) - tld<L>(C::y() + i - 1));
     pdf = iy / IZPI_CIE_Y_INTEGRAL;
     return;
   }
-  lambda = c_cie_wl[i];
+  lambda = tld<L>(C::wl() + i);
   pdf = y / IZPI_CIE_Y_INTEGRAL;
 }
 // spectral.GetCIEValues (spectral.go:227-253); the index scan over the ascending CIE
 // wavelengths is bisected (sorted_interval returns index - 1)
+template <bool L = false>
 IZPI_DEV void cie_values(double w, double& x, double& y, double& z) {
-  if (w <= c_cie_wl[0]) { x = c_cie_x[0]; y = c_cie_y[0]; z = c_cie_z[0]; return; }
-  if (w >= c_cie_wl[IZPI_CIE_N - 1]) { x = c_cie_x[IZPI_CIE_N - 1]; y = c_cie_y[IZPI_CIE_N - 1]; z = c_cie_z[IZPI_CIE_N - 1]; return; }
+  using C = Cie<L>;
+  const double *W = C::wl(), *X = C::x(), *Y = C::y(), *Z = C::z();
+  if (w <= tld<L>(W)) { x = tld<L>(X); y = tld<L>(Y); z = tld<L>(Z); return; }
+  if (w >= tld<L>(W + IZPI_CIE_N - 1)) {
+    x = tld<L>(X + IZPI_CIE_N - 1); y = tld<L>(Y + IZPI_CIE_N - 1); z = tld<L>(Z + IZPI_CIE_N - 1);
+    return;
+  }
   int index = 0;
-  if (w == w) index = (int)sorted_interval(c_cie_wl, IZPI_CIE_N, w) + 1;
-  double w1 = c_cie_wl[index - 1], w2 = c_cie_wl[index];
+  if (w == w) index = (int)sorted_interval<L>(W, IZPI_CIE_N, w) + 1;
+  double w1 = tld<L>(W + index - 1), w2 = tld<L>(W + index);
   double t = (w - w1) / (w2 - w1);
-  x = c_cie_x[index - 1] + t * (c_cie_x[index] - c_cie_x[index - 1]);
-  y = c_cie_y[index - 1] + t * (c_cie_y[index] - c_cie_y[index - 1]);
-  z = c_cie_z[index - 1] + t * (c_cie_z[index] - c_cie_z[index - 1]);
+  x = tld<L>(X + index - 1) + t * (tld<L>(X + index) - tld<L>(X + index - 1));
+  y = tld<L>(Y + index - 1) + t * (tld<L>(Y + index) - tld<L>(Y + index - 1));
+  z = tld<L>(Z + index - 1) + t * (tld<L>(Z + index) - tld<L>(Z + index - 1));
 }
 
 // ============================================================ wavefront state
@@ -920,7 +1003,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
     if (gs_kind(gs) == IZPI_MAT_PBR) {
       const TexSlot ns = mat_slot(sc, mt_staged, h.mat, 1);
       if (slot_set(ns)) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
-        V3 nts = slot_rgb(sc, ns, h.u, h.v);
+        V3 nts = slot_rgb(sc, ns, h.u, h.v, mt_staged);
         h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
         h.nraw_ok = true;
         nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
@@ -975,15 +1058,15 @@ IZPI_DEV void light_pack(const GLight& L, uint32_t k, double* out) {  // k = 0..
   out[k] = v;
 }
 // HitableSlice.PDFValue over Scene.Lights (hitable_slice.go:98-105) from the packed
-// records (LDS when staged, else `glob`, packed the same way on the fly).
-IZPI_DEV double lights_pdf(const DevScene& sc, const double* lds, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
+// records (LDS when staged, else packed the same way on the fly from the GLight records).
+IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
   const double weight = 1.0 / (double)sc.num_lights;
   double sum = 0;
   for (uint32_t i = 0; i < sc.num_lights; i++) {
     double r[16];
-    if (lds) {
+    if (staged) {
 #pragma unroll
-      for (int k = 0; k < 16; k++) r[k] = lds[i * 16 + k];
+      for (int k = 0; k < 16; k++) r[k] = lds_ld(lt_lds() + i * 16 + k);
     } else {
 #pragma unroll
       for (int k = 0; k < 16; k++) light_pack(sc.lights[i], k, r);
@@ -1091,8 +1174,8 @@ struct ShadeParams {
   double* recs;                // [slots][rec_dense][D] unwinding records
   double* pool;                // [blocks][rec_pool][D] overflow unwinding records
   const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
-  uint32_t num_mc, mc_in_lds;  // materials; mat_const staged in LDS (num_mc <= MC_LDS, mc_stage)
-  uint32_t lt_in_lds;          // the lights' PDFValue records staged in LDS (num_lights <= LT_LDS, mc_stage)
+  uint32_t num_mc, num_tex, num_spd;  // materials, textures, SPD table entries of the scene
+  uint32_t staged;             // the scene's small tables are staged in LDS per block (shade_stage)
   uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
@@ -1176,16 +1259,34 @@ IZPI_DEV double4* mc_lds() {
   __shared__ double4 c[MC_LDS];
   return c;
 }
-IZPI_DEV void mc_stage(const DevScene& sc, const ShadeParams& sp) {
-  if (sp.mc_in_lds) {
-    if (threadIdx.x < sp.num_mc) mc_lds()[threadIdx.x] = sp.mat_const[threadIdx.x];
-    for (uint32_t t = threadIdx.x; t < 4 * sp.num_mc; t += blockDim.x) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
+// Copy the scene's small tables into this block's LDS (ShadeParams::staged): the
+// materials' constant colours and texture slots, the lights' PDFValue records, the
+// material and texture records, the tabulated SPDs, the background SPD, the CIE tables.
+IZPI_DEV void shade_stage(const DevScene& sc, const ShadeParams& sp) {
+  if (sp.staged) {
+    const uint32_t t0 = threadIdx.x, nt = blockDim.x;
+    for (uint32_t t = t0; t < sp.num_mc; t += nt) mc_lds()[t] = sp.mat_const[t];
+    for (uint32_t t = t0; t < 4 * sp.num_mc; t += nt) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
+    for (uint32_t t = t0; t < 16 * sc.num_lights; t += nt) light_pack(sc.lights[t >> 4], t & 15, lt_lds() + (t & ~15u));
+    constexpr uint32_t MW = sizeof(izpi_material) / 8, TW = sizeof(izpi_texture) / 8;
+    for (uint32_t t = t0; t < MW * sp.num_mc; t += nt)
+      reinterpret_cast<uint64_t*>(mat_lds())[t] = reinterpret_cast<const uint64_t*>(sc.materials)[t];
+    for (uint32_t t = t0; t < TW * sp.num_tex; t += nt)
+      reinterpret_cast<uint64_t*>(tex_lds())[t] = reinterpret_cast<const uint64_t*>(sc.textures)[t];
+    for (uint32_t t = t0; t < sp.num_spd; t += nt) { spd_lds()[t] = sc.spd_wl[t]; spd_lds()[SPD_LDS + t] = sc.spd_val[t]; }
+    for (uint32_t t = t0; t < sp.num_bg_spd; t += nt) { bg_lds()[t] = sp.bg_wl[t]; bg_lds()[BG_LDS + t] = sp.bg_val[t]; }
+    for (uint32_t t = t0; t < IZPI_CIE_N; t += nt) {
+      double* c = cie_lds();
+      c[t] = c_cie_wl[t]; c[IZPI_CIE_N + t] = c_cie_x[t]; c[2 * IZPI_CIE_N + t] = c_cie_y[t];
+      c[3 * IZPI_CIE_N + t] = c_cie_z[t]; c[4 * IZPI_CIE_N + t] = c_cie_ycum.v[t];
+    }
   }
-  if (sp.lt_in_lds)
-    for (uint32_t t = threadIdx.x; t < 16 * sc.num_lights; t += blockDim.x) light_pack(sc.lights[t >> 4], t & 15, lt_lds() + (t & ~15u));
   __syncthreads();
 }
-IZPI_DEV double4 mat_const_of(const ShadeParams& sp, uint32_t m) { return sp.mc_in_lds ? mc_lds()[m] : sp.mat_const[m]; }
+IZPI_DEV double4 mat_const_of(const ShadeParams& sp, uint32_t m) {
+  if (sp.staged) return lds_ld(&mc_lds()[m]);
+  return sp.mat_const[m];
+}
 
 // Result slot of work unit `unit` (= pixel * chunk_spp + sample). Unit-major: paths of
 // neighbouring units finish close in time and fill whole lines (a sample-major layout
@@ -1294,16 +1395,22 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
     out[0] = c.x; out[1] = c.y; out[2] = c.z;
   } else {
     double cx, cy, cz;  // render/spectral.go:162-166
-    cie_values(P.lambda, cx, cy, cz);
+    if (sp.staged) cie_values<true>(P.lambda, cx, cy, cz);
+    else cie_values<false>(P.lambda, cx, cy, cz);
     out[0] = (L.x * cx) / P.lpdf;
     out[1] = (L.x * cy) / P.lpdf;
     out[2] = (L.x * cz) / P.lpdf;
   }
 }
 
+// The background SPD at lambda (sampler/spectral.go:48-51,79), staged or not
+IZPI_DEV double bg_value(const ShadeParams& sp, double lambda) {
+  if (sp.staged) return spd_value<true>(bg_lds(), bg_lds() + BG_LDS, sp.num_bg_spd, lambda, sp.bg_sorted != 0);
+  return spd_value<false>(sp.bg_wl, sp.bg_val, sp.num_bg_spd, lambda, sp.bg_sorted != 0);
+}
 IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colour) {
   // colour.go:34-36 returns blue; sampler/spectral.go:48-51 the background SPD.
-  return colour ? mk(0, 0, 1.0) : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda, sp.bg_sorted != 0), 0, 0);
+  return colour ? mk(0, 0, 1.0) : mk(bg_value(sp, P.lambda), 0, 0);
 }
 
 // Start the path of work unit `unit`: per-sample LCG streams, wavelength (spectral),
@@ -1329,7 +1436,9 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
   P.lambda = 0;
   P.lpdf = 1;
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) {
-    sample_wavelength(rng.next(), P.lambda, P.lpdf);
+    const double r = rng.next();
+    if (sp.staged) sample_wavelength<true>(r, P.lambda, P.lpdf);
+    else sample_wavelength<false>(r, P.lambda, P.lpdf);
     if (P.lpdf == 0) {  // render/spectral.go:78-80: skipped, still counted in 1/spp
       double* out = sample_out(sp, unit);
       out[0] = 0; out[1] = 0; out[2] = 0;
@@ -1426,7 +1535,9 @@ IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
 // serialises ~88 atomics/us), then further units from the head while its path needs no
 // tracing; the path goes to entry j of `out`.
 template <int SAMPLER>
-__global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+__global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp_in, const WaveParams wp) {
+  ShadeParams sp = sp_in;
+  sp.staged = 0;  // k_start stages no tables: its path starts read them from global memory
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   bool want = j < sp.slots;
   bool push = false;
@@ -1573,6 +1684,7 @@ template <int SAMPLER, int MATSET>
 IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
                          PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt, uint32_t& c_ls) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
+  const bool st = sp.staged != 0;  // the scene's small tables are in this block's LDS
   SCLK_T(sc0);
   {
     const RayOD rh = in.ray[i];
@@ -1607,26 +1719,26 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       if (len > 100.0) len = 100.0;
     }
     const uint32_t mat_id = R.kind >> KIND_MAT_SHIFT;  // dielectric material stashed by the glass bounce
-    const izpi_material& gm_ = sc.materials[mat_id];
+    const izpi_material gm_ = mat_rec(sc, st, mat_id);
     if (COLOUR) att = mk(gm::exp(-gm_.rgb[0] * len), gm::exp(-gm_.rgb[1] * len), gm::exp(-gm_.rgb[2] * len));
-    else att.x = gm_.absorb_tex >= 0 ? gm::exp(-tex_spectral(sc, gm_.absorb_tex, P.lambda) * len) : 1.0;
+    else att.x = gm_.absorb_tex >= 0 ? gm::exp(-tex_spectral(sc, gm_.absorb_tex, P.lambda, 0.0, 0.0, st) * len) : 1.0;
     spec = true;
     next_o = hp;
     next_d = rd;
   } else if (H.prim < 0) {
     L = COLOUR ? mk(sp.background[0], sp.background[1], sp.background[2])
-               : mk(spd_value(sp.bg_wl, sp.bg_val, sp.num_bg_spd, P.lambda, sp.bg_sorted != 0), 0, 0);
+               : mk(bg_value(sp, P.lambda), 0, 0);
     terminal = true;
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, sp.mc_in_lds != 0);
+    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st);
     hit_n = h.n;
     rec_mat = h.mat;
     next_o = h.p;
     // the shade record carries the material kind and, for a constant RGB texture, its
     // value: the common Lambert/light hit reads no material or texture record
-    const izpi_material& m = sc.materials[h.mat];
+    const izpi_material m = mat_rec(sc, st, h.mat);
     const bool cconst = COLOUR && (gs_cflags(gs) & 1u) != 0;
     V3 cval = mk(0, 0, 0);
     if (cconst) { const double4 c4 = mat_const_of(sp, h.mat); cval = mk(c4.x, c4.y, c4.z); }
@@ -1634,8 +1746,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       case IZPI_MAT_DIFFUSE_LIGHT: {  // no scatter: return emitted (diffuselight.go:49-63)
         if (dot(h.n, rd) < 0.0) {
           if (cconst) L = cval;
-          else if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-          else L.x = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
+          else if (COLOUR) L = tex_rgb(sc, m.albedo_tex, h.u, h.v, st);
+          else L.x = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v, st);
         }
         terminal = true;
         break;
@@ -1645,8 +1757,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         rng.next();
         cos_onb.build(h.n);
         if (cconst) att = cval;
-        else if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v);
-        else att.x = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
+        else if (COLOUR) att = tex_rgb(sc, m.albedo_tex, h.u, h.v, st);
+        else att.x = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v, st);
         have_pdf = true;
         break;
       }
@@ -1655,7 +1767,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         if constexpr (!ms_has(MATSET, MS_ISO)) { atomicOr(sp.error, 2u); terminal = true; break; }
         (void)random_in_unit_sphere(rng);
         cos_onb.build(h.n);
-        const V3 a = tex_rgb(sc, m.albedo_tex, h.u, h.v);
+        const V3 a = tex_rgb(sc, m.albedo_tex, h.u, h.v, st);
         if (COLOUR) att = a; else att.x = a.x;
         have_pdf = true;
         zero_spdf = true;
@@ -1663,7 +1775,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       }
       case IZPI_MAT_DIELECTRIC: {  // dielectric.go:156-207
         if constexpr (!ms_has(MATSET, MS_DIEL)) { atomicOr(sp.error, 2u); terminal = true; break; }
-        const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda);
+        const double ri = COLOUR ? m.ref_idx : tex_spectral(sc, m.spectral_tex, P.lambda, 0.0, 0.0, st);
         bool reflected;
         next_d = dielectric_scatter(rd, h.n, ri, rng, reflected);
         const bool beer_rgb = COLOUR && (m.flags & IZPI_MATF_BEER_LAMBERT) && !(m.rgb[0] == 0 && m.rgb[1] == 0 && m.rgb[2] == 0);
@@ -1695,18 +1807,17 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         if constexpr (!ms_has(MATSET, MS_PBR)) { atomicOr(sp.error, 2u); terminal = true; break; }
         // the four texture slots (LDS, or one 64-B record); every lookup below is issued
         // before the first of them is used
-        const bool stg = sp.mc_in_lds != 0;
-        const TexSlot s_alb = mat_slot(sc, stg, h.mat, 0), s_nrm = mat_slot(sc, stg, h.mat, 1),
-                      s_rgh = mat_slot(sc, stg, h.mat, 2), s_met = mat_slot(sc, stg, h.mat, 3);
+        const TexSlot s_alb = mat_slot(sc, st, h.mat, 0), s_nrm = mat_slot(sc, st, h.mat, 1),
+                      s_rgh = mat_slot(sc, st, h.mat, 2), s_met = mat_slot(sc, st, h.mat, 3);
         double alb_s = 0;
-        if (COLOUR) att = slot_rgb(sc, s_alb, h.u, h.v);
-        else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v);
-        else { V3 c = slot_rgb(sc, s_alb, h.u, h.v); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
-        V3 rough = slot_set(s_rgh) ? slot_rgb(sc, s_rgh, h.u, h.v) : mk(0.5, 0.5, 0.5);
-        V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v) : mk(0.0, 0.0, 0.0);
+        if (COLOUR) att = slot_rgb(sc, s_alb, h.u, h.v, st);
+        else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v, st);
+        else { V3 c = slot_rgb(sc, s_alb, h.u, h.v, st); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
+        V3 rough = slot_set(s_rgh) ? slot_rgb(sc, s_rgh, h.u, h.v, st) : mk(0.5, 0.5, 0.5);
+        V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v, st) : mk(0.0, 0.0, 0.0);
         V3 normal = h.n;
         if (slot_set(s_nrm)) {
-          V3 nuv = h.nraw_ok ? h.nraw : slot_rgb(sc, s_nrm, h.u, h.v);
+          V3 nuv = h.nraw_ok ? h.nraw : slot_rgb(sc, s_nrm, h.u, h.v, st);
           V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
           V3 nn0 = h.n;
           V3 t = cross(nn0, mk(0, 1, 0));
@@ -1771,7 +1882,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         const double spdf = zero_spdf ? 0.0 : sc_cos / 3.141592653589793;  // Isotropic.ScatteringPDF is 0
         rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, spdf, rec_mat);
         SCLK_T(sc3);
-        const double pdf_val = 0.5 * lights_pdf(sc, sp.lt_in_lds ? lt_lds() : nullptr, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
+        const double pdf_val = 0.5 * lights_pdf(sc, st, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         SCLK_ADD(SCLK_LPDF, sc3);
         rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
         next_d = dir;
@@ -1858,7 +1969,7 @@ template <int SAMPLER, int MATSET>
 __global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
-  mc_stage(sc, sp);
+  shade_stage(sc, sp);
   uint32_t parity = 0;  // block_reserve2 LDS buffer set
   const uint32_t n = *wp.in_count;
   // this pass's k_trace2 is done with its dequeue cursor: reset it for the next pass's
@@ -1946,7 +2057,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 // Same per-ray code paths, results and counters as k_trace + k_shade.
 template <int SAMPLER, int MATSET, int STACK>
 __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
-  mc_stage(sc, sp);
+  shade_stage(sc, sp);
   __shared__ int32_t lds_stack[STACK * 256];
   int32_t* stk = lds_stack + threadIdx.x;
   const uint32_t n = *wp.in_count;
@@ -2279,6 +2390,7 @@ struct izpi_ctx {
   bool have_scene = false;
   uint32_t num_textures = 0;     // of the uploaded scene (izpi_gpu_gomath texture lookups)
   uint32_t num_materials = 0;    // of the uploaded scene
+  uint32_t num_spd = 0;          // tabulated SPD entries of the uploaded scene
   // The workspace sizing of the last render and what it was decided for (render_impl): a
   // request of the same shape reuses it, so frames of one renderer never re-size (sizing
   // from the free HBM of each frame made C4 reallocate its 148 GB every frame, 2 s each).
@@ -2834,13 +2946,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.pool_shift = 0;
   while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
   sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = misc(ctx, 0);
-  sp.num_mc = ctx->num_materials; sp.mc_in_lds = ctx->num_materials <= MC_LDS ? 1u : 0u;
-  sp.lt_in_lds = sc.num_lights <= LT_LDS ? 1u : 0u;
-#ifdef IZPI_NO_LT_LDS
-  sp.lt_in_lds = 0;  // A/B builds
-#endif
-#ifdef IZPI_NO_MC_LDS
-  sp.mc_in_lds = 0;  // A/B builds
+  sp.num_mc = ctx->num_materials; sp.num_tex = ctx->num_textures; sp.num_spd = ctx->num_spd;
+  sp.staged = ctx->num_materials <= MC_LDS && ctx->num_materials <= MAT_LDS && sc.num_lights <= LT_LDS &&
+              ctx->num_textures <= TEX_LDS && ctx->num_spd <= SPD_LDS && nbg <= BG_LDS;
+#ifdef IZPI_NO_STAGING
+  sp.staged = 0;  // A/B builds
 #endif
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
@@ -3383,6 +3493,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   ctx->sizing_valid = false;  // per-slot sizes depend on the scene
   ctx->num_textures = d->num_textures;
   ctx->num_materials = d->num_materials;
+  ctx->num_spd = d->num_spd;
   return IZPI_OK;
 }
 
