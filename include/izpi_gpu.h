@@ -213,14 +213,18 @@ int izpi_gpu_postprocess(izpi_ctx* ctx, double* canvas_dev, uint32_t width, uint
 
 /* GPU BVH4 builder: Morton codes and a radix sort, then a binary
  * tree (method: IZPI_BVH_PLOC clustering or IZPI_BVH_LBVH radix tree), collapsed to
- * 4-wide nodes with collectChildren's rule and <= leaf_max (1..4) primitives per leaf, written in the reference's BVH4Node
+ * 4-wide nodes with collectChildren's rule (or, with IZPI_BVH_SAH, the collapse of least
+ * surface-area cost) and <= leaf_max (1..4) primitives per leaf, written in the reference's BVH4Node
  * format (conservative f32 bounds, separate leaf nodes), breadth-first with the root at
  * 0. boxes: [n][6] f64 host array (izpi_host_scene_prim_boxes). nodes: host array of at
  * least 2n entries; order[k] (n entries) = input index of leaf position k. The topology
  * differs from hitable.NewBVH4's, so images match the reference tree's except for
  * equal-t tie-breaks and f32 culling at tMax. */
 enum { IZPI_BVH_LBVH = 0, /* Karras radix tree over the Morton order */
-       IZPI_BVH_PLOC = 1  /* locally-ordered clustering (Meister & Bittner 2018) over the Morton order */ };
+       IZPI_BVH_PLOC = 1, /* locally-ordered clustering (Meister & Bittner 2018) over the Morton order */
+       /* flag (PLOC only): collapse to 4-wide nodes by the surface-area cost model's
+        * dynamic programme instead of collectChildren's rule; leaves still hold <= leaf_max */
+       IZPI_BVH_SAH = 0x100 };
 int izpi_gpu_build_bvh4(izpi_ctx* ctx, const double* boxes, uint32_t n, uint32_t leaf_max, uint32_t method,
                         izpi_bvh4_node* nodes, uint32_t max_nodes, uint32_t* num_nodes, uint32_t* order, double* build_ms);
 

@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
     uint32_t num_nodes = 0;
     double ms = 0;
     if (izpi_host_scene_prim_boxes(host, boxes)) return fail("izpi_host_scene_prim_boxes", izpi_host_last_error());
-    if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC, nodes, 2 * np, &num_nodes, order, &ms))
+    if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes, 2 * np, &num_nodes, order, &ms))
       return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
     if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
     free(boxes); free(nodes); free(order);

@@ -174,7 +174,7 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 		var ms C.double
 		if n > 0 {
 			C.izpi_host_scene_prim_boxes(r.host, (*C.double)(unsafe.Pointer(&boxes[0])))
-			if rc := C.izpi_gpu_build_bvh4(r.ctx, (*C.double)(unsafe.Pointer(&boxes[0])), C.uint32_t(n), C.izpi_host_bvh_leaf_max(desc), C.IZPI_BVH_PLOC,
+			if rc := C.izpi_gpu_build_bvh4(r.ctx, (*C.double)(unsafe.Pointer(&boxes[0])), C.uint32_t(n), C.izpi_host_bvh_leaf_max(desc), C.IZPI_BVH_PLOC|C.IZPI_BVH_SAH,
 				&nodes[0], C.uint32_t(len(nodes)), &numNodes, (*C.uint32_t)(unsafe.Pointer(&order[0])), &ms); rc != 0 {
 				return nil, r.deviceError("izpi_gpu_build_bvh4", rc)
 			}

@@ -29,6 +29,8 @@ FILTER_GAMMA, FILTER_CLAMP = 1, 2
 MAX_FILTERS = 8
 HOST_SKIP_BVH = 1
 BVH_LBVH, BVH_PLOC = 0, 1
+BVH_SAH = 0x100  # flag: collapse by the surface-area cost model (PLOC only)
+BVH_PLOC_SAH = BVH_PLOC | BVH_SAH
 
 
 def prim_ref(kind, idx):

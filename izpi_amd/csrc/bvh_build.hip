@@ -291,15 +291,72 @@ __global__ void k_ploc_offsets(uint32_t total, const int32_t* pl, const int32_t*
   off[id] = o;
 }
 
+// SAH-optimal collapse (the dynamic programme of Ylitie, Karras & Laine 2017 for 4-wide
+// nodes): for every binary node n and i = 1..4, D(n, i) is the least SAH cost of covering
+// n's subtree with at most i child slots of the wide node above it. A slot is either a
+// leaf (<= leaf_max primitives: a leaf-node visit plus its primitive tests) or a wide node
+// (one node visit plus the best split of its two binary children over 4 slots). Costs
+// are weighted by surface area; the collapse then follows the recorded decisions instead
+// of collectChildren's greedy expansion. dec bits: 0 = the single slot is a leaf, 1-2 =
+// the wide node's split (k slots on the left), 3-4 / 5-6 / 7-8 = the split for i = 2 / 3 / 4
+// (0: use i - 1 slots).
+#ifndef IZPI_SAH_CN
+#define IZPI_SAH_CN 1.0   // visit of a wide node (one node step)
+#endif
+#ifndef IZPI_SAH_CL
+#define IZPI_SAH_CL 0.5   // visit of a leaf node (often skipped by the traversal's leaf shortcut)
+#endif
+#ifndef IZPI_SAH_CT
+#define IZPI_SAH_CT 1.0   // one primitive test
+#endif
+__global__ void k_sah_leaves(uint32_t n, const Box6* pbox, double4* dcost, uint16_t* dec) {
+  const uint32_t id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= n) return;
+  const double c = half_area(pbox[id]) * (IZPI_SAH_CL + IZPI_SAH_CT);
+  dcost[id] = make_double4(c, c, c, c);
+  dec[id] = 1;
+}
+// Nodes created by one PLOC iteration, ids [b0, b0 + cnt): their children are older.
+__global__ void k_sah_level(uint32_t b0, uint32_t cnt, const int32_t* pl, const int32_t* pr, const Box6* pbox,
+                            const uint32_t* psize, uint32_t leaf_max, double4* dcost, uint16_t* dec) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= cnt) return;
+  const uint32_t id = b0 + k;
+  const double4 l4 = dcost[pl[id]], r4 = dcost[pr[id]];
+  const double L[5] = {0, l4.x, l4.y, l4.z, l4.w}, R[5] = {0, r4.x, r4.y, r4.z, r4.w};
+  const double area = half_area(pbox[id]);
+  double best4 = L[1] + R[3];
+  uint32_t k4 = 1;
+  for (uint32_t j = 2; j <= 3; j++)
+    if (L[j] + R[4 - j] < best4) { best4 = L[j] + R[4 - j]; k4 = j; }
+  double d[5];
+  d[1] = area * IZPI_SAH_CN + best4;
+  uint32_t bits = k4 << 1;
+  if (psize[id] <= leaf_max) {
+    const double lc = area * (IZPI_SAH_CL + IZPI_SAH_CT * (double)psize[id]);
+    if (lc <= d[1]) { d[1] = lc; bits |= 1u; }
+  }
+  for (uint32_t i = 2; i <= 4; i++) {
+    d[i] = d[i - 1];
+    uint32_t ki = 0;
+    for (uint32_t j = 1; j < i; j++)
+      if (L[j] + R[i - j] < d[i]) { d[i] = L[j] + R[i - j]; ki = j; }
+    bits |= ki << (1 + 2 * (i - 1));
+  }
+  dcost[id] = make_double4(d[1], d[2], d[3], d[4]);
+  dec[id] = (uint16_t)bits;
+}
+
 // To the layout the collapse reads (Karras' numbering): internal node k -> 2n-2-k (the
 // root, created last, becomes 0), leaf p -> n-1+DFS position; leaf order from the DFS.
 __global__ void k_ploc_to_tree(uint32_t n, const int32_t* pl, const int32_t* pr, const Box6* pbox, const uint32_t* psize,
                                const uint32_t* off, const uint32_t* ids_s, int32_t* left, int32_t* right, int32_t* first,
-                               int32_t* last, Box6* nb, uint32_t* order) {
+                               int32_t* last, Box6* nb, uint32_t* order, const uint16_t* dec, uint16_t* dec_t) {
   const uint32_t id = blockIdx.x * 256 + threadIdx.x;
   if (id >= 2 * n - 1) return;
   const int nn1 = (int)n - 1;
   auto map = [&](int32_t x) { return x < (int32_t)n ? nn1 + (int32_t)off[x] : (int32_t)(2 * n - 2) - x; };
+  if (dec) dec_t[map((int32_t)id)] = dec[id];
   if (id < n) {
     nb[nn1 + off[id]] = pbox[id];
     order[off[id]] = ids_s[id];
@@ -321,15 +378,39 @@ struct Tree {
   const Box6* box;
   int n;
   int leaf_max;
+  const uint16_t* dec;  // SAH collapse decisions (k_sah_level), or null: collectChildren's rule
   __device__ int size(int b) const { return b >= n - 1 ? 1 : last[b] - first[b] + 1; }
   __device__ int start(int b) const { return b >= n - 1 ? b - (n - 1) : first[b]; }
-  __device__ bool is_leaf(int b) const { return size(b) <= leaf_max; }
+  __device__ bool is_leaf(int b) const { return dec ? (dec[b] & 1u) != 0 : size(b) <= leaf_max; }
 };
+
+// The wide node b's child slots from the SAH decisions: its split over 4 slots, each side
+// expanded by its own recorded split for the slots it gets, in left-to-right order.
+__device__ int sah_collect(const Tree& t, int b, int* res) {
+  int sn[4], si[4], sp = 0, c = 0;
+  const int k4 = (t.dec[b] >> 1) & 3;
+  sn[sp] = t.right[b]; si[sp++] = 4 - k4;
+  int m = t.left[b], i = k4;
+  for (;;) {
+    const int ki = (i > 1 && t.size(m) > 1) ? (t.dec[m] >> (1 + 2 * (i - 1))) & 3 : 0;
+    if (i > 1 && ki == 0) { i--; continue; }
+    if (i <= 1) {
+      res[c++] = m;
+      if (sp == 0) break;
+      sp--; m = sn[sp]; i = si[sp];
+      continue;
+    }
+    sn[sp] = t.right[m]; si[sp++] = i - ki;
+    m = t.left[m]; i = ki;
+  }
+  return c;
+}
 
 // collectChildren (bvh4.go:796-855) on the binary tree, leaves = subtrees of <= leaf_max.
 // Where the reference expands the first inner child, this expands the one with the
 // largest surface area (measured: 7% fewer node visits on C3's mesh).
 __device__ int collect(const Tree& t, int b, int* res) {
+  if (t.dec) return sah_collect(t, b, res);
   int c = 0;
   res[c++] = t.left[b];
   res[c++] = t.right[b];
@@ -436,7 +517,10 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
   if (n == 0) return IZPI_OK;
   if (leaf_max < 1 || leaf_max > 4) { err = "leaf_max must be 1..4 (bvh4.go:638)"; return IZPI_ERR_INVALID; }
   if (n > (1u << 27)) { err = "too many primitives for the leaf-ref encoding"; return IZPI_ERR_UNSUPPORTED; }
+  const bool sah = (method & IZPI_BVH_SAH) != 0;
+  method &= ~(uint32_t)IZPI_BVH_SAH;
   if (method != IZPI_BVH_LBVH && method != IZPI_BVH_PLOC) { err = "unknown BVH build method"; return IZPI_ERR_INVALID; }
+  if (sah && method != IZPI_BVH_PLOC) { err = "the SAH collapse needs the PLOC tree (IZPI_BVH_PLOC)"; return IZPI_ERR_INVALID; }
   hipEvent_t e0, e1;
   BVH_TRY(hipEventCreate(&e0));
   BVH_TRY(hipEventCreate(&e1));
@@ -472,7 +556,8 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
   BVH_TRY(rocprim::radix_sort_pairs(nullptr, temp_bytes, codes.p, codes_s.p, ids.p, ids_s.p, (size_t)n, 0, 63, st));
   BVH_TRY(temp.alloc(temp_bytes));
   BVH_TRY(rocprim::radix_sort_pairs(temp.p, temp_bytes, codes.p, codes_s.p, ids.p, ids_s.p, (size_t)n, 0, 63, st));
-  Tree t{left.p, right.p, first.p, last.p, nb.p, ni, (int)leaf_max};
+  DevBuf<uint16_t> dec_t;  // SAH collapse decisions in the collapse's numbering (PLOC)
+  Tree t{left.p, right.p, first.p, last.p, nb.p, ni, (int)leaf_max, nullptr};
   uint32_t total = 0;
   DevBuf<uint32_t> ord;  // leaf order (PLOC); the sorted ids are the leaf order of the LBVH
   const uint32_t* leaf_order = ids_s.p;
@@ -498,6 +583,8 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
     DevBuf<uint8_t> stemp;
     BVH_TRY(stemp.alloc(sbytes));
     uint32_t m = n, base = n;
+    std::vector<uint32_t> iters;  // ids created per iteration: [iters[k], iters[k + 1])
+    iters.push_back(n);
     while (m > 1) {
       const dim3 gm((m + 255) / 256);
       hipLaunchKernelGGL(k_ploc_nn, gm, dim3(256), 0, st, cl.p, m, pbox.p, IZPI_PLOC_RADIUS, nnb.p);
@@ -518,13 +605,26 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
       const uint32_t merges = tail[0] + tail[1], alive = tail[2] + tail[3];
       if (merges == 0) { err = "PLOC made no progress"; return IZPI_ERR_INVALID; }  // a global closest pair always exists
       base += merges;
+      iters.push_back(base);
       m = alive;
       std::swap(cl.p, cl2.p);
     }
     hipLaunchKernelGGL(k_ploc_offsets, dim3((ntot + 255) / 256), dim3(256), 0, st, ntot, pl.p, pr.p, psize.p, pparent.p,
                        off.p);
+    DevBuf<double4> dcost;
+    DevBuf<uint16_t> dec;
+    if (sah) {
+      BVH_TRY(dcost.alloc(ntot)); BVH_TRY(dec.alloc(ntot)); BVH_TRY(dec_t.alloc(ntot));
+      hipLaunchKernelGGL(k_sah_leaves, g, dim3(256), 0, st, n, pbox.p, dcost.p, dec.p);
+      for (size_t k = 0; k + 1 < iters.size(); k++) {
+        const uint32_t cnt = iters[k + 1] - iters[k];
+        hipLaunchKernelGGL(k_sah_level, dim3((cnt + 255) / 256), dim3(256), 0, st, iters[k], cnt, pl.p, pr.p, pbox.p,
+                           psize.p, leaf_max, dcost.p, dec.p);
+      }
+      t.dec = dec_t.p;
+    }
     hipLaunchKernelGGL(k_ploc_to_tree, dim3((ntot + 255) / 256), dim3(256), 0, st, n, pl.p, pr.p, pbox.p, psize.p, off.p,
-                       ids_s.p, left.p, right.p, first.p, last.p, nb.p, ord.p);
+                       ids_s.p, left.p, right.p, first.p, last.p, nb.p, ord.p, dec.p, dec_t.p);
     BVH_TRY(hipGetLastError());
     BVH_TRY(hipStreamSynchronize(st));  // the PLOC buffers are freed at the end of this scope
     leaf_order = ord.p;

@@ -163,13 +163,19 @@ IZPI_DEV izpi_texture tex_rec(const DevScene& sc, bool st, int32_t id) {
 // ImageTxt.Value (image.go:73-101): the nearest texel of a w x h image at (u, v), from
 // its device storage form (TEXF_RGBA or TEXF_GRAY, see TexSlot).
 IZPI_DEV V3 image_rgb(const double* texels, uint64_t off, uint32_t w, uint32_t h, uint32_t fmt, double u, double v) {
+#ifdef IZPI_EXP_TEX_NOLOAD  // timing only (wrong images): no texel index or load
+  return mk(0.5, 0.45, 0.9);
+#endif
   int64_t i = go_int(u * (double)w);
   int64_t j = go_int((1 - v) * ((double)h - 0.001));
   if (i < 0) i = 0;
   if (j < 0) j = 0;
   if (i > (int64_t)w - 1) i = (int64_t)w - 1;
   if (j > (int64_t)h - 1) j = (int64_t)h - 1;
-  const uint64_t k = (uint64_t)j * w + (uint64_t)i;
+  uint64_t k = (uint64_t)j * w + (uint64_t)i;
+#ifdef IZPI_EXP_TEX_HOT  // timing only (wrong images): every lookup hits the image's first 8 texels
+  k &= 7;
+#endif
   if (fmt == TEXF_GRAY) {
     const double g = texels[off + k];
     return mk(g, g, g);
@@ -972,6 +978,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 }
 
+#ifdef IZPI_EXP_NO_NMAP  // timing only (wrong images): normal maps ignored
+#define IZPI_EXP_NMAP(x) false
+#else
+#define IZPI_EXP_NMAP(x) (x)
+#endif
 // Full hit record of the closest primitive (triangle.go:223-264, sphere.go:71-92).
 struct HitRec {
   double t, u, v;
@@ -1002,7 +1013,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
     }
     if (gs_kind(gs) == IZPI_MAT_PBR) {
       const TexSlot ns = mat_slot(sc, mt_staged, h.mat, 1);
-      if (slot_set(ns)) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
+      if (IZPI_EXP_NMAP(slot_set(ns))) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
         V3 nts = slot_rgb(sc, ns, h.u, h.v, mt_staged);
         h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
         h.nraw_ok = true;
@@ -1816,7 +1827,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         V3 rough = slot_set(s_rgh) ? slot_rgb(sc, s_rgh, h.u, h.v, st) : mk(0.5, 0.5, 0.5);
         V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v, st) : mk(0.0, 0.0, 0.0);
         V3 normal = h.n;
-        if (slot_set(s_nrm)) {
+        if (IZPI_EXP_NMAP(slot_set(s_nrm))) {
           V3 nuv = h.nraw_ok ? h.nraw : slot_rgb(sc, s_nrm, h.u, h.v, st);
           V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
           V3 nn0 = h.n;

@@ -137,7 +137,7 @@ int main(int argc, char** argv) {
     double ms = 0;
     if (n) {
       izpi_host_scene_prim_boxes(host, boxes.data());
-      if (izpi_gpu_build_bvh4(ctx, boxes.data(), n, 3, IZPI_BVH_PLOC, nodes.data(), (uint32_t)nodes.size(), &num_nodes,
+      if (izpi_gpu_build_bvh4(ctx, boxes.data(), n, 3, IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes.data(), (uint32_t)nodes.size(), &num_nodes,
                               order.data(), &ms))
         die(izpi_gpu_last_error(ctx));
       if (izpi_host_scene_set_bvh(host, nodes.data(), num_nodes, order.data())) die(izpi_host_last_error());

@@ -26,7 +26,7 @@ from .scene import HostScene
 
 
 # primitives per leaf of the GPU-built tree (the reference allows up to 4, bvh4.go:638)
-GPU_BVH_METHOD = N.BVH_PLOC
+GPU_BVH_METHOD = N.BVH_PLOC_SAH
 GPU_BVH_LEAF_MAX = 3  # measured on C3: 3 -> 1146, 2 -> 1137, 4 -> 1065 Msamples/s
 
 

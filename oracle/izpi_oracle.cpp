@@ -1433,6 +1433,8 @@ void oracle_prim_boxes(oracle_scene* s, double* out) {
 uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32_t method, izpi_bvh4_node* nodes,
                       uint32_t* order) {
   if (n == 0) return 0;
+  const bool sah = (method & 0x100u) != 0;  // IZPI_BVH_SAH
+  method &= ~0x100u;
   // Morton codes of the centroids, 21 bits per axis
   double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (uint32_t i = 0; i < n; i++)
@@ -1566,7 +1568,71 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32
   }
   }  // method
   auto size = [&](int id) { return bn[id].hi - bn[id].lo + 1; };
-  auto is_leaf = [&](int id) { return size(id) <= (int)leaf_max; };
+  // IZPI_BVH_SAH (PLOC trees): the collapse of least surface-area cost. For each binary
+  // node and i = 1..4, D[i] = the least cost of covering its subtree with at most i child
+  // slots; a slot is a leaf (<= leaf_max primitives: Cl + Ct per primitive) or a 4-wide
+  // node (Cn plus the best split of its two children over 4 slots), all weighted by the
+  // box's half area. Children have larger indices than their parents in PLOC's numbering,
+  // so one backward sweep sees them first. Same costs, operation order and tie rules as the
+  // device builder's k_sah_leaves / k_sah_level (bvh_build.hip).
+  const double Cn = 1.0, Cl = 0.5, Ct = 1.0;
+  std::vector<std::array<double, 5>> D;
+  std::vector<uint32_t> dec;
+  if (sah && method == 1) {
+    D.assign(bn.size(), {0, 0, 0, 0, 0});
+    dec.assign(bn.size(), 0);
+    for (size_t id = bn.size(); id-- > 0;) {
+      const BN& x = bn[id];
+      const double* b = x.box;
+      const double dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+      const double area = dx * dy + dy * dz + dz * dx;
+      if (x.l < 0) {
+        const double c = area * (Cl + Ct);
+        D[id] = {0, c, c, c, c};
+        dec[id] = 1;
+        continue;
+      }
+      const auto& L = D[x.l];
+      const auto& R = D[x.r];
+      double best4 = L[1] + R[3];
+      uint32_t k4 = 1;
+      for (uint32_t j = 2; j <= 3; j++)
+        if (L[j] + R[4 - j] < best4) { best4 = L[j] + R[4 - j]; k4 = j; }
+      std::array<double, 5> d{};
+      d[1] = area * Cn + best4;
+      uint32_t bits = k4 << 1;
+      const int sz = x.hi - x.lo + 1;
+      if (sz <= (int)leaf_max) {
+        const double lc = area * (Cl + Ct * (double)sz);
+        if (lc <= d[1]) { d[1] = lc; bits |= 1u; }
+      }
+      for (uint32_t i = 2; i <= 4; i++) {
+        d[i] = d[i - 1];
+        uint32_t ki = 0;
+        for (uint32_t j = 1; j < i; j++)
+          if (L[j] + R[i - j] < d[i]) { d[i] = L[j] + R[i - j]; ki = j; }
+        bits |= ki << (1 + 2 * (i - 1));
+      }
+      D[id] = d;
+      dec[id] = bits;
+    }
+  }
+  auto is_leaf = [&](int id) { return dec.empty() ? size(id) <= (int)leaf_max : (dec[id] & 1u) != 0; };
+  // the wide node's slots from the recorded splits, left to right
+  auto sah_slots = [&](int b, int* res) {
+    int c = 0;
+    std::vector<std::pair<int, int>> work{{bn[b].r, 4 - (int)((dec[b] >> 1) & 3u)}, {bn[b].l, (int)((dec[b] >> 1) & 3u)}};
+    while (!work.empty()) {
+      auto [m, i] = work.back();
+      work.pop_back();
+      while (i > 1 && bn[m].l >= 0 && ((dec[m] >> (1 + 2 * (i - 1))) & 3u) == 0) i--;
+      if (i <= 1 || bn[m].l < 0) { res[c++] = m; continue; }
+      const int ki = (int)((dec[m] >> (1 + 2 * (i - 1))) & 3u);
+      work.push_back({bn[m].r, i - ki});
+      work.push_back({bn[m].l, ki});
+    }
+    return c;
+  };
   auto empty = [](izpi_bvh4_node& nd) {
     for (int s2 = 0; s2 < 4; s2++) {
       nd.child[s2] = -1; nd.prim_count[s2] = 0;
@@ -1578,7 +1644,7 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32
     nd.min_x[s2] = conservativeFloat32Min(b[0]); nd.min_y[s2] = conservativeFloat32Min(b[1]); nd.min_z[s2] = conservativeFloat32Min(b[2]);
     nd.max_x[s2] = conservativeFloat32Max(b[3]); nd.max_y[s2] = conservativeFloat32Max(b[4]); nd.max_z[s2] = conservativeFloat32Max(b[5]);
   };
-  if (is_leaf(0)) {
+  if (size(0) <= (int)leaf_max) {  // the whole scene is one leaf (the device builder's n <= leaf_max)
     empty(nodes[0]);
     nodes[0].child[0] = 0; nodes[0].prim_count[0] = (int32_t)n;
     slot(nodes[0], 0, 0);
@@ -1591,8 +1657,9 @@ uint32_t oracle_lbvh4(const double* boxes, uint32_t n, uint32_t leaf_max, uint32
     next.clear();
     for (auto& fe : frontier) {
       int res[4], c = 0;
-      res[c++] = bn[fe.first].l; res[c++] = bn[fe.first].r;
-      bool expanded = true;
+      if (!dec.empty()) c = sah_slots(fe.first, res);
+      else { res[c++] = bn[fe.first].l; res[c++] = bn[fe.first].r; }
+      bool expanded = dec.empty();
       while (expanded && c < 4) {  // collectChildren (bvh4.go:796-855), largest surface area first
         expanded = false;
         int pick = -1;

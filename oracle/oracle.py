@@ -188,7 +188,8 @@ def postprocess(canvas, width, height, filters):
 
 
 def lbvh4(boxes, leaf_max=4, method=1):
-    """Sequential restatement of the GPU BVH4 builder (method 0 LBVH, 1 PLOC):
+    """Sequential restatement of the GPU BVH4 builder (method 0 LBVH, 1 PLOC; | 0x100 the
+    surface-area-cost collapse):
     (nodes (m, 128) uint8, order)."""
     boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
     n = len(boxes)

@@ -1,6 +1,6 @@
 """The alternative BVH4 builder: a Morton-ordered binary tree
-(PLOC clustering or an LBVH radix tree) collapsed with collectChildren's rule into the
-reference's BVH4Node format.
+(PLOC clustering or an LBVH radix tree) collapsed with collectChildren's rule, or by the
+surface-area cost model (IZPI_BVH_SAH), into the reference's BVH4Node format.
 
 CPU side (here): the oracle's sequential restatement of the builder (oracle_lbvh4)
 yields valid BVH4 trees (the invariants of bvh4_test.go:13-83,453-496 that do not
@@ -78,7 +78,7 @@ def test_host_prim_boxes_equal_oracle():
         assert h.prim_boxes().tobytes() == o.prim_boxes().tobytes()
 
 
-@pytest.mark.parametrize("method", [N.BVH_LBVH, N.BVH_PLOC])
+@pytest.mark.parametrize("method", [N.BVH_LBVH, N.BVH_PLOC, N.BVH_PLOC_SAH])
 @pytest.mark.parametrize("n_side", [1, 3, 24])
 def test_lbvh4_tree_invariants(n_side, method):
     scene = configs.cornell_dragon(1.0, n=n_side)
@@ -88,7 +88,7 @@ def test_lbvh4_tree_invariants(n_side, method):
         check_tree(nodes, order, boxes, leaf_max=lm)
 
 
-@pytest.mark.parametrize("method", [N.BVH_LBVH, N.BVH_PLOC])
+@pytest.mark.parametrize("method", [N.BVH_LBVH, N.BVH_PLOC, N.BVH_PLOC_SAH])
 def test_lbvh4_small_and_degenerate_inputs(method):
     rng = np.random.default_rng(2)
     for n in (1, 2, 4, 5, 17):
@@ -127,6 +127,42 @@ def test_lbvh4_scene_finds_the_reference_closest_hits():
     tb = np.array([h.t if h.hit else np.inf for h in b])
     assert (ta == tb).all()
     assert sum(h.prim_ref != g.prim_ref for h, g in zip(a, b)) <= n // 1000
+
+
+def sah_cost(nodes, cn=1.0, cl=0.5, ct=1.0):
+    """Surface-area cost of a BVH4 under the builder's model: each wide node's visit (cn)
+    and each leaf's visit and primitive tests (cl + ct per primitive), weighted by the
+    half area of the node's box (its slot box in the parent; the root: its slots' union)."""
+    f, child, count = node_view(nodes)
+    def ha(lo, hi):
+        d = hi.astype(np.float64) - lo.astype(np.float64)
+        return d[0] * d[1] + d[1] * d[2] + d[2] * d[0]
+    used = child[0] != -1
+    total = cn * ha(f[0, :3, used].min(0), f[0, 3:, used].max(0)) if count[0, 0] == 0 else 0.0
+    for k in range(len(nodes)):
+        if count[k, 0] > 0:
+            continue
+        for sl in range(4):
+            c = child[k, sl]
+            if c == -1:
+                continue
+            a = ha(f[k, :3, sl], f[k, 3:, sl])
+            total += a * (cl + ct * count[c, 0]) if count[c, 0] > 0 else a * cn
+    return total
+
+
+@pytest.mark.parametrize("lm", [2, 3, 4])
+def test_sah_collapse_costs_less(lm):
+    """IZPI_BVH_SAH picks the collapse of least surface-area cost over the same PLOC binary
+    tree: its cost under that model is below the greedy collectChildren collapse's, and it
+    keeps the same leaf order (the collapse only regroups the binary tree's subtrees)."""
+    scene = configs.cornell_dragon(1.0, n=24)
+    boxes = HostScene(scene, 1.0, skip_bvh=True).prim_boxes()
+    g_nodes, g_order = O.lbvh4(boxes, lm, N.BVH_PLOC)
+    s_nodes, s_order = O.lbvh4(boxes, lm, N.BVH_PLOC_SAH)
+    assert (g_order == s_order).all()
+    check_tree(s_nodes, s_order, boxes, leaf_max=lm)
+    assert sah_cost(s_nodes) < sah_cost(g_nodes)
 
 
 def test_set_bvh_validates():

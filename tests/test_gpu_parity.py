@@ -472,7 +472,7 @@ def test_postprocess_kernel_bitwise(gpu):
     r.close()
 
 
-@pytest.mark.parametrize("method", [N.BVH_PLOC, N.BVH_LBVH])
+@pytest.mark.parametrize("method", [N.BVH_PLOC, N.BVH_LBVH, N.BVH_PLOC_SAH])
 @pytest.mark.parametrize("which", ["cornell", "dragon", "glass", "degenerate", "tiny"])
 def test_gpu_bvh4_builder_equals_oracle_restatement(gpu, which, method):
     """izpi_gpu_build_bvh4 (Morton sort + Karras tree + refit + collapse on the GPU) ==

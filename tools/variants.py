@@ -73,6 +73,8 @@ def child(a):
                           "device_ms": round(st["total_ms"], 3), "trace_ms": round(st["kernel_ms"], 3),
                           "shade_ms": round(st["shade_ms"], 3), "tail_ms": round(st["tail_ms"], 3),
                           "launches": st["launches"], "rays": st["rays"],
+                          "nodes_per_ray": round(st["node_visits"] / max(st["rays"], 1), 3),
+                          "tri_per_ray": round(st["tri_tests"] / max(st["rays"], 1), 3),
                           "digest": hashlib.sha1(img.tobytes()).hexdigest()[:16]}), flush=True)
     r.close()
 
