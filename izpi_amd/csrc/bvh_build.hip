@@ -59,7 +59,9 @@ namespace {
     }                                                                       \
   } while (0)
 
+#ifndef IZPI_PLOC_RADIUS
 #define IZPI_PLOC_RADIUS 8  // PLOC search window (+-positions); 8 and 16 measured equal on C3's mesh
+#endif
 
 constexpr float kMaxF32 = 3.40282346638528859811704183484516925440e+38f;
 

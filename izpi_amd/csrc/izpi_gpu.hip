@@ -992,8 +992,20 @@ struct HitRec {
   V3 nraw;
 };
 // `uvp` is the hit record, whose (u, v): read only for UV-textured triangles and for spheres.
+// A normal map's texel nts at the hit of triangle `prim` (leaf order) applied to the
+// geometric normal n through the triangle's tangent frame (triangle.go:250-264).
+IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts) {
+  nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
+  const GTriTex& tt = sc.tritex[prim];
+  V3 tg = ld3(tt.tg), bt = ld3(tt.bt);
+  V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
+             tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
+  return sdiv(nn, length(nn));
+}
+// defer_nmap: a PBR triangle's normal map is left to the caller (h.n stays geometric), which
+// looks the texel up together with the material's other three (one round of texel loads).
 IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, const GShade& gs, V3 o, V3 d, double time,
-                         bool want_uv, HitRec& h, bool mt_staged = false) {
+                         bool want_uv, HitRec& h, bool mt_staged = false, bool defer_nmap = false) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
   h.mat = gs_mat(gs);
@@ -1011,18 +1023,13 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
       h.u = w * uv[0] + u * uv[2] + v * uv[4];
       h.v = w * uv[1] + u * uv[3] + v * uv[5];
     }
-    if (gs_kind(gs) == IZPI_MAT_PBR) {
+    if (gs_kind(gs) == IZPI_MAT_PBR && !defer_nmap) {
       const TexSlot ns = mat_slot(sc, mt_staged, h.mat, 1);
       if (IZPI_EXP_NMAP(slot_set(ns))) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
-        V3 nts = slot_rgb(sc, ns, h.u, h.v, mt_staged);
+        const V3 nts = slot_rgb(sc, ns, h.u, h.v, mt_staged);
         h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
         h.nraw_ok = true;
-        nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
-        const GTriTex& tt = sc.tritex[c.prim];
-        V3 tg = ld3(tt.tg), bt = ld3(tt.bt);
-        V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
-                   tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
-        n = sdiv(nn, length(nn));
+        n = nmap_tbn(sc, c.prim, n, nts);
       }
     }
     h.n = n;
@@ -1519,6 +1526,18 @@ IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint
   out.hit[pos] = in.hit[i];
 }
 // The path state of entry i (the ray and hit are read by shade_item).
+// What a shading pass reads of entry i besides its path state: the traced ray, the first
+// 16 B of its hit record (t, primitive) and the ray time.
+struct EntryIn {
+  RayOD ray;
+  double2 hit;
+  double time;
+};
+IZPI_DEV void load_entry(const WaveBuf& b, uint32_t i, EntryIn& E) {
+  E.ray = b.ray[i];
+  E.hit = *reinterpret_cast<const double2*>(b.hit + i);
+  E.time = b.time ? b.time[i] : 0.0;
+}
 template <int SAMPLER>
 IZPI_DEV void load_path(const WaveBuf& b, uint32_t i, PathSt& P) {
   const PathHot ph = b.path[i];
@@ -1693,21 +1712,16 @@ IZPI_DEV void sclk_zero() {
 // the block to free.
 template <int SAMPLER, int MATSET>
 IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
-                         PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt, uint32_t& c_ls) {
+                         const EntryIn& E, PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt,
+                         uint32_t& c_ls) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const bool st = sp.staged != 0;  // the scene's small tables are in this block's LDS
   SCLK_T(sc0);
-  {
-    const RayOD rh = in.ray[i];
-    for (int k = 0; k < 3; k++) { R.o[k] = rh.o[k]; R.d[k] = rh.d[k]; }
-    R.kind = kind;
-    R.time = in.time ? in.time[i] : 0.0;  // NewRay(hr.P, dir, r.Time()): the next ray keeps the time
-  }
+  for (int k = 0; k < 3; k++) { R.o[k] = E.ray.o[k]; R.d[k] = E.ray.d[k]; }
+  R.kind = kind;
+  R.time = E.time;  // NewRay(hr.P, dir, r.Time()): the next ray keeps the time
   HitOut H;
-  {
-    const double2 hh = *reinterpret_cast<const double2*>(in.hit + i);  // t, prim (u, v read on demand)
-    H.t = hh.x; H.prim = (int32_t)__double2loint(hh.y); H.pad = 0; H.u = 0; H.v = 0;
-  }
+  H.t = E.hit.x; H.prim = (int32_t)__double2loint(E.hit.y); H.pad = 0; H.u = 0; H.v = 0;  // (u, v) read on demand
   Lcg rng;
   rng.s = P.rng;
   const V3 ro = mk(R.o[0], R.o[1], R.o[2]), rd = mk(R.d[0], R.d[1], R.d[2]);
@@ -1743,7 +1757,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st);
+    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR));
     hit_n = h.n;
     rec_mat = h.mat;
     next_o = h.p;
@@ -1826,9 +1840,14 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         else { V3 c = slot_rgb(sc, s_alb, h.u, h.v, st); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
         V3 rough = slot_set(s_rgh) ? slot_rgb(sc, s_rgh, h.u, h.v, st) : mk(0.5, 0.5, 0.5);
         V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v, st) : mk(0.0, 0.0, 0.0);
+        const bool has_nmap = IZPI_EXP_NMAP(slot_set(s_nrm));
+        const V3 nuv = has_nmap ? slot_rgb(sc, s_nrm, h.u, h.v, st) : mk(0, 0, 0);  // one texel for both uses
+        if (has_nmap && IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
+          h.n = nmap_tbn(sc, H.prim, h.n, nuv);  // the hit record's normal (triangle.go:250-264)
+          hit_n = h.n;
+        }
         V3 normal = h.n;
-        if (IZPI_EXP_NMAP(slot_set(s_nrm))) {
-          V3 nuv = h.nraw_ok ? h.nraw : slot_rgb(sc, s_nrm, h.u, h.v, st);
+        if (has_nmap) {
           V3 tn = mk(2.0 * nuv.x - 1.0, 2.0 * nuv.y - 1.0, nuv.z);
           V3 nn0 = h.n;
           V3 t = cross(nn0, mk(0, 1, 0));
@@ -2007,9 +2026,16 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     RayRec R;
     P.rslot = 0; P.blk = 0; P.depth = 0;
     uint32_t kind = RAY_DEAD;
-    if (valid) kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
+    EntryIn E;
+    if (valid) {
+      // the kind word, path state, ray and hit record in one round of loads (a dead entry's
+      // path and hit are read too, and ignored): waiting for the kind word first, then the
+      // path, then the ray put three memory round trips in front of every item
+      kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
+      load_path<SAMPLER>(wp.in, i, P);
+      load_entry(wp.in, i, E);
+    }
     const bool live = valid && !(kind & RAY_DEAD);
-    if (live) load_path<SAMPLER>(wp.in, i, P);
     if (sp.rec_pool) {  // a path at depth >= rec_dense writes its records to an overflow block
       const bool need = live && P.depth >= sp.rec_dense && P.blk == 0;
       const uint32_t b = pool_alloc(sp, need);
@@ -2017,7 +2043,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       parked = need && b == 0;
       c_park += parked ? 1u : 0u;
     }
-    if (live && !parked) shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, P, R, push, done, fblk, c_lt, c_ls);
+    if (live && !parked) shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls);
     if (sp.rec_pool && fblk) pool_free_one(sp, fblk);
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t1 = __builtin_readcyclecounter();
@@ -2092,7 +2118,9 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
       }
       bool push = false, done = false;
       uint32_t fblk = 0;
-      shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, P, R, push, done, fblk, c_lt, c_ls);
+      EntryIn E;
+      load_entry(wp.in, i, E);
+      shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls);
       if (fblk) pool_free_one(sp, fblk);
       if (!push) break;
       store_entry<SAMPLER>(wp.in, i, P, R);

@@ -1,0 +1,4 @@
+set -e
+timeout -k 10 300 python tools/variants.py run --config C3 --spp 128 --frames 2 base t128 > gpurun_out/ab_c3_w.log 2>&1
+timeout -k 10 300 python tools/variants.py run --config C4 --spp 128 --frames 2 base t128 > gpurun_out/ab_c4_w.log 2>&1
+timeout -k 10 300 python tools/variants.py run --config C5 --spp 32 --frames 1 base t128 > gpurun_out/ab_c5_w.log 2>&1

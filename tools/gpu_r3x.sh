@@ -1,0 +1,6 @@
+set -e
+timeout -k 10 300 python tools/variants.py run --config C3 --spp 128 --frames 2 old base > gpurun_out/ab_c3_x.log 2>&1
+timeout -k 10 300 python tools/variants.py run --config C4 --spp 128 --frames 2 old base > gpurun_out/ab_c4_x.log 2>&1
+timeout -k 10 300 python tools/variants.py run --config C5 --spp 32 --frames 1 old base > gpurun_out/ab_c5_x.log 2>&1
+timeout -k 10 300 python tools/variants.py run --config C2 --spp 64 --frames 2 old base > gpurun_out/ab_c2_x.log 2>&1
+bash tools/gpu_tests.sh
