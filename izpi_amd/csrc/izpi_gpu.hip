@@ -2609,7 +2609,10 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks, int threads = 256) {
 #ifndef IZPI_TRACE_WPE
 #define IZPI_TRACE_WPE 5
 #endif
-constexpr int TRACE_RING = 16, TRACE_WPE = IZPI_TRACE_WPE;
+#ifndef IZPI_TRACE_RING
+#define IZPI_TRACE_RING 16
+#endif
+constexpr int TRACE_RING = IZPI_TRACE_RING, TRACE_WPE = IZPI_TRACE_WPE;
 struct Tracer {
   bool p2 = true;    // DIST
   bool tri = false;  // TRI
