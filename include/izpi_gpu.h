@@ -82,10 +82,10 @@ enum {
  * defaults, and a NULL izpi_render_req.tuning means all defaults. The library reads
  * no environment variables: an inherited variable cannot change a production render. */
 typedef struct izpi_render_tuning {
-  uint32_t slots;        /* cap on paths in flight; 0 = 256M, within half of the HBM this context may use */
-  uint32_t chunk_units;  /* per-sample results held at once (pixels x spp of a chunk); 0 = 1/4 of that HBM */
+  uint32_t slots;        /* cap on paths in flight; 0 = 256M, within 17/32 of the HBM this context may use */
+  uint32_t chunk_units;  /* per-sample results held at once (pixels x spp of a chunk); 0 = 1/8 of that HBM */
   uint32_t rec_dense;    /* unwinding levels per record slot; 0 = 8 (Colour), 32 (Spectral) */
-  uint32_t pool_div;     /* record slots per overflow block; 0 = 16 (Lambert/light scenes), 4 (others) */
+  uint32_t pool_div;     /* record slots per overflow block; 0 = 16 (Colour scenes without glass), 4 (others) */
   uint32_t trace_chunk;  /* queue entries per k_trace2 dequeue; 0 = 512 */
   uint32_t refill_min;   /* idle lanes before a k_trace2 refill (1..64); 0 = 24 */
   uint32_t prim_weight;  /* k_trace2 primitive-step weight against node steps, x/16; 0 = 32 */

@@ -2878,7 +2878,12 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // spp: 2 chunks, C5 at 4096 spp: 12; a chunk's drain costs a few ms).
   uint64_t max_units = std::max<uint64_t>(64ull << 20, (avail / 8) / (3 * sizeof(double)));
   if (tu.chunk_units) max_units = tu.chunk_units;
-  const uint32_t chunk = reuse ? ctx->sizing.chunk : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
+  // the chunks of a request are balanced: as many as the limit needs, equal in size (C4 at
+  // 1024 spp: 2 chunks of 512 instead of 774 + 250, 13 GB less to allocate, same drains)
+  uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(req->spp, max_units / num_pixels));
+  const uint32_t nchunks = (req->spp + chunk - 1) / chunk;
+  chunk = (req->spp + nchunks - 1) / nchunks;
+  if (reuse) chunk = ctx->sizing.chunk;
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
   // blocks (ShadeParams::rec_pool). Colour records are 40 B (24 B compact), spectral 24 B.
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
@@ -2909,11 +2914,14 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
                                  sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(HitSt)) +
                             (uint64_t)rec_dense * D * sizeof(double);
   // Overflow blocks per slot. Lambert/light scenes: 1 per 16 slots (C3: ~3% of the paths
-  // in flight are deeper than 8). Scenes with specular materials or the spectral sampler
-  // run deep chains through glass: 1 per 4 slots (C5 at 1 per 16 parked 29% of its
+  // in flight are deeper than 8). Scenes with glass or the spectral sampler run deep
+  // chains through glass: 1 per 4 slots (C5 at 1 per 16 parked 29% of its
   // shading items, 574 -> 502 ms per 16-spp frame with no parks at 1 per 4). A frame that
   // still parks more than 1/64 of its rays doubles the pool for the renderer's next frame.
-  uint32_t pool_div = (spectral || !ctx->basic_materials) ? 4u : 16u;
+  // Metal / PBR scenes without glass stay at 1 per 16: C4's paths (1.85 rays per sample)
+  // park none, and 1 per 4 allocated 56 GB of pool there (a second of a first frame on
+  // boxes whose driver clears memory as it maps it).
+  uint32_t pool_div = (spectral || !ctx->sc.no_pathlen) ? 4u : 16u;
   pool_div = std::max(1u, pool_div >> std::min(ctx->pool_grow, 4u));
   if (tu.pool_div) pool_div = tu.pool_div;
   if (reuse) pool_div = ctx->sizing.pool_div;

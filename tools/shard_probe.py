@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--bvh", default="gpu")
     ap.add_argument("--pass-log", action="store_true", help="per-pass trace/shade times and queue lengths on stderr")
+    ap.add_argument("--tail-paths", type=int, default=0, help="tuning: k_tail takes over at <= this many paths")
     a = ap.parse_args()
     import torch
     from izpi_amd import _native as N
@@ -27,8 +28,13 @@ def main():
     from izpi_amd.renderer import GPURenderer, common_tiles
     cfg = configs.configs()[a.config]
     spp = a.spp or cfg.spp
+    tune = {}
+    if a.pass_log:
+        tune["flags"] = [N.TUNE_PASS_LOG]
+    if a.tail_paths:
+        tune["tail_paths"] = a.tail_paths
     r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, bvh=a.bvh,
-                    tuning=N.tuning(flags=[N.TUNE_PASS_LOG]) if a.pass_log else None)
+                    tuning=N.tuning(**tune) if tune else None)
     all_tiles = common_tiles(cfg.width, cfg.height)
     t1 = None
     for w in [int(x) for x in a.worlds.split(",")]:
