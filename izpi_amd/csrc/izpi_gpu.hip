@@ -489,11 +489,14 @@ IZPI_DEV void pool_publish(unsigned long long* ctr) {
 }
 
 // ============================================================ traversal
-// BVH4.Hit (bvh4.go:49-164) for one ray in one lane, LDS stack: k_tail's traversal
-// (the wavefront passes use k_trace2 below). Same visit order and counters.
+// BVH4.Hit (bvh4.go:49-164) for one ray in one lane: k_tail's traversal (the wavefront
+// passes use k_trace2 below). Same visit order and counters. The stack's first
+// TAIL_LDS_STACK entries are in LDS (stk, stride 256), deeper ones (STACK > TAIL_LDS_STACK,
+// rare) in the lane's global spill column (gsp, stride gstride).
+constexpr int TAIL_LDS_STACK = 32;
 template <int STACK>
-IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32_t* stk, uint32_t& c_rays,
-                        uint32_t& c_nodes, uint32_t& c_tri, uint32_t& c_sph, uint32_t* err) {
+IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32_t* stk, int32_t* gsp, uint32_t gstride,
+                        uint32_t& c_rays, uint32_t& c_nodes, uint32_t& c_tri, uint32_t& c_sph, uint32_t* err) {
   const RayOD& r = b.ray[qi];
   const uint32_t kind = b.kind[qi];
   const V3 o = mk(r.o[0], r.o[1], r.o[2]), d = mk(r.d[0], r.d[1], r.d[2]);
@@ -545,7 +548,8 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
         if (next == -1) {
           next = ach[i];
         } else if (sp < STACK) {
-          stk[sp * 256] = ach[i];
+          if (STACK <= TAIL_LDS_STACK || sp < TAIL_LDS_STACK) stk[sp * 256] = ach[i];
+          else gsp[(size_t)(sp - TAIL_LDS_STACK) * gstride] = ach[i];
           sp++;
         } else {
           atomicOr(err, 1u);  // unreachable: STACK >= host-computed bound
@@ -556,7 +560,7 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
       cur = next;
     } else if (sp > 0) {
       sp--;
-      cur = stk[sp * 256];
+      cur = (STACK <= TAIL_LDS_STACK || sp < TAIL_LDS_STACK) ? stk[sp * 256] : gsp[(size_t)(sp - TAIL_LDS_STACK) * gstride];
     } else {
       cur = -1;
     }
@@ -2093,10 +2097,12 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 // (no refill: the unit head is exhausted), so the passes of different paths overlap.
 // Same per-ray code paths, results and counters as k_trace + k_shade.
 template <int SAMPLER, int MATSET, int STACK>
-__global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+__global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp, int32_t* spill) {
   shade_stage(sc, sp);
-  __shared__ int32_t lds_stack[STACK * 256];
+  __shared__ int32_t lds_stack[std::min(STACK, TAIL_LDS_STACK) * 256];
   int32_t* stk = lds_stack + threadIdx.x;
+  const uint32_t gstride = gridDim.x * 256;
+  int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
   const uint32_t n = *wp.in_count;
   uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_lt = 0, c_ls = 0;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
@@ -2104,7 +2110,7 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
     if (wp.in.kind[i] & RAY_DEAD) continue;
     bool traced = (wp.in.kind[i] & RAY_PARKED) != 0;  // a parked entry's ray is already traced
     for (;;) {
-      if (!traced) trace_one<STACK>(sc, wp.in, i, stk, c_rays, c_nodes, c_tri, c_sph, sp.error);
+      if (!traced) trace_one<STACK>(sc, wp.in, i, stk, gsp, gstride, c_rays, c_nodes, c_tri, c_sph, sp.error);
       traced = false;
       PathSt P;
       RayRec R;
@@ -2698,6 +2704,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     ctx->err = "grid larger than the counter rows";
     return IZPI_ERR_INVALID;
   }
+  if (tail_deep && (size_t)tail_res * 256 * (64 - TAIL_LDS_STACK) * sizeof(int32_t) > ctx->spill_cap) {
+    ctx->err = "k_tail's stack spill does not fit k_trace2's spill area";
+    return IZPI_ERR_INVALID;
+  }
   uint64_t tail_max = (uint64_t)tail_res * 256;
   if (tu.tail_paths) tail_max = tu.tail_paths;
   if (tu.flags & IZPI_TUNE_NO_TAIL) tail_max = 0;
@@ -2767,8 +2777,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         wp.in = q[cur]; wp.in_count = qn[cur];
         HIP_TRY(hipEventRecord(ctx->ev2, st));
         if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
-        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp);
-        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp);
+        // (the deep instance spills stack entries past 32 into k_trace2's spill area, which
+        // holds 64 entries for each of k_trace2's threads, more than k_tail has)
+        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp, ctx->d_spill);
+        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev3, st));
         HIP_TRY(hipEventSynchronize(ctx->ev3));
