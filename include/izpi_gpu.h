@@ -98,7 +98,8 @@ enum {
   IZPI_TUNE_NO_LEAF_SHORTCUT = 4, /* re-test every leaf box (A10) instead of inferring it */
   IZPI_TUNE_SCALAR_SLAB = 8,      /* the scalar twin of RayAABB4 for every ray */
   IZPI_TUNE_NO_TAIL = 16,         /* no k_tail: wavefront passes to the end */
-  IZPI_TUNE_PASS_LOG = 32         /* diagnostics: per-pass device times on stderr */
+  IZPI_TUNE_PASS_LOG = 32,        /* diagnostics: per-pass device times on stderr */
+  IZPI_TUNE_NO_LDS_BVH = 64       /* small scenes: traverse from global memory, not the per-block LDS copy */
 };
 
 typedef struct izpi_render_req {

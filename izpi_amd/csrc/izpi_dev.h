@@ -114,6 +114,8 @@ struct DevScene {
   uint32_t leaf_shortcut;       // every leaf's slot-0 box equals its parent slot's box
   uint32_t tri_only;            // no spheres: leaf tests may be spread over the wave
   uint32_t no_pathlen;          // no dielectric material: every traced ray is a sampler ray (RAY_MAIN)
+  uint32_t num_inner;           // GInner records
+  uint32_t num_prims;           // GPrim records (and GLeaf slots, indexed by first primitive)
   izpi_camera cam;
 };
 

@@ -582,11 +582,33 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
 // spill[e * stride + gtid], <= 64 entries as bvh4.go:71) and read back on pop. Counters
 // are kept per wave in SGPRs (popcounts of ballots).
 // TRI: the scene holds no spheres (DevScene::tri_only), so the sphere code is compiled out.
-template <int S, int WPE, bool DIST, bool TRI>
+// LB: the whole BVH (inner nodes, leaf records, primitives) is small enough to sit in this
+// block's LDS (bvh_lds_fits: at most BVH_LDS_BYTES): every node and primitive load is an
+// LDS read instead of an L1/L2 round trip (C2, C4, C5: 10-22 primitives).
+constexpr uint32_t BVH_LDS_BYTES = 4096;
+template <int S, int WPE, bool DIST, bool TRI, bool LB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
+  static_assert(!LB || DIST, "the LDS-resident BVH instance runs the distributed leaf tests");
+  typedef float v4f __attribute__((ext_vector_type(4)));   // clang vectors: copyable out of an LDS lvalue
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(3))) v4f LF4;
+  typedef const __attribute__((address_space(3))) v2d LD2;
+  __shared__ float4 bvh_lds[LB ? BVH_LDS_BYTES / 16 : 1];
+  // LDS layout: inner nodes (8 float4 each), leaf records by first primitive (2), primitives (5)
+  LF4* const l_inner = (LF4*)bvh_lds;
+  LF4* const l_leaves = l_inner + (size_t)8 * (LB ? sc.num_inner : 0);
+  LD2* const l_prims = (LD2*)(l_leaves + (size_t)2 * (LB ? sc.num_prims : 0));
+  if constexpr (LB) {
+    const uint32_t ni = 8 * sc.num_inner, nl = 2 * sc.num_prims, np5 = 5 * sc.num_prims;
+    for (uint32_t t = threadIdx.x; t < ni + nl + np5; t += 256)
+      bvh_lds[t] = t < ni ? reinterpret_cast<const float4*>(sc.inner)[t]
+                          : (t < ni + nl ? reinterpret_cast<const float4*>(sc.leaves)[t - ni]
+                                         : reinterpret_cast<const float4*>(sc.prims)[t - ni - nl]);
+    __syncthreads();
+  }
   __shared__ int32_t lds_stack[S * 256];
   // DIST: one wave-wide batch of leaf tests: (primitive << 6 | owner lane), then the
   // test's result flags in the same word; distances and barycentrics
@@ -733,8 +755,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const double2* rp = reinterpret_cast<const double2*>(wp.in.ray + oqi);
           const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2];
           const double otmin = ray_tmin(wp.in, oqi, okind);
-          const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
-          const double2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3], p4 = pp[4];
+          double2 p0, p1, p2, p3, p4;
+          if constexpr (LB) {
+            LD2* pp = l_prims + (size_t)5 * pi;
+            const v2d a0 = pp[0], a1 = pp[1], a2 = pp[2], a3 = pp[3], a4 = pp[4];
+            p0 = make_double2(a0.x, a0.y); p1 = make_double2(a1.x, a1.y); p2 = make_double2(a2.x, a2.y);
+            p3 = make_double2(a3.x, a3.y); p4 = make_double2(a4.x, a4.y);
+          } else {
+            const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
+            p0 = pp[0]; p1 = pp[1]; p2 = pp[2]; p3 = pp[3]; p4 = pp[4];
+          }
           const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
           double t = 0, u = 0, v = 0;
           const V3 o = mk(r0.x, r0.y, r1.x), d = mk(r1.y, r2.x, r2.y);
@@ -855,14 +885,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         // slots 1-3 are invalid. Mixed waves (nearly every node step) then issue one set
         // of loads and wait once, instead of running the two branches one after the other.
         const bool is_leaf = ref_is_leaf(cur);
-        const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
-                                                                   : (const void*)(sc.inner + cur));
-        // leaf lanes read their last five loads from the root node (a cached valid address;
-        // the values are not used)
-        const float4* np = is_leaf ? reinterpret_cast<const float4*>(sc.inner) : lp;
-        const float4 q0 = lp[0], q1 = lp[1];
-        const float4 mnz_ = np[2], mxx_ = np[3], mxy_ = np[4], mxz_ = np[5];
-        const int4 ch_ = *reinterpret_cast<const int4*>(np + 6);
+        float4 q0, q1, mnz_, mxx_, mxy_, mxz_;
+        int4 ch_;
+        if constexpr (LB) {
+          LF4* lp = is_leaf ? l_leaves + (size_t)2 * leaf_start(cur) : l_inner + (size_t)8 * cur;
+          LF4* np = is_leaf ? l_inner : lp;
+          const v4f a0 = lp[0], a1 = lp[1], a2 = np[2], a3 = np[3], a4 = np[4], a5 = np[5], c = np[6];
+          q0 = make_float4(a0.x, a0.y, a0.z, a0.w); q1 = make_float4(a1.x, a1.y, a1.z, a1.w);
+          mnz_ = make_float4(a2.x, a2.y, a2.z, a2.w); mxx_ = make_float4(a3.x, a3.y, a3.z, a3.w);
+          mxy_ = make_float4(a4.x, a4.y, a4.z, a4.w); mxz_ = make_float4(a5.x, a5.y, a5.z, a5.w);
+          ch_ = make_int4(__float_as_int(c.x), __float_as_int(c.y), __float_as_int(c.z), __float_as_int(c.w));
+        } else {
+          const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
+                                                                     : (const void*)(sc.inner + cur));
+          // leaf lanes read their last five loads from the root node (a cached valid address;
+          // the values are not used)
+          const float4* np = is_leaf ? reinterpret_cast<const float4*>(sc.inner) : lp;
+          q0 = lp[0]; q1 = lp[1];
+          mnz_ = np[2]; mxx_ = np[3]; mxy_ = np[4]; mxz_ = np[5];
+          ch_ = *reinterpret_cast<const int4*>(np + 6);
+        }
         // GLeaf = (mn.x, mn.y, mn.z, mx.x), (mx.y, mx.z, start, count)
         const float4 mnx = q0;
         const float4 mny = make_float4(is_leaf ? q0.y : q1.x, q1.y, q1.z, q1.w);
@@ -2622,6 +2664,7 @@ constexpr int TRACE_RING = IZPI_TRACE_RING, TRACE_WPE = IZPI_TRACE_WPE;
 struct Tracer {
   bool p2 = true;    // DIST
   bool tri = false;  // TRI
+  bool lds_bvh = false;  // LB
   // queue entries per dequeue and idle lanes per refill, measured on C3: chunk 128 / refill
   // 16 -> 211 ms of k_trace2 per frame, 512 / 24 -> 201, 1024 -> 207, 2048 -> 216, 64 -> 303
   uint32_t prim_w = 32, tchunk = 512, refill_min = 24;
@@ -2634,7 +2677,8 @@ inline const izpi_render_tuning& tuning_of(const izpi_render_req* req) {
   return req && req->tuning ? *req->tuning : kDefaultTuning;
 }
 
-#define IZPI_T2_LIST(X) X(true, false) X(true, true) X(false, false) X(false, true)
+#define IZPI_T2_LIST(X) \
+  X(true, false, false) X(true, true, false) X(false, false, false) X(false, true, false) X(true, false, true) X(true, true, true)
 
 // Pick the k_trace2 instance and its grid (no allocation: the caller grows d_spill to
 // t->spill_bytes).
@@ -2647,9 +2691,11 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
   // DIST packs (primitive << 6 | lane) into one LDS word
   if (ctx->num_prims >= (1u << 26)) t->p2 = false;
   t->tri = ctx->sc.tri_only != 0 && !(tu.flags & IZPI_TUNE_GENERAL_TRACE);
+  t->lds_bvh = t->p2 && !(tu.flags & IZPI_TUNE_NO_LDS_BVH) &&
+               (uint64_t)ctx->sc.num_inner * sizeof(GInner) + (uint64_t)ctx->sc.num_prims * (sizeof(GLeaf) + sizeof(GPrim)) <= BVH_LDS_BYTES;
   int rc = IZPI_ERR_INVALID;
-#define IZPI_T2_OCC(P, T) \
-  if (t->p2 == P && t->tri == T) rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T>, &t->blocks);
+#define IZPI_T2_OCC(P, T, L) \
+  if (t->p2 == P && t->tri == T && t->lds_bvh == L) rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T, L>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
 #undef IZPI_T2_OCC
   if (rc) return rc;
@@ -2660,9 +2706,9 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
 void launch_trace(izpi_ctx* ctx, const DevScene& sc, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
   const dim3 g(t.blocks), b(256);
   const uint32_t stride = (uint32_t)t.blocks * 256;
-#define IZPI_T2_LAUNCH(P, T)                                                                                   \
-  if (t.p2 == P && t.tri == T) {                                                                               \
-    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T>), g, b, 0, st, sc, wp, ctx->d_counters,          \
+#define IZPI_T2_LAUNCH(P, T, L)                                                                                \
+  if (t.p2 == P && t.tri == T && t.lds_bvh == L) {                                                             \
+    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T, L>), g, b, 0, st, sc, wp, ctx->d_counters,       \
                        misc(ctx, 1), spill, stride, t.prim_w, t.tchunk, t.refill_min);                        \
     return;                                                                                                    \
   }
@@ -3516,6 +3562,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(texels.data(), texels.size(), &dtex);
   UP(d->spd_wavelengths, d->num_spd, &dswl);
   UP(d->spd_values, d->num_spd, &dsv);
+  sc.num_inner = n_inner; sc.num_prims = d->num_prims;
   sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tritex = dtt; sc.lights = dlt; sc.materials = dm;
   sc.mat_const = dmc; sc.mat_tex = dmt; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;

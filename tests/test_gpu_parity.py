@@ -253,6 +253,22 @@ def test_kernel_variants_bitwise(gpu, tune):
     r.close()
 
 
+@pytest.mark.parametrize("flags", [0, N.TUNE_NO_LDS_BVH])
+@pytest.mark.parametrize("which", ["cornell", "glass", "pbr"])
+def test_small_scene_lds_bvh_bitwise(gpu, which, flags):
+    """A scene whose whole BVH4 (inner nodes, leaf records, primitives) fits in 4 KB is
+    traversed from every block's LDS copy (C1, C2, C4, C5); with IZPI_TUNE_NO_LDS_BVH from
+    global memory. Both equal the oracle bit for bit, counters included (bvh4.go:49-164)."""
+    scene, sampler = {"cornell": (configs.cornell_rgb(), N.SAMPLER_COLOUR),
+                      "glass": (configs.cornell_glass_spectral(), N.SAMPLER_SPECTRAL),
+                      "pbr": (configs.cornell_pbr(1.0, res=64), N.SAMPLER_COLOUR)}[which]
+    r = GPURenderer(scene, 48, 48, 4, sampler=sampler, tuning=N.tuning(flags=flags) if flags else None)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 48, 48, 4, sampler)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
+
+
 @pytest.mark.parametrize("tune", [{"rec_dense": 1, "pool_div": 100000},
                                   {"rec_dense": 3, "pool_div": 100000, "flags": N.TUNE_NO_TAIL}])
 def test_record_pool_spectral_glass_bitwise(gpu, tune):
