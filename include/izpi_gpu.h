@@ -82,7 +82,7 @@ enum {
  * defaults, and a NULL izpi_render_req.tuning means all defaults. The library reads
  * no environment variables: an inherited variable cannot change a production render. */
 typedef struct izpi_render_tuning {
-  uint32_t slots;        /* cap on paths in flight; 0 = 256M, within 17/32 of the HBM this context may use */
+  uint32_t slots;        /* cap on paths in flight; 0 = 256M, within 15/32 of the HBM this context may use */
   uint32_t chunk_units;  /* per-sample results held at once (pixels x spp of a chunk); 0 = 1/8 of that HBM */
   uint32_t rec_dense;    /* unwinding levels per record slot; 0 = 8 (Colour), 32 (Spectral) */
   uint32_t pool_div;     /* record slots per overflow block; 0 = 16 (Colour scenes without glass), 4 (others) */

@@ -2927,9 +2927,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   size_t free_b = 0, total_b = 0;
   if (!reuse && hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
   const uint64_t avail = free_b ? ((uint64_t)free_b + render_buffer_bytes(ctx)) / std::max(1u, ctx->dev_share) : 0;
-  // The render workspace stays within 17/32 of the HBM (~152 GB of 288, ~160 GB with the
-  // canvas, post-processing and counter buffers): per-sample results within 1/8, the
-  // wavefront state in the rest.
+  // The render workspace stays within 15/32 of the HBM (~135 GB of 288, under the ~137 GB
+  // C3 takes at its slot cap): per-sample results within 1/8, the wavefront state in the
+  // rest. At 17/32 C4 took 153 GB, and a fresh process allocating it right after processes
+  // of ~131-137 GB waited 0.4-3.9 s for the driver to clear VRAM (first frame up to 6.6x
+  // steady); at 113 GB it allocated in 2 ms and its steady frame was 0.7% slower.
   // Per-sample results wait in HBM ([units][3] doubles) until k_accumulate folds them in
   // sample order. One chunk per request when it fits in 1/8 of the HBM (C3: 12.9 GB of
   // 288 GB), so the wavefront drains once per frame instead of once per chunk (C4 at 1024
@@ -2990,7 +2992,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // (135 GB); C5 at 128 spp ran 1.4% faster at 64M slots than at 118M (less state, better
   // cache and TLB reach in k_shade), so the smaller budget costs the deep-path scenes nothing.
   const uint64_t samples_bytes = (uint64_t)num_pixels * chunk * 3 * sizeof(double);
-  const uint64_t budget = avail / 32 * 17;
+  const uint64_t budget = avail / 32 * 15;
   if (avail > 0)
     slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (budget > samples_bytes ? budget - samples_bytes : 0) /
                                                                           (per_slot + 2 * per_block / pool_div + 1)));
