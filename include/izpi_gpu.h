@@ -87,8 +87,8 @@ typedef struct izpi_render_tuning {
   uint32_t rec_dense;    /* unwinding levels per record slot; 0 = 8 (Colour), 32 (Spectral) */
   uint32_t pool_div;     /* record slots per overflow block; 0 = 16 (Colour scenes without glass), 4 (others) */
   uint32_t trace_chunk;  /* queue entries per k_trace2 dequeue; 0 = 512 */
-  uint32_t refill_min;   /* idle lanes before a k_trace2 refill (1..64); 0 = 24 */
-  uint32_t prim_weight;  /* k_trace2 primitive-step weight against node steps, x/16; 0 = 32 */
+  uint32_t refill_min;   /* idle lanes before a k_trace2 refill (1..64); 0 = 24 (40 with the BVH in LDS) */
+  uint32_t prim_weight;  /* k_trace2 primitive-step weight against node steps, x/16; 0 = 32 (24 with the BVH in LDS) */
   uint32_t flags;        /* IZPI_TUNE_* */
   uint64_t tail_paths;   /* k_tail takes over at <= this many paths; 0 = the resident lanes */
 } izpi_render_tuning;

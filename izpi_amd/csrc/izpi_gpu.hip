@@ -2685,14 +2685,21 @@ inline const izpi_render_tuning& tuning_of(const izpi_render_req* req) {
 int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
   *t = Tracer();
   if (tu.flags & IZPI_TUNE_NO_DIST) t->p2 = false;
-  if (tu.prim_weight) t->prim_w = tu.prim_weight;
-  if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
-  if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
   // DIST packs (primitive << 6 | lane) into one LDS word
   if (ctx->num_prims >= (1u << 26)) t->p2 = false;
   t->tri = ctx->sc.tri_only != 0 && !(tu.flags & IZPI_TUNE_GENERAL_TRACE);
   t->lds_bvh = t->p2 && !(tu.flags & IZPI_TUNE_NO_LDS_BVH) &&
                (uint64_t)ctx->sc.num_inner * sizeof(GInner) + (uint64_t)ctx->sc.num_prims * (sizeof(GLeaf) + sizeof(GPrim)) <= BVH_LDS_BYTES;
+  if (t->lds_bvh) {
+    // With the tree in LDS a step costs little next to a refill's ray loads: refill later
+    // and weight primitive steps less (profiles/r3i/tune_sweep2.log, trace per frame
+    // against 24 / 32: C5 -10.5%, C4 -6.3%, C2 -5.2%; C3's global-memory instance keeps them)
+    t->refill_min = 40;
+    t->prim_w = 24;
+  }
+  if (tu.prim_weight) t->prim_w = tu.prim_weight;
+  if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
+  if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
   int rc = IZPI_ERR_INVALID;
 #define IZPI_T2_OCC(P, T, L) \
   if (t->p2 == P && t->tri == T && t->lds_bvh == L) rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T, L>, &t->blocks);
