@@ -99,7 +99,8 @@ enum {
   IZPI_TUNE_SCALAR_SLAB = 8,      /* the scalar twin of RayAABB4 for every ray */
   IZPI_TUNE_NO_TAIL = 16,         /* no k_tail: wavefront passes to the end */
   IZPI_TUNE_PASS_LOG = 32,        /* diagnostics: per-pass device times on stderr */
-  IZPI_TUNE_NO_LDS_BVH = 64       /* small scenes: traverse from global memory, not the per-block LDS copy */
+  IZPI_TUNE_NO_LDS_BVH = 64,      /* small scenes: traverse from global memory, not the per-block LDS copy */
+  IZPI_TUNE_NO_RAY_LDS = 128      /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
 };
 
 typedef struct izpi_render_req {
@@ -116,9 +117,10 @@ typedef struct izpi_render_req {
   double background[3];       /* Colour background (leader.go:140: black) */
   uint64_t seed;              /* master seed of the per-sample LCG streams */
   uint32_t post;              /* IZPI_POST_*: post-processing of a whole-frame IZPI_OUT_CANVAS render */
-  uint32_t pad_post;
+  uint32_t abi_version;       /* IZPI_ABI_VERSION (2); 0 = a request laid out by ABI 1, which ends before `tuning`:
+                                 the library then reads no further and uses the default tuning */
   double exposure;            /* XYZToRGB exposure (Scene.Exposure = camera exposure) */
-  const izpi_render_tuning* tuning; /* NULL = defaults */
+  const izpi_render_tuning* tuning; /* NULL = defaults; read only when abi_version >= 2 */
 } izpi_render_req;
 
 /* Post-processing applied by Render for the Spectral sampler (renderer.go:215-219):
@@ -265,6 +267,15 @@ int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint
  * every rank the worst status: a rank's own failure returns its status, a failure of
  * another rank IZPI_ERR_PEER (last_error names the rank). */
 int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats);
+
+/* Progress of the render running on ctx (izpi_gpu_render, _render_device, _render_rank),
+ * callable from another thread while it runs (RendererImpl.Render's per-tile progress
+ * bar, renderer.go:119-121, rgb.go:54-56): samples (pixels x spp) whose paths have
+ * finished, as of the library's last queue poll (every <= 8 wavefront passes, a lower
+ * bound), and the request's samples. After the call returns, done == total. The multi
+ * form sums the contexts of `m` (their shares of one frame). */
+int izpi_gpu_progress(izpi_ctx* ctx, uint64_t* samples_done, uint64_t* samples_total);
+int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* samples_total);
 
 /* Test hook (fault injection): where = 1 makes izpi_gpu_render_rank fail this rank's local
  * checks, 2 makes every render on this context fail as a device fault would; 0 = off. */

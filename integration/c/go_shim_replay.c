@@ -101,6 +101,7 @@ int main(int argc, char** argv) {
     return fail("upload", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
   izpi_render_req req;
   memset(&req, 0, sizeof req);
+  req.abi_version = IZPI_ABI_VERSION;
   req.width = W; req.height = H; req.spp = spp; req.max_depth = 50;
   req.out_layout = IZPI_OUT_CANVAS;
   req.seed = 12345;

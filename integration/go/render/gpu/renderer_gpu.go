@@ -192,6 +192,7 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 	}
 	// 5. the request: whole frame, Render's post-processing (renderer.go:215-219)
 	desc := C.izpi_host_scene_desc(r.host)
+	r.req.abi_version = C.IZPI_ABI_VERSION
 	r.req.width, r.req.height = C.uint32_t(opt.SizeX), C.uint32_t(opt.SizeY)
 	r.req.spp, r.req.max_depth = C.uint32_t(opt.NumSamples), C.uint32_t(opt.MaxDepth)
 	r.req.out_layout = C.IZPI_OUT_CANVAS

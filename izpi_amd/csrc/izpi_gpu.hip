@@ -29,6 +29,7 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <thread>
 
@@ -585,13 +586,19 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
 // LB: the whole BVH (inner nodes, leaf records, primitives) is small enough to sit in this
 // block's LDS (bvh_lds_fits: at most BVH_LDS_BYTES): every node and primitive load is an
 // LDS read instead of an L1/L2 round trip (C2, C4, C5: 10-22 primitives).
+// RL: triangle-only scene whose hits need no (u, v) (wp.hit_uv == 0, C3): the lane's f64 ray
+// is kept in LDS from its refill on, so a primitive test reads its owner's ray with three
+// ds_read_b128 instead of re-reading the 48-B record from global memory, where it has
+// usually left the XCD's L2 by then; the (u, v) arrays it does not need make room for it
+// (31.8 KB of LDS per block: still 5 blocks per CU).
 constexpr uint32_t BVH_LDS_BYTES = 4096;
-template <int S, int WPE, bool DIST, bool TRI, bool LB>
+template <int S, int WPE, bool DIST, bool TRI, bool LB, bool RL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   static_assert(!LB || DIST, "the LDS-resident BVH instance runs the distributed leaf tests");
+  static_assert(!RL || (DIST && TRI && !LB), "the LDS-resident ray instance is the triangle-only global-BVH one");
   typedef float v4f __attribute__((ext_vector_type(4)));   // clang vectors: copyable out of an LDS lvalue
   typedef double v2d __attribute__((ext_vector_type(2)));
   typedef const __attribute__((address_space(3))) v4f LF4;
@@ -614,11 +621,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // test's result flags in the same word; distances and barycentrics
   // (+4: an owner reads its four entries unconditionally, past the wave's last batch entry)
   __shared__ uint32_t dist_owner[DIST ? 260 : 1];
-  __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST ? 260 : 1], dist_v[DIST ? 260 : 1];
+  __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST && !RL ? 260 : 1], dist_v[DIST && !RL ? 260 : 1];
   // (u, v) of the lane's accepted hit so far: the hit record is stored once, when the ray finishes
   // (a global store per accepted hit would hold up the wave's next load wait, since
   // vmcnt counts stores and loads in one queue)
-  __shared__ double2 lds_uv[256];
+  __shared__ double2 lds_uv[RL ? 1 : 256];
+  // RL: the lane's ray (o, d) as three double2, written at its refill
+  __shared__ double2 ray_lds[RL ? 3 * 256 : 1];
   const uint32_t wbase = threadIdx.x & ~63u;
   int32_t* stk = lds_stack + threadIdx.x;
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
@@ -689,6 +698,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           const uint32_t k = read_kind ? wp.in.kind[my] : (uint32_t)RAY_MAIN;
           // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
           const RayOD& r = wp.in.ray[my];
+          if constexpr (RL) {
+            const double2* rp = reinterpret_cast<const double2*>(&r);
+            const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+            ray_lds[3 * threadIdx.x] = r0; ray_lds[3 * threadIdx.x + 1] = r1; ray_lds[3 * threadIdx.x + 2] = r2;
+          }
           if (!(k & (RAY_PARKED | RAY_DEAD)) && (uint64_t)__double_as_longlong(r.o[0]) != DEAD_BITS) {
             qi = my;
             lkind = k;
@@ -752,8 +766,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const uint32_t okind = (uint32_t)__shfl((int)lkind, (int)ow);
         if (lane < total) {
           const int32_t pi = (int32_t)(ent >> 6);
-          const double2* rp = reinterpret_cast<const double2*>(wp.in.ray + oqi);
-          const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+          double2 r0, r1, r2;
+          if constexpr (RL) {
+            const uint32_t ro = 3 * (wbase + ow);
+            r0 = ray_lds[ro]; r1 = ray_lds[ro + 1]; r2 = ray_lds[ro + 2];
+          } else {
+            const double2* rp = reinterpret_cast<const double2*>(wp.in.ray + oqi);
+            r0 = rp[0]; r1 = rp[1]; r2 = rp[2];
+          }
           const double otmin = ray_tmin(wp.in, oqi, okind);
           double2 p0, p1, p2, p3, p4;
           if constexpr (LB) {
@@ -779,7 +799,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (sph_roots(sph_center(pa, time), pa[6], o, d, t, u))
               flags |= 1u | (t > otmin ? 4u : 0u) | (u > otmin ? 8u : 0u);
           }
-          dist_t[wbase + lane] = t; dist_u[wbase + lane] = u; dist_v[wbase + lane] = v;
+          dist_t[wbase + lane] = t;
+          if constexpr (!RL) { dist_u[wbase + lane] = u; dist_v[wbase + lane] = v; }
           dist_owner[wbase + lane] = flags;
         }
         const uint32_t n_sph_tests = TRI ? 0u : (uint32_t)__popcll(__ballot(lane < total && (dist_owner[wbase + lane] & 2u)));
@@ -797,7 +818,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           for (uint32_t i = 0; i < 4; i++)  // reject only `t > tMax` (triangle.go:219), in primitive order
             if (i < cnt && (f[i] & 1u) && !(tt[i] > tmax)) { tmax = tt[i]; acc = (int32_t)i; }
           if (acc >= 0) {
-            lds_uv[threadIdx.x] = make_double2(dist_u[j0 + acc], dist_v[j0 + acc]);
+            if constexpr (!RL) lds_uv[threadIdx.x] = make_double2(dist_u[j0 + acc], dist_v[j0 + acc]);
             bprim = pk + acc;
             clean_from = sp;
           }
@@ -989,8 +1010,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       pend = lf ? leaf_start(top) + leaf_count(top) : pend;
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
-        const double2 uv = bprim >= 0 ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        if (wp.hit_uv) {
+        const double2 uv = (!RL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
+        if (!RL && wp.hit_uv) {
           wp.in.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
         } else {  // nothing reads (u, v): half the record
           *reinterpret_cast<double2*>(wp.in.hit + qi) = make_double2(bprim >= 0 ? tmax : 0.0, __hiloint2double(0, bprim));
@@ -2526,6 +2547,9 @@ struct izpi_ctx {
   bool any_uv = false;           // a material reads the hit's (u, v) (image textures)
   uint32_t pool_grow = 0;        // overflow pool doublings earned by frames that parked (render_impl)
   uint32_t dev_share = 1;        // contexts of this process on this device (izpi_gpu_multi_open): they split its HBM
+  // Progress of the running render (izpi_gpu_progress, read from other threads): samples
+  // whose paths have finished, as of the host's last queue poll, and the request's samples.
+  std::atomic<uint64_t> prog_done{0}, prog_total{0};
 };
 
 namespace {
@@ -2665,6 +2689,7 @@ struct Tracer {
   bool p2 = true;    // DIST
   bool tri = false;  // TRI
   bool lds_bvh = false;  // LB
+  bool ray_lds = false;  // RL
   // queue entries per dequeue and idle lanes per refill, measured on C3: chunk 128 / refill
   // 16 -> 211 ms of k_trace2 per frame, 512 / 24 -> 201, 1024 -> 207, 2048 -> 216, 64 -> 303
   uint32_t prim_w = 32, tchunk = 512, refill_min = 24;
@@ -2674,15 +2699,18 @@ struct Tracer {
 
 const izpi_render_tuning kDefaultTuning{};
 inline const izpi_render_tuning& tuning_of(const izpi_render_req* req) {
-  return req && req->tuning ? *req->tuning : kDefaultTuning;
+  // an ABI-1 request (abi_version 0) ends before `tuning`: nothing past it is read
+  return req && req->abi_version >= 2 && req->tuning ? *req->tuning : kDefaultTuning;
 }
 
-#define IZPI_T2_LIST(X) \
-  X(true, false, false) X(true, true, false) X(false, false, false) X(false, true, false) X(true, false, true) X(true, true, true)
+#define IZPI_T2_LIST(X)                                                                                      \
+  X(true, false, false, false) X(true, true, false, false) X(false, false, false, false) X(false, true, false, false) \
+  X(true, false, true, false) X(true, true, true, false) X(true, true, false, true)
 
 // Pick the k_trace2 instance and its grid (no allocation: the caller grows d_spill to
 // t->spill_bytes).
-int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
+// need_uv: the caller reads the hits' (u, v) (WaveParams::hit_uv).
+int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, bool need_uv, Tracer* t) {
   *t = Tracer();
   if (tu.flags & IZPI_TUNE_NO_DIST) t->p2 = false;
   // DIST packs (primitive << 6 | lane) into one LDS word
@@ -2697,12 +2725,14 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
     t->refill_min = 40;
     t->prim_w = 24;
   }
+  t->ray_lds = t->p2 && t->tri && !t->lds_bvh && !need_uv && !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
   if (tu.prim_weight) t->prim_w = tu.prim_weight;
   if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
   if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
   int rc = IZPI_ERR_INVALID;
-#define IZPI_T2_OCC(P, T, L) \
-  if (t->p2 == P && t->tri == T && t->lds_bvh == L) rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T, L>, &t->blocks);
+#define IZPI_T2_OCC(P, T, L, R)                                               \
+  if (t->p2 == P && t->tri == T && t->lds_bvh == L && t->ray_lds == R) \
+    rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T, L, R>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
 #undef IZPI_T2_OCC
   if (rc) return rc;
@@ -2713,9 +2743,9 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, Tracer* t) {
 void launch_trace(izpi_ctx* ctx, const DevScene& sc, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
   const dim3 g(t.blocks), b(256);
   const uint32_t stride = (uint32_t)t.blocks * 256;
-#define IZPI_T2_LAUNCH(P, T, L)                                                                                \
-  if (t.p2 == P && t.tri == T && t.lds_bvh == L) {                                                             \
-    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T, L>), g, b, 0, st, sc, wp, ctx->d_counters,       \
+#define IZPI_T2_LAUNCH(P, T, L, R)                                                                             \
+  if (t.p2 == P && t.tri == T && t.lds_bvh == L && t.ray_lds == R) {                                           \
+    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T, L, R>), g, b, 0, st, sc, wp, ctx->d_counters,    \
                        misc(ctx, 1), spill, stride, t.prim_w, t.tchunk, t.refill_min);                        \
     return;                                                                                                    \
   }
@@ -2823,6 +2853,10 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
       }
       const uint32_t head = ctx->h_count[0];
       n = ctx->h_count[(3 + cur) * MISC_STRIDE];
+      {  // units handed out minus the entries still queued: samples finished (a lower bound)
+        const uint64_t started = std::min<uint64_t>(head, sp.total_units);
+        ctx->prog_done.store((uint64_t)s0 * num_pixels + (started > n ? started - n : 0), std::memory_order_relaxed);
+      }
       if (pass_log) fprintf(stderr, "IZPI_BATCH queue %u head %u\n", n, head);
       if (head >= sp.total_units) B = 1;
       // every unit has started: finish the remaining paths in one k_tail launch
@@ -2845,6 +2879,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     }
     ap.chunk_spp = cs;
     ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
+    ctx->prog_done.store((uint64_t)(s0 + cs) * num_pixels, std::memory_order_relaxed);
     hipLaunchKernelGGL(k_accumulate, dim3((num_pixels + 255) / 256), dim3(256), 0, st, ap);
     HIP_TRY(hipGetLastError());
   }
@@ -2895,6 +2930,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (ctx->fault_inject == 2) { ctx->err = "injected render fault (izpi_gpu_debug_fault)"; return IZPI_ERR_DEVICE; }
   if (!ctx->have_scene) { ctx->err = "render before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
+  if (req->abi_version > IZPI_ABI_VERSION) { ctx->err = "render request from a newer ABI"; return IZPI_ERR_INVALID; }
   if (req->sampler != IZPI_SAMPLER_COLOUR && req->sampler != IZPI_SAMPLER_SPECTRAL) { ctx->err = "unsupported sampler"; return IZPI_ERR_UNSUPPORTED; }
   if (req->post != IZPI_POST_NONE &&
       ((req->post & ~(uint32_t)(IZPI_POST_SPECTRAL | IZPI_POST_GAMMA_CLAMP)) || req->out_layout != IZPI_OUT_CANVAS ||
@@ -2916,6 +2952,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const uint64_t num_pixels64 = (uint64_t)ntiles * tw * th;
   if (num_pixels64 > (1ull << 30)) { ctx->err = "too many pixels in one request"; return IZPI_ERR_INVALID; }
   const uint32_t num_pixels = (uint32_t)num_pixels64;
+  ctx->prog_done.store(0, std::memory_order_relaxed);
+  ctx->prog_total.store(num_pixels64 * req->spp, std::memory_order_relaxed);
   if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
   const izpi_render_tuning& tu = tuning_of(req);
   // this render's view of the scene: the traversal shortcuts the tuning switches off
@@ -2923,7 +2961,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (tu.flags & IZPI_TUNE_NO_LEAF_SHORTCUT) sc.leaf_shortcut = 0;
   if (tu.flags & IZPI_TUNE_SCALAR_SLAB) sc.nan_free_bounds = 0;
   Tracer tr;
-  int trc = make_tracer(ctx, tu, &tr);
+  int trc = make_tracer(ctx, tu, !ctx->sc.tri_only || ctx->any_uv, &tr);
   if (trc) return trc;
   // Sizing against the HBM this context may use: what is free plus the render buffers it
   // holds and would release (a later frame reuses them, so every frame of a renderer sizes
@@ -3281,7 +3319,8 @@ const char* izpi_gpu_last_error(izpi_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   if (!ctx || !d) return IZPI_ERR_INVALID;
-  if (d->abi_version != IZPI_ABI_VERSION) { ctx->err = "ABI version mismatch"; return IZPI_ERR_INVALID; }
+  // the scene descriptor is laid out alike in ABI 1 and 2
+  if (d->abi_version < 1 || d->abi_version > IZPI_ABI_VERSION) { ctx->err = "ABI version mismatch"; return IZPI_ERR_INVALID; }
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   free_scene(ctx);
@@ -3754,7 +3793,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh;
   wp.in_count = misc(ctx, 3); wp.trace_next = misc(ctx, 2); wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
-  int rc = make_tracer(ctx, kDefaultTuning, &tr);
+  int rc = make_tracer(ctx, kDefaultTuning, true, &tr);
   if (rc) return rc;
   if ((rc = grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes))) return rc;
   launch_trace(ctx, ctx->sc, tr, wp, ctx->stream, ctx->d_spill);
@@ -4057,6 +4096,25 @@ int izpi_host_assemble_shares(uint32_t width, uint32_t height, const uint32_t* t
       if (packed_target(mine.data(), p, tw, th, height, &x, &row))
         memcpy(canvas + ((size_t)row * width + x) * 4, packed + (size_t)p * 4, 4 * sizeof(double));
     }
+  }
+  return IZPI_OK;
+}
+
+int izpi_gpu_progress(izpi_ctx* ctx, uint64_t* samples_done, uint64_t* samples_total) {
+  if (!ctx || !samples_done || !samples_total) return IZPI_ERR_INVALID;
+  // total first: a render starting between the two loads shows 0 of its own total at worst
+  *samples_total = ctx->prog_total.load(std::memory_order_relaxed);
+  *samples_done = std::min(ctx->prog_done.load(std::memory_order_relaxed), *samples_total);
+  return IZPI_OK;
+}
+
+int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* samples_total) {
+  if (!m || !samples_done || !samples_total) return IZPI_ERR_INVALID;
+  *samples_done = 0; *samples_total = 0;
+  for (izpi_ctx* c : m->ctx) {
+    uint64_t d = 0, t = 0;
+    izpi_gpu_progress(c, &d, &t);
+    *samples_done += d; *samples_total += t;
   }
   return IZPI_OK;
 }

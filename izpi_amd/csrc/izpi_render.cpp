@@ -137,7 +137,7 @@ int main(int argc, char** argv) {
     double ms = 0;
     if (n) {
       izpi_host_scene_prim_boxes(host, boxes.data());
-      if (izpi_gpu_build_bvh4(ctx, boxes.data(), n, 3, IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes.data(), (uint32_t)nodes.size(), &num_nodes,
+      if (izpi_gpu_build_bvh4(ctx, boxes.data(), n, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes.data(), (uint32_t)nodes.size(), &num_nodes,
                               order.data(), &ms))
         die(izpi_gpu_last_error(ctx));
       if (izpi_host_scene_set_bvh(host, nodes.data(), num_nodes, order.data())) die(izpi_host_last_error());
@@ -150,6 +150,7 @@ int main(int argc, char** argv) {
   // ---- Render (renderer.go:108-222)
   izpi_render_req req;
   memset(&req, 0, sizeof req);
+  req.abi_version = IZPI_ABI_VERSION;
   req.width = W; req.height = H; req.spp = spp; req.max_depth = depth;
   req.sampler = spectral ? IZPI_SAMPLER_SPECTRAL : IZPI_SAMPLER_COLOUR;
   req.out_layout = IZPI_OUT_CANVAS;

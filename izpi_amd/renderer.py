@@ -25,9 +25,7 @@ from . import _native as N
 from .scene import HostScene
 
 
-# primitives per leaf of the GPU-built tree (the reference allows up to 4, bvh4.go:638)
 GPU_BVH_METHOD = N.BVH_PLOC_SAH
-GPU_BVH_LEAF_MAX = 3  # measured on C3: 3 -> 1146, 2 -> 1137, 4 -> 1065 Msamples/s
 
 
 def gpu_leaf_max(desc):
@@ -68,6 +66,7 @@ def make_request(width, height, spp, max_depth, sampler, background, seed, expos
     """izpi_render_req for Render (the arrays it points to are kept alive on `req._keep`).
     tuning: an N.RenderTuning (launch settings; None = the library's defaults)."""
     req = N.RenderReq()
+    req.abi_version = N.IZPI_ABI_VERSION
     req.post = post
     req.exposure = exposure
     req.width, req.height = width, height
@@ -174,6 +173,13 @@ class GPURenderer:
         _check(rc, self.ctx, "izpi_gpu_render")
         self.stats = st.as_dict()
         return canvas
+
+    def progress(self):
+        """(samples finished, samples of the request) of the render running on this context,
+        readable from another thread while render() runs (izpi_gpu_progress)."""
+        d, t = C.c_uint64(), C.c_uint64()
+        _check(N.lib().izpi_gpu_progress(self.ctx, C.byref(d), C.byref(t)), self.ctx, "izpi_gpu_progress")
+        return d.value, t.value
 
     def render_spectral_rgb(self):
         """The full reference Render() for the Spectral sampler: XYZ render, then

@@ -233,7 +233,7 @@ def test_queue_keeps_every_slot_while_units_remain(gpu, name, capfd):
                                   {"flags": N.TUNE_NO_DIST},
                                   {"flags": N.TUNE_NO_TAIL}, {"flags": N.TUNE_NO_TAIL, "slots": 3000},
                                   {"tail_paths": 100},
-                                  {"flags": N.TUNE_GENERAL_TRACE},
+                                  {"flags": N.TUNE_GENERAL_TRACE}, {"flags": N.TUNE_NO_RAY_LDS},
                                   {"rec_dense": 1, "pool_div": 100000},
                                   {"rec_dense": 2, "pool_div": 100000, "flags": N.TUNE_NO_TAIL},
                                   {"rec_dense": 50}])
@@ -806,4 +806,34 @@ def test_spectral_sampling_device_bitwise(gpu):
         O.lib().oracle_cie_values(float(v), o3)
         ref[k] = list(o3)
     assert xyz.tobytes() == ref.tobytes()
+    r.close()
+
+
+def test_progress_is_monotone_and_completes(gpu):
+    """izpi_gpu_progress polled from another thread while a frame renders (the per-tile
+    progress of renderer.go:119-121): never decreasing, bounded by the request's samples,
+    equal to them once the call returns; the frame stays bit-exact."""
+    import threading
+    scene = configs.cornell_dragon(1.0, n=60)
+    r = GPURenderer(scene, 96, 96, 32, tuning=N.tuning(slots=20000))
+    seen, stop = [], threading.Event()
+
+    def poll():
+        while not stop.is_set():
+            seen.append(r.progress())
+
+    th = threading.Thread(target=poll)
+    th.start()
+    try:
+        img = r.render()
+    finally:
+        stop.set()
+        th.join()
+    total = 96 * 96 * 32
+    assert r.progress() == (total, total)
+    done = [d for d, t in seen if t == total]
+    assert done == sorted(done) and all(0 <= d <= total for d in done)
+    assert any(0 < d < total for d in done), seen[:5]
+    ref, ostats = oracle_canvas(scene, 96, 96, 32, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
     r.close()
