@@ -17,15 +17,18 @@ GPUs (strong scaling: the frame is fixed, its 32x32 tiles are dealt tile % N):
   Both forms do the gather inside the timed step.
 
 The JSON line also carries
-  roofline:     the dominant kernel k_trace2 against HBM peak. `achieved` = HBM traffic
-                per frame, measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
-                MI355X_MICROARCH.md's gfx950 correction) over a one-frame child run of this
-                same revision, divided by k_trace2's HIP-event time per frame in the timed
-                run. `achieved_algorithmic` is SURVEY.md §8(d)'s model (128 B per node
-                visit, 72 B per triangle test, 32 B per sphere test, counted exactly by the
-                kernel) over the same time: those bytes are mostly served by L2 and the
-                Infinity Cache, so it is not bounded by HBM peak. TCC hit rates come from a
-                third PMC pass.
+  roofline:     the dominant kernel k_trace2 against HBM peak. `achieved` = L2 memory-side
+                traffic per frame, measured by rocprofv3 PMC passes (FETCH_SIZE x2 +
+                WRITE_SIZE; the x2 is MI355X_MICROARCH.md's gfx950 correction, checked for
+                k_trace2's access shapes by tools/fetch_calib) over a one-frame child run of
+                this same revision, divided by k_trace2's HIP-event time per frame in the timed
+                run. Those counters include Infinity-Cache hits, so `frac` is the L2-miss
+                fabric rate against HBM peak (`levels.l2_miss_fabric_frac`); `levels` puts the
+                same bytes against the Infinity Cache's measured random-gather rate
+                (`mall_frac`) and SURVEY.md §8(d)'s algorithmic bytes (128 B per node visit,
+                72 B per triangle test, 32 B per sphere test, counted exactly by the kernel)
+                against the L2's rate (`l2_frac`), and names the nearest ceiling. TCC hit
+                rates come from a third PMC pass.
   cpu_baseline: the CPU oracle (deterministic restatement of the Go hot path) on a
                 bounded sample of the same frame on the CPUs this process may use (rank 0,
                 N=1), with the host's CPU model and core counts.
@@ -45,6 +48,11 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md, L2 (per XCD): 34.5 TB/s aggregate over the 8 XCDs
+# MI355X_MICROARCH.md, "Indexed rows: gather into LDS": uniformly random rows served by the
+# Infinity Cache read at 8.6 TB/s chip-wide from a 38 MB table and 7.4-7.9 TB/s from a 151 MB
+# one; C3's BVH + triangles are 136 MB, so the 151-MB figure (mid-range) is the ceiling
+MALL_GATHER_GBS = 7650.0
 PMC_PASSES = {"fetch": ["FETCH_SIZE"], "write": ["WRITE_SIZE"], "tcc": ["TCC_HIT_sum", "TCC_MISS_sum"],
               "sq": ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                      "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_ANY"]}
@@ -471,9 +479,29 @@ def main():
             "avg_launch_ms": trace_ms_frame / launches, "launches_per_frame": launches}
     if "k_trace2" in pmc:
         t = pmc["k_trace2"]
-        roof["traffic"] = t["bytes_per_frame"] / max(t["dispatches"], 1)  # HBM bytes per launch
+        roof["traffic"] = t["bytes_per_frame"] / max(t["dispatches"], 1)  # L2 memory-side bytes per launch
         roof["achieved"] = round(t["bytes_per_frame"] / (trace_ms_frame * 1e-3) / 1e9, 2)
         roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
+        # What `frac` measures, level by level: FETCH_SIZE / WRITE_SIZE count the
+        # L2's memory-side requests, Infinity-Cache hits included, so `achieved` is the L2-miss
+        # fabric rate, an upper bound of the HBM rate. The same bytes against the measured
+        # Infinity-Cache random-gather rate, and the algorithmic bytes against the L2's rate:
+        roof["levels"] = {
+            "l2_miss_fabric_frac": roof["frac"],
+            "mall_frac": round(roof["achieved"] / MALL_GATHER_GBS, 5),
+            "l2_frac": round(achieved_alg / L2_PEAK_GBS, 5),
+            "mall_gather_gbs": MALL_GATHER_GBS, "l2_gbs": L2_PEAK_GBS,
+            # FETCH_SIZE x 2 = 128 B per line requested past L2, checked for this kernel's access
+            # shapes (16-B streams, 128-B nodes, 80-B records, 48-B runs, 32-B partial reads) by
+            # tools/fetch_calib (profiles/r4a/fetch_calib.jsonl)
+            "fetch_correction": "x2, calibrated",
+        }
+        lv = {k: roof["levels"][k] for k in ("l2_miss_fabric_frac", "mall_frac", "l2_frac")}
+        roof["levels"]["nearest_ceiling"] = max(lv, key=lv.get)
+        rays_frame = agg["rays"] / steps  # sampler rays (k_tail's few included)
+        if rays_frame > 0:
+            roof["bytes_per_ray_past_l2"] = {"fetch": round(t["fetch_bytes_per_frame"] / rays_frame, 2),
+                                             "write": round(t["write_bytes_per_frame"] / rays_frame, 2)}
         roof["traffic_per_frame"] = t["bytes_per_frame"]
         roof["fetch_per_frame"] = t["fetch_bytes_per_frame"]
         roof["write_per_frame"] = t["write_bytes_per_frame"]

@@ -91,6 +91,12 @@ typedef struct izpi_render_tuning {
   uint32_t prim_weight;  /* k_trace2 primitive-step weight against node steps, x/16; 0 = 32 (24 with the BVH in LDS) */
   uint32_t flags;        /* IZPI_TUNE_* */
   uint64_t tail_paths;   /* k_tail takes over at <= this many paths; 0 = the resident lanes */
+  /* izpi_gpu_render_rank: longest wait for the other ranks in one collective step, in ms
+   * (the gather waits for the slowest rank's render: set it above a frame's time); past it,
+   * or when RCCL reports an asynchronous error, the communicator is aborted and the call
+   * returns IZPI_ERR_PEER. 0 = wait without a deadline (the async-error poll still runs). */
+  uint32_t peer_timeout_ms;
+  uint32_t pad_tuning;
 } izpi_render_tuning;
 enum {
   IZPI_TUNE_NO_DIST = 1,          /* k_trace2 runs each leaf's tests in its own lane */
@@ -262,10 +268,14 @@ int izpi_gpu_comm_init(izpi_ctx* ctx, uint32_t nranks, uint32_t rank, const uint
 /* Collective: every rank passes the same whole-frame request. Rank r renders the tiles
  * t % nranks == r, ncclGather moves the packed shares to rank 0, which writes the canvas
  * into out_dev (device memory on its GPU; ignored on other ranks) and applies req->post.
- * stats: this rank's share. Every rank runs the same collectives whatever fails locally,
- * and two ncclAllReduce(max) agreement steps (after the buffers, after the gather) give
- * every rank the worst status: a rank's own failure returns its status, a failure of
- * another rank IZPI_ERR_PEER (last_error names the rank). */
+ * stats: this rank's share. Every rank runs the same collectives whatever fails locally
+ * (its own HIP errors included), and two ncclAllReduce(max) agreement steps (after the
+ * buffers, after the gather) give every rank the worst status: a rank's own failure returns
+ * its status, a failure of another rank IZPI_ERR_PEER (last_error names the rank).
+ * A rank that dies or hangs instead of failing: each collective step is waited on by
+ * polling the stream and ncclCommGetAsyncError; an asynchronous RCCL error, or a wait past
+ * tuning->peer_timeout_ms, aborts the communicator (ncclCommAbort) and returns
+ * IZPI_ERR_PEER. The context then has no communicator: izpi_gpu_comm_init makes a new one. */
 int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats);
 
 /* Progress of the render running on ctx (izpi_gpu_render, _render_device, _render_rank),
@@ -278,7 +288,9 @@ int izpi_gpu_progress(izpi_ctx* ctx, uint64_t* samples_done, uint64_t* samples_t
 int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* samples_total);
 
 /* Test hook (fault injection): where = 1 makes izpi_gpu_render_rank fail this rank's local
- * checks, 2 makes every render on this context fail as a device fault would; 0 = off. */
+ * checks, 2 makes every render on this context fail as a device fault would, 3 makes this
+ * rank's stream stall before the gather as a rank waiting on a dead peer does (released
+ * once the call has given up on it); 0 = off. */
 int izpi_gpu_debug_fault(izpi_ctx* ctx, int where);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */

@@ -31,6 +31,7 @@ import (
 	"fmt"
 	"image"
 	"image/color"
+	"time"
 	"unsafe"
 
 	"github.com/flynn-nrg/floatimage/floatimage"
@@ -39,6 +40,9 @@ import (
 	"github.com/flynn-nrg/izpi/internal/sampler"
 	"github.com/flynn-nrg/izpi/internal/texture"
 	"google.golang.org/protobuf/proto"
+
+	pb "github.com/cheggaaa/pb/v3"
+	log "github.com/sirupsen/logrus"
 )
 
 // Ensure interface compliance (renderer.go:26-28).
@@ -65,6 +69,7 @@ type Options struct {
 	Seed                               uint64        // master seed of the per-sample LCG streams
 	BVH                                BVH
 	PNGPipeline                        bool          // Gamma + Clamp(1.0) on the GPU (leader.go:179-182)
+	Verbose                            bool          // progress bar while a frame renders (renderer.go:119-121)
 }
 
 // Renderer renders one frame per Render call on one MI355X (or several, Options.Devices).
@@ -79,8 +84,11 @@ type Renderer struct {
 	host  *C.izpi_host_scene
 	req   C.izpi_render_req
 	bg    *C.double // C.malloc: [75] wavelengths then [75] values of the spectral background, or nil
-	sizeX int
-	sizeY int
+	sizeX   int
+	sizeY   int
+	ndev    int    // contexts of the render (1, or len(Options.Devices))
+	verbose bool   // progress bar (Options.Verbose)
+	numRays uint64 // rays of the last Render (RendererImpl.numRays, renderer.go:213)
 }
 
 // Tile is one workUnit rectangle with inclusive bounds (renderer.go:56-70), as a
@@ -100,7 +108,7 @@ func (r *Renderer) deviceError(what string, rc C.int) error {
 // textures as loaded by the leader (filename -> ImageTxt), streamed triangles if any.
 func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 	streamed []*pb_transport.Triangle, opt Options) (*Renderer, error) {
-	r := &Renderer{sizeX: opt.SizeX, sizeY: opt.SizeY}
+	r := &Renderer{sizeX: opt.SizeX, sizeY: opt.SizeY, ndev: 1, verbose: opt.Verbose}
 	ok := false
 	defer func() {
 		if !ok {
@@ -160,6 +168,7 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 			return nil, fmt.Errorf("izpi_gpu_multi_open(%v): status %d", opt.Devices, int(rc))
 		}
 		r.ctx = C.izpi_gpu_multi_context(r.m, 0) // owned by r.m
+		r.ndev = len(opt.Devices)
 	} else if rc := C.izpi_gpu_open(C.int(opt.Device), &r.ctx); rc != 0 {
 		return nil, fmt.Errorf("izpi_gpu_open(%d): status %d", opt.Device, int(rc))
 	}
@@ -226,21 +235,77 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 	return r, nil
 }
 
-// Render mirrors RendererImpl.Render (renderer.go:108-222): the whole frame in one call.
+// Render mirrors RendererImpl.Render (renderer.go:108-222): the whole frame in one call,
+// with the reference's begin / completion log lines (the ray count is the library's
+// Sampler-call count, colour.go:38) and, when verbose, a progress bar fed by
+// izpi_gpu_progress while the call runs (the reference counts tiles, renderer.go:119-121;
+// this one counts samples).
 func (r *Renderer) Render(ctx context.Context) image.Image {
 	pix := make([]float64, r.sizeX*r.sizeY*4) // floatimage.NewFloat64NRGBA backing store (renderer.go:88)
 	req := r.req                              // C pointers only
+	st := make([]C.izpi_render_stats, r.ndev) // one per context of the fan-out
+	log.Infof("Begin rendering on %v MI355X context(s)", r.ndev)
+	startTime := time.Now()
+	done := make(chan struct{})
+	polled := make(chan struct{})
+	go r.progress(done, polled)
+	var rc C.int
 	if r.m != nil {
-		if rc := C.izpi_gpu_multi_render(r.m, &req, (*C.double)(unsafe.Pointer(&pix[0])), nil); rc != 0 {
-			panic(r.deviceError("izpi_gpu_multi_render", rc))
+		rc = C.izpi_gpu_multi_render(r.m, &req, (*C.double)(unsafe.Pointer(&pix[0])), &st[0])
+	} else {
+		rc = C.izpi_gpu_render(r.ctx, &req, (*C.double)(unsafe.Pointer(&pix[0])), &st[0])
+	}
+	close(done)
+	<-polled
+	if rc != 0 {
+		what := "izpi_gpu_render"
+		if r.m != nil {
+			what = "izpi_gpu_multi_render"
 		}
-		return floatimage.NewFloat64NRGBA(image.Rect(0, 0, r.sizeX, r.sizeY), pix)
+		log.Fatalf("%v", r.deviceError(what, rc)) // the reference log.Fatals on render errors
 	}
-	var st C.izpi_render_stats
-	if rc := C.izpi_gpu_render(r.ctx, &req, (*C.double)(unsafe.Pointer(&pix[0])), &st); rc != 0 {
-		panic(r.deviceError("izpi_gpu_render", rc)) // the reference log.Fatals on render errors
+	r.numRays = 0
+	for i := range st {
+		r.numRays += uint64(st[i].rays)
 	}
+	log.Infof("Rendering completed in %v using %v rays", time.Since(startTime), r.numRays)
 	return floatimage.NewFloat64NRGBA(image.Rect(0, 0, r.sizeX, r.sizeY), pix)
+}
+
+// NumRays is the ray count of the last Render (the figure of its completion log line).
+func (r *Renderer) NumRays() uint64 { return r.numRays }
+
+// progress polls the running render's finished samples every 200 ms into a progress bar
+// (verbose only) until done is closed, then closes polled.
+func (r *Renderer) progress(done <-chan struct{}, polled chan<- struct{}) {
+	defer close(polled)
+	if !r.verbose {
+		<-done
+		return
+	}
+	var d, t C.uint64_t
+	poll := func() {
+		if r.m != nil {
+			C.izpi_gpu_multi_progress(r.m, &d, &t)
+		} else {
+			C.izpi_gpu_progress(r.ctx, &d, &t)
+		}
+	}
+	bar := pb.Start64(int64(r.sizeX) * int64(r.sizeY) * int64(r.req.spp))
+	tick := time.NewTicker(200 * time.Millisecond)
+	defer tick.Stop()
+	for {
+		select {
+		case <-done:
+			poll()
+			bar.SetCurrent(int64(d))
+			bar.Finish()
+			return
+		case <-tick.C:
+			poll()
+			bar.SetCurrent(int64(d))
+		}
+	}
 }
 
 // RenderTiles is the worker's RenderTile (worker/render.go:17-75) for a batch of

@@ -84,7 +84,8 @@ class SceneDesc(C.Structure):
 class RenderTuning(C.Structure):
     _fields_ = [("slots", C.c_uint32), ("chunk_units", C.c_uint32), ("rec_dense", C.c_uint32),
                 ("pool_div", C.c_uint32), ("trace_chunk", C.c_uint32), ("refill_min", C.c_uint32),
-                ("prim_weight", C.c_uint32), ("flags", C.c_uint32), ("tail_paths", C.c_uint64)]
+                ("prim_weight", C.c_uint32), ("flags", C.c_uint32), ("tail_paths", C.c_uint64),
+                ("peer_timeout_ms", C.c_uint32), ("pad_tuning", C.c_uint32)]
 
 
 TUNE_NO_DIST, TUNE_GENERAL_TRACE, TUNE_NO_LEAF_SHORTCUT, TUNE_SCALAR_SLAB, TUNE_NO_TAIL, TUNE_PASS_LOG = 1, 2, 4, 8, 16, 32

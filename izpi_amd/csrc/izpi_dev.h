@@ -117,6 +117,13 @@ struct DevScene {
   uint32_t num_inner;           // GInner records
   uint32_t num_prims;           // GPrim records (and GLeaf slots, indexed by first primitive)
   izpi_camera cam;
+#ifdef IZPI_SHADOW
+  // measurement builds only (byte breakdown): copies of the traversal arrays that
+  // k_trace2 reads beside the real ones, so a class's bytes past L2 show as extra FETCH_SIZE
+  const GInner* sh_inner;
+  const GLeaf* sh_leaves;
+  const GPrim* sh_prims;
+#endif
 };
 
 struct RenderParams {

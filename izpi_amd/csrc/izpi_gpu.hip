@@ -661,6 +661,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   int clean_from = 0;     // stack entries at positions >= clean_from were pushed after the last accepted hit
   int32_t bprim = -1;
   bool fast = false;      // slab4_fast is exact for this ray
+#ifdef IZPI_SHADOW
+  // measurement: spilled stack entries stored / loaded (wave counts), and a sink for the
+  // shadow loads (bit 1: inner nodes, 2: leaf records, 4: primitives)
+  uint64_t c_spill_st = 0, c_spill_ld = 0;
+  uint32_t sh_acc = 0;
+#endif
   // wave-private range [c_pos, c_end) of the input queue; the first one is the wave's own
   uint32_t c_pos = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk);  // (uniform: SGPR)
   uint32_t c_end = c_pos + chunk < n ? c_pos + chunk : n;
@@ -784,6 +790,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           } else {
             const double2* pp = reinterpret_cast<const double2*>(sc.prims + pi);
             p0 = pp[0]; p1 = pp[1]; p2 = pp[2]; p3 = pp[3]; p4 = pp[4];
+#ifdef IZPI_SHADOW
+            if (IZPI_SHADOW & 4) {
+              const uint4* sq = reinterpret_cast<const uint4*>(sc.sh_prims + pi);
+              const uint4 s0 = sq[0], s1 = sq[1], s2 = sq[2], s3 = sq[3], s4 = sq[4];
+              sh_acc ^= s0.x ^ s1.y ^ s2.z ^ s3.w ^ s4.x;
+            }
+#endif
           }
           const double pa[9] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y, p4.x};
           double t = 0, u = 0, v = 0;
@@ -896,6 +909,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           while (sp + 3 - low > S) {
             gsp[(size_t)low * spill_stride] = stk[(low & (S - 1)) * 256];
             low++;
+#ifdef IZPI_SHADOW
+            c_spill_st++;
+#endif
           }
         }
       }
@@ -925,6 +941,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           q0 = lp[0]; q1 = lp[1];
           mnz_ = np[2]; mxx_ = np[3]; mxy_ = np[4]; mxz_ = np[5];
           ch_ = *reinterpret_cast<const int4*>(np + 6);
+#ifdef IZPI_SHADOW
+          if ((IZPI_SHADOW & 1) && !is_leaf) {
+            const uint4* sq = reinterpret_cast<const uint4*>(sc.sh_inner + cur);
+            const uint4 s0 = sq[0], s1 = sq[1], s2 = sq[2], s3 = sq[3], s4 = sq[4], s5 = sq[5], s6 = sq[6];
+            sh_acc ^= s0.x ^ s1.y ^ s2.z ^ s3.w ^ s4.x ^ s5.y ^ s6.z;
+          }
+          if ((IZPI_SHADOW & 2) && is_leaf) {
+            const uint4* sq = reinterpret_cast<const uint4*>(sc.sh_leaves + leaf_start(cur));
+            const uint4 s0 = sq[0], s1 = sq[1];
+            sh_acc ^= s0.x ^ s1.y;
+          }
+#endif
         }
         // GLeaf = (mn.x, mn.y, mn.z, mx.x), (mx.y, mx.z, start, count)
         const float4 mnx = q0;
@@ -996,6 +1024,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (do_pop && spn < low) {
           top = gsp[(size_t)spn * spill_stride];
           low = spn;
+#ifdef IZPI_SHADOW
+          c_spill_ld++;
+#endif
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, not for every pop
       }
@@ -1032,6 +1063,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     atomicAdd(counters + CNT_CLK_NODE, (unsigned long long)k_node);
     atomicAdd(counters + CNT_CLK_PRIM, (unsigned long long)k_prim);
     atomicAdd(counters + CNT_CLK_ADV, (unsigned long long)k_adv);
+  }
+#endif
+#ifdef IZPI_SHADOW
+  {
+    if (c_spill_st) atomicAdd(counters + CNT_CLK_REFILL, (unsigned long long)c_spill_st);
+    if (c_spill_ld) atomicAdd(counters + CNT_CLK_NODE, (unsigned long long)c_spill_ld);
+    if (sh_acc == 0x9E3779B9u) atomicOr(err, 0u);
   }
 #endif
   if (lane == 0) {
@@ -2536,6 +2574,8 @@ struct izpi_ctx {
   hipEvent_t evb[3 * IZPI_PASS_BATCH] = {};
   // RCCL communicator of a multi-process render (izpi_gpu_comm_init), or null
   ncclComm_t comm = nullptr;
+  // izpi_gpu_debug_fault 3: the pinned word a stalled stream waits on (null when none)
+  volatile uint32_t* stall_word = nullptr;
   uint32_t comm_rank = 0, comm_size = 1;
   int32_t* d_status = nullptr;   // agreement word of izpi_gpu_render_rank ([0] in, [1] max over ranks)
   int fault_inject = 0;          // izpi_gpu_debug_fault: 1 fail before rendering, 2 fail the render
@@ -3170,6 +3210,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
           cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL], cnt[CNT_SCLK_PUSH], cnt[CNT_SCLK_MAT], cnt[CNT_SCLK_FIN],
           cnt[CNT_SCLK_MIX], cnt[CNT_SCLK_LPDF]);
 #endif
+#ifdef IZPI_SHADOW
+  fprintf(stderr, "IZPI_SHADOW spill_stores %llu spill_loads %llu (entries)\n", cnt[CNT_CLK_REFILL], cnt[CNT_CLK_NODE]);
+#endif
 #ifdef IZPI_TRACE_CLOCKS
   fprintf(stderr, "IZPI_TRACE_CLOCKS refill %llu node %llu prim %llu advance %llu (wave cycles)\n", cnt[CNT_CLK_REFILL],
           cnt[CNT_CLK_NODE], cnt[CNT_CLK_PRIM], cnt[CNT_CLK_ADV]);
@@ -3282,7 +3325,7 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
   ok = ok && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
        hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess &&
        hipEventCreate(&ctx->ev2) == hipSuccess && hipEventCreate(&ctx->ev3) == hipSuccess &&
-       hipHostMalloc((void**)&ctx->h_count, 9 * MISC_STRIDE * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+       hipHostMalloc((void**)&ctx->h_count, (9 * MISC_STRIDE + 8) * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
        hipMalloc((void**)&ctx->d_misc, 8 * MISC_STRIDE * sizeof(uint32_t)) == hipSuccess &&
        hipMalloc((void**)&ctx->d_pool_ctr, POOL_SHARDS * POOL_CTR_STRIDE * sizeof(unsigned long long)) == hipSuccess &&
        hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) == hipSuccess;
@@ -3611,6 +3654,15 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   UP(d->spd_wavelengths, d->num_spd, &dswl);
   UP(d->spd_values, d->num_spd, &dsv);
   sc.num_inner = n_inner; sc.num_prims = d->num_prims;
+#ifdef IZPI_SHADOW
+  {
+    GInner* si; GLeaf* sl; GPrim* sp;
+    UP(inner.data(), inner.size(), &si);
+    UP(leaves.data(), leaves.size(), &sl);
+    UP(prims.data(), prims.size(), &sp);
+    sc.sh_inner = si; sc.sh_leaves = sl; sc.sh_prims = sp;
+  }
+#endif
   sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tritex = dtt; sc.lights = dlt; sc.materials = dm;
   sc.mat_const = dmc; sc.mat_tex = dmt; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
@@ -4004,15 +4056,69 @@ namespace {
 // Agreement step of a multi-rank render: every rank contributes (status << 16 | rank) and
 // all receive the maximum, i.e. the worst status and the highest rank that had it
 // (ncclAllReduce(max), rccl.h). Returns non-zero only if the collective itself failed.
-int agree_status(izpi_ctx* ctx, int local, int* worst_status, uint32_t* worst_rank) {
+// Device-side stall of the fault-injection hook (izpi_gpu_debug_fault 3): one thread spins
+// until the host sets *release (a mapped pinned word), as a stream stuck in a collective on
+// a dead peer does; bounded (about 60 s of clock) so that the grid always drains.
+__global__ void k_stall(const volatile uint32_t* release) {
+  const uint64_t t0 = __builtin_readcyclecounter();
+  while (__atomic_load_n(release, __ATOMIC_RELAXED) == 0u && __builtin_readcyclecounter() - t0 < (1ull << 37))
+    __builtin_amdgcn_s_sleep(100);
+}
+
+// Wait for this context's stream (a collective step) as a rank that may outlive its peers:
+// poll the stream and the communicator's asynchronous error; an RCCL error or a wait past
+// the deadline aborts the communicator and returns IZPI_ERR_PEER (render/remote.go:40-55
+// logs a failed remote tile and carries on; here the call returns instead of hanging).
+int wait_peers(izpi_ctx* ctx, uint32_t timeout_ms, const char* step) {
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t naps = 0;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(ctx->stream);
+    if (q == hipSuccess) return IZPI_OK;
+    if (q != hipErrorNotReady) { ctx->err = std::string(step) + ": " + hipGetErrorString(q); return IZPI_ERR_HIP; }
+    ncclResult_t ae = ncclSuccess;
+    const ncclResult_t qr = ncclCommGetAsyncError(ctx->comm, &ae);
+    const bool failed = qr != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (failed || (timeout_ms && ms > timeout_ms)) {
+      ctx->err = std::string(step) + (failed ? ": RCCL reported " + std::string(ncclGetErrorString(qr != ncclSuccess ? qr : ae))
+                                             : ": no answer from the other ranks within " + std::to_string(timeout_ms) + " ms") +
+                 "; communicator aborted";
+      (void)ncclCommAbort(ctx->comm);
+      ctx->comm = nullptr;
+      if (ctx->stall_word) { *ctx->stall_word = 1u; ctx->stall_word = nullptr; }  // test hook: let the stall drain
+      (void)hipStreamSynchronize(ctx->stream);
+      return IZPI_ERR_PEER;
+    }
+    // sub-millisecond polls at first (a collective normally completes in microseconds),
+    // then 1 ms naps for a gather that waits on the slowest rank's render
+    std::this_thread::sleep_for(std::chrono::microseconds(naps++ < 200 ? 20 : 1000));
+  }
+}
+
+// Agree on the worst status over all ranks. The collective is issued whatever failed
+// locally before it (a failed staging copy only makes this rank's word stale), so that no
+// rank is left waiting in it; a local HIP error is reported after the collective.
+int agree_status(izpi_ctx* ctx, int local, uint32_t timeout_ms, int* worst_status, uint32_t* worst_rank) {
   const int32_t word = (int32_t)((uint32_t)std::min(local, 0x7FFF) << 16 | (ctx->comm_rank & 0xFFFFu));
   int32_t* h = (int32_t*)ctx->h_count + 8 * MISC_STRIDE;  // pinned scratch
   h[0] = word;
-  HIP_TRY(hipMemcpyAsync(ctx->d_status, h, sizeof(word), hipMemcpyHostToDevice, ctx->stream));
+  h[1] = word;  // this rank's own word, should the collective's copy-back fail
+  const hipError_t e1 = hipMemcpyAsync(ctx->d_status, h, sizeof(word), hipMemcpyHostToDevice, ctx->stream);
   const ncclResult_t r = ncclAllReduce(ctx->d_status, ctx->d_status + 1, 1, ncclInt32, ncclMax, ctx->comm, ctx->stream);
-  if (r != ncclSuccess) { ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r); return IZPI_ERR_HIP; }
-  HIP_TRY(hipMemcpyAsync(h + 1, ctx->d_status + 1, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (r != ncclSuccess) {
+    ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r) + "; communicator aborted";
+    (void)ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
+    return IZPI_ERR_PEER;
+  }
+  const hipError_t e2 = hipMemcpyAsync(h + 1, ctx->d_status + 1, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
+  const int rc = wait_peers(ctx, timeout_ms, "status agreement");
+  if (rc) return rc;
+  if (e1 != hipSuccess || e2 != hipSuccess) {
+    ctx->err = std::string("status agreement: ") + hipGetErrorString(e1 != hipSuccess ? e1 : e2);
+    return IZPI_ERR_HIP;
+  }
   const int32_t out = h[1];
   *worst_status = (int)((uint32_t)out >> 16);
   *worst_rank = (uint32_t)out & 0xFFFFu;
@@ -4042,33 +4148,49 @@ int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_
   if (!ctx->comm || !ctx->d_status) { ctx->err = "render_rank before izpi_gpu_comm_init"; return IZPI_ERR_INVALID; }
   memset(&ctx->last, 0, sizeof(ctx->last));
   if (stats) *stats = ctx->last;
-  HIP_TRY(hipSetDevice(ctx->device));
-  // ---- 1
+  const uint32_t timeout_ms = tuning_of(req).peer_timeout_ms;
+  // ---- 1 (local failures, HIP ones included, are recorded and agreed on, not returned early)
   Shares sh;
   int prc = IZPI_OK;
-  if (ctx->comm_rank == 0 && !out_dev) { ctx->err = "rank 0 needs an output canvas"; prc = IZPI_ERR_INVALID; }
+  const hipError_t de = hipSetDevice(ctx->device);
+  if (de != hipSuccess) { ctx->err = std::string("hipSetDevice: ") + hipGetErrorString(de); prc = IZPI_ERR_HIP; }
+  else if (ctx->comm_rank == 0 && !out_dev) { ctx->err = "rank 0 needs an output canvas"; prc = IZPI_ERR_INVALID; }
   else if (req && req->post != IZPI_POST_NONE && req->num_tiles != 0) { ctx->err = "post-processing needs a whole-frame request"; prc = IZPI_ERR_INVALID; }
   if (!prc) prc = make_shares(ctx, req, ctx->comm_size, sh);
   if (!prc) prc = grow(ctx, (void**)&ctx->d_share, &ctx->share_cap, sh.block * sizeof(double));
   if (!prc && ctx->comm_rank == 0) prc = grow(ctx, (void**)&ctx->d_gather, &ctx->gather_cap, (size_t)ctx->comm_size * sh.block * sizeof(double));
   if (prc == IZPI_OK && ctx->fault_inject == 1) { ctx->err = "injected fault before rendering"; prc = IZPI_ERR_DEVICE; }
+  const std::string local_err = ctx->err;
   int worst = 0;
   uint32_t wr = 0;
-  int rc = agree_status(ctx, prc, &worst, &wr);
+  int rc = agree_status(ctx, prc, timeout_ms, &worst, &wr);
   if (rc) return rc;
-  if (prc) return prc;
+  if (prc) { ctx->err = local_err; return prc; }
   if (worst) return peer_failure(ctx, worst, wr, "before rendering");
-  // ---- 2
-  const int rrc = render_share(ctx, req, sh, ctx->comm_rank);
+  // ---- 2 (a failed share posts a zeroed block: the gather runs on every rank)
+  int rrc = render_share(ctx, req, sh, ctx->comm_rank);
   if (stats) *stats = ctx->last;
   if (rrc) (void)hipMemsetAsync(ctx->d_share, 0, sh.block * sizeof(double), ctx->stream);
+  if (ctx->fault_inject == 3) {  // test hook: this rank's stream stalls as on a dead peer
+    ctx->stall_word = (volatile uint32_t*)((uint32_t*)ctx->h_count + 8 * MISC_STRIDE + 4);  // beside agree_status's two words
+    *ctx->stall_word = 0u;
+    hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, ctx->stream, (const volatile uint32_t*)ctx->stall_word);
+  }
   // ncclGather (rccl.h:745): block r of the root's buffer = rank r's packed share
   const ncclResult_t r = ncclGather(ctx->d_share, ctx->comm_rank == 0 ? ctx->d_gather : nullptr, sh.block, ncclFloat64, 0,
                                     ctx->comm, ctx->stream);
-  if (r != ncclSuccess) { ctx->err = std::string("ncclGather: ") + ncclGetErrorString(r); return IZPI_ERR_HIP; }
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  if ((rc = agree_status(ctx, rrc, &worst, &wr))) return rc;
-  if (rrc) return rrc;
+  if (r != ncclSuccess) {  // the peers may already wait in the gather: abort rather than leave them there
+    ctx->err = std::string("ncclGather: ") + ncclGetErrorString(r) + "; communicator aborted";
+    (void)ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
+    if (ctx->stall_word) { *ctx->stall_word = 1u; ctx->stall_word = nullptr; }
+    (void)hipStreamSynchronize(ctx->stream);
+    return IZPI_ERR_PEER;
+  }
+  if ((rc = wait_peers(ctx, timeout_ms, "share gather"))) return rc;
+  const std::string share_err = ctx->err;
+  if ((rc = agree_status(ctx, rrc, timeout_ms, &worst, &wr))) return rc;
+  if (rrc) { ctx->err = share_err; return rrc; }
   if (worst) return peer_failure(ctx, worst, wr, "while rendering its share");
   // ---- 3
   if (ctx->comm_rank == 0 && (rc = assemble(ctx, req, sh, out_dev))) return rc;

@@ -13,7 +13,8 @@ import pytest
 
 from izpi_amd import _native as N
 from izpi_amd import build, configs, ingest
-from izpi_amd.renderer import GPURenderer
+from izpi_amd.renderer import GPURenderer, gpu_leaf_max
+from oracle import oracle as O
 
 ROOT = Path(__file__).resolve().parents[1]
 EXAMPLE = ROOT / "izpi_amd" / "data" / "scenes" / "cornell_box_transparent_pyramid_spectral.pbtxt"
@@ -51,8 +52,36 @@ def test_go_shim_call_sequence_bitwise(gpu, tmp_path, which, png, devices):
     post = (N.POST_SPECTRAL if which == "spectral" else N.POST_NONE) | (N.POST_GAMMA_CLAMP if png else 0)
     r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu")
     want = r.render(post=post)
+    leaf_max, exposure = gpu_leaf_max(r.host.desc), r.exposure
     r.close()
     assert got.tobytes() == want.tobytes()
+    # and the CPU oracle on the same (GPU-built) tree, with Render's post-processing
+    assert got.tobytes() == _oracle_frame(s, 40, 40, 4, leaf_max, exposure, png).tobytes()
+
+
+def _oracle_frame(s, W, H, spp, leaf_max, exposure, png, bg=None):
+    """The oracle's Render() of scene s on the PLOC + surface-area tree (O.lbvh4 restates
+    the GPU builder node for node): the sampler, then FireflyRejection + XYZToRGB for the
+    Spectral sampler (renderer.go:215-219), then Gamma + Clamp(1) for the png pipeline."""
+    o = O.OracleScene(s, aspect_override=W / H)
+    nodes, order = O.lbvh4(o.prim_boxes(), leaf_max, N.BVH_PLOC_SAH)
+    o.set_bvh(nodes, order)
+    req = N.RenderReq(width=W, height=H, spp=spp, max_depth=50, sampler=s.sampler, seed=12345)
+    keep = []
+    if bg is not None:
+        wl, val = (np.ascontiguousarray(x, np.float64) for x in bg)
+        keep += [wl, val]
+        req.num_bg_spd = len(wl)
+        req.bg_spd_wavelengths = O.dptr(wl)
+        req.bg_spd_values = O.dptr(val)
+    canvas, _ = o.render(req, threads=8)
+    o.close()
+    canvas = canvas.reshape(-1)
+    if s.sampler == N.SAMPLER_SPECTRAL:
+        canvas = O.xyz_to_rgb(O.firefly(canvas, W, H), W, H, exposure)
+    if png:
+        canvas = O.postprocess(canvas, W, H, [(N.FILTER_GAMMA, 0.0), (N.FILTER_CLAMP, 1.0)])
+    return np.asarray(canvas).reshape(H, W, 4)
 
 
 @pytest.mark.gpu
@@ -68,8 +97,10 @@ def test_go_shim_spectral_black_background_bitwise(gpu, tmp_path, devices):
     wl = 380.0 + 5.0 * np.arange(75)
     r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", spectral_background=(wl, np.zeros(75)))
     want = r.render(post=N.POST_SPECTRAL)
+    leaf_max, exposure = gpu_leaf_max(r.host.desc), r.exposure
     r.close()
     assert got.tobytes() == want.tobytes()
+    assert got.tobytes() == _oracle_frame(s, 40, 40, 4, leaf_max, exposure, False, bg=(wl, np.zeros(75))).tobytes()
 
 
 @pytest.mark.gpu

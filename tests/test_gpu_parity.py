@@ -618,6 +618,45 @@ def test_render_rank_failures_return_without_hanging(gpu):
     r.close()
 
 
+def test_render_rank_stalled_peer_hits_the_deadline(gpu):
+    """A rank whose collective never completes (izpi_gpu_debug_fault 3 stalls this rank's
+    stream before the gather, as a dead peer leaves it): with tuning.peer_timeout_ms the call
+    polls the stream and ncclCommGetAsyncError, aborts the communicator past the deadline
+    and returns IZPI_ERR_PEER instead of hanging; after a new izpi_gpu_comm_init the context
+    renders bit-exact again."""
+    import ctypes as C
+    import time
+    import torch
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 64, 64, 4)
+    L = N.lib()
+    cid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    assert L.izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    canvas = torch.zeros((64, 64, 4), dtype=torch.float64, device="cuda:0")
+    req = r.request()
+    tu = N.tuning(peer_timeout_ms=300)
+    req.tuning = C.pointer(tu)
+    st = N.RenderStats()
+    assert L.izpi_gpu_debug_fault(r.ctx, 3) == 0
+    t0 = time.time()
+    rc = L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st))
+    dt = time.time() - t0
+    assert rc == N.IZPI_ERR_PEER, (rc, L.izpi_gpu_last_error(r.ctx))
+    assert b"no answer from the other ranks within 300 ms" in L.izpi_gpu_last_error(r.ctx)
+    assert dt < 20.0, dt
+    assert L.izpi_gpu_debug_fault(r.ctx, 0) == 0
+    # the communicator is gone: the next call says so at once
+    assert L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st)) == N.IZPI_ERR_INVALID
+    assert L.izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    assert L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st)) == 0
+    torch.cuda.synchronize()
+    ref, _ = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(canvas.cpu().numpy(), ref)
+    r.close()
+
+
 def test_multi_render_device_failure_is_reported(gpu):
     """izpi_gpu_multi_render with one failing device (a render fault injected on context 1,
     then a context without a scene): the call returns that device's status and names it,
