@@ -2576,6 +2576,7 @@ struct izpi_ctx {
   ncclComm_t comm = nullptr;
   // izpi_gpu_debug_fault 3: the pinned word a stalled stream waits on (null when none)
   volatile uint32_t* stall_word = nullptr;
+  uint32_t* stall_host = nullptr;  // its allocation (coherent pinned host memory)
   uint32_t comm_rank = 0, comm_size = 1;
   int32_t* d_status = nullptr;   // agreement word of izpi_gpu_render_rank ([0] in, [1] max over ranks)
   int fault_inject = 0;          // izpi_gpu_debug_fault: 1 fail before rendering, 2 fail the render
@@ -3325,7 +3326,7 @@ int izpi_gpu_open(int device, izpi_ctx** out) {
   ok = ok && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
        hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess &&
        hipEventCreate(&ctx->ev2) == hipSuccess && hipEventCreate(&ctx->ev3) == hipSuccess &&
-       hipHostMalloc((void**)&ctx->h_count, (9 * MISC_STRIDE + 8) * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+       hipHostMalloc((void**)&ctx->h_count, 9 * MISC_STRIDE * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
        hipMalloc((void**)&ctx->d_misc, 8 * MISC_STRIDE * sizeof(uint32_t)) == hipSuccess &&
        hipMalloc((void**)&ctx->d_pool_ctr, POOL_SHARDS * POOL_CTR_STRIDE * sizeof(unsigned long long)) == hipSuccess &&
        hipMalloc((void**)&ctx->d_counters, CNT_N * sizeof(unsigned long long)) == hipSuccess;
@@ -3350,6 +3351,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
                   ctx->d_gather, ctx->d_status, ctx->d_cpart};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
+  if (ctx->stall_host) (void)hipHostFree(ctx->stall_host);
   for (int i = 0; i < 3 * IZPI_PASS_BATCH; i++) if (ctx->evb[i]) (void)hipEventDestroy(ctx->evb[i]);
   hipEvent_t evs[] = {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3};
   for (hipEvent_t ev : evs) if (ev) (void)hipEventDestroy(ev);
@@ -4057,11 +4059,11 @@ namespace {
 // all receive the maximum, i.e. the worst status and the highest rank that had it
 // (ncclAllReduce(max), rccl.h). Returns non-zero only if the collective itself failed.
 // Device-side stall of the fault-injection hook (izpi_gpu_debug_fault 3): one thread spins
-// until the host sets *release (a mapped pinned word), as a stream stuck in a collective on
-// a dead peer does; bounded (about 60 s of clock) so that the grid always drains.
+// until the host sets *release (a coherent pinned word), as a stream stuck in a collective
+// on a dead peer does; bounded (about 7 s of clock) so that the grid always drains.
 __global__ void k_stall(const volatile uint32_t* release) {
   const uint64_t t0 = __builtin_readcyclecounter();
-  while (__atomic_load_n(release, __ATOMIC_RELAXED) == 0u && __builtin_readcyclecounter() - t0 < (1ull << 37))
+  while (__atomic_load_n(release, __ATOMIC_RELAXED) == 0u && __builtin_readcyclecounter() - t0 < (1ull << 34))
     __builtin_amdgcn_s_sleep(100);
 }
 
@@ -4084,9 +4086,11 @@ int wait_peers(izpi_ctx* ctx, uint32_t timeout_ms, const char* step) {
       ctx->err = std::string(step) + (failed ? ": RCCL reported " + std::string(ncclGetErrorString(qr != ncclSuccess ? qr : ae))
                                              : ": no answer from the other ranks within " + std::to_string(timeout_ms) + " ms") +
                  "; communicator aborted";
+      // test hook: let the stall drain first (ncclCommAbort waits for the operations it
+      // aborts, which sit behind it on the stream)
+      if (ctx->stall_word) { *ctx->stall_word = 1u; ctx->stall_word = nullptr; }
       (void)ncclCommAbort(ctx->comm);
       ctx->comm = nullptr;
-      if (ctx->stall_word) { *ctx->stall_word = 1u; ctx->stall_word = nullptr; }  // test hook: let the stall drain
       (void)hipStreamSynchronize(ctx->stream);
       return IZPI_ERR_PEER;
     }
@@ -4172,18 +4176,24 @@ int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_
   if (stats) *stats = ctx->last;
   if (rrc) (void)hipMemsetAsync(ctx->d_share, 0, sh.block * sizeof(double), ctx->stream);
   if (ctx->fault_inject == 3) {  // test hook: this rank's stream stalls as on a dead peer
-    ctx->stall_word = (volatile uint32_t*)((uint32_t*)ctx->h_count + 8 * MISC_STRIDE + 4);  // beside agree_status's two words
-    *ctx->stall_word = 0u;
-    hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, ctx->stream, (const volatile uint32_t*)ctx->stall_word);
+    // the release word is fine-grained (coherent) host memory: the spinning kernel sees
+    // the host's store while it runs
+    if (!ctx->stall_host && hipHostMalloc((void**)&ctx->stall_host, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      ctx->stall_host = nullptr;
+    if (ctx->stall_host) {
+      ctx->stall_word = ctx->stall_host;
+      *ctx->stall_word = 0u;
+      hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, ctx->stream, (const volatile uint32_t*)ctx->stall_word);
+    }
   }
   // ncclGather (rccl.h:745): block r of the root's buffer = rank r's packed share
   const ncclResult_t r = ncclGather(ctx->d_share, ctx->comm_rank == 0 ? ctx->d_gather : nullptr, sh.block, ncclFloat64, 0,
                                     ctx->comm, ctx->stream);
   if (r != ncclSuccess) {  // the peers may already wait in the gather: abort rather than leave them there
     ctx->err = std::string("ncclGather: ") + ncclGetErrorString(r) + "; communicator aborted";
+    if (ctx->stall_word) { *ctx->stall_word = 1u; ctx->stall_word = nullptr; }
     (void)ncclCommAbort(ctx->comm);
     ctx->comm = nullptr;
-    if (ctx->stall_word) { *ctx->stall_word = 1u; ctx->stall_word = nullptr; }
     (void)hipStreamSynchronize(ctx->stream);
     return IZPI_ERR_PEER;
   }

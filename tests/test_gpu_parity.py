@@ -234,6 +234,7 @@ def test_queue_keeps_every_slot_while_units_remain(gpu, name, capfd):
                                   {"flags": N.TUNE_NO_TAIL}, {"flags": N.TUNE_NO_TAIL, "slots": 3000},
                                   {"tail_paths": 100},
                                   {"flags": N.TUNE_GENERAL_TRACE}, {"flags": N.TUNE_NO_RAY_LDS},
+                                  {"trace_chunk": 16, "refill_min": 64},
                                   {"rec_dense": 1, "pool_div": 100000},
                                   {"rec_dense": 2, "pool_div": 100000, "flags": N.TUNE_NO_TAIL},
                                   {"rec_dense": 50}])
@@ -644,7 +645,7 @@ def test_render_rank_stalled_peer_hits_the_deadline(gpu):
     dt = time.time() - t0
     assert rc == N.IZPI_ERR_PEER, (rc, L.izpi_gpu_last_error(r.ctx))
     assert b"no answer from the other ranks within 300 ms" in L.izpi_gpu_last_error(r.ctx)
-    assert dt < 20.0, dt
+    assert dt < 5.0, dt  # the deadline, not the stall's own bound (~7 s), ended the wait
     assert L.izpi_gpu_debug_fault(r.ctx, 0) == 0
     # the communicator is gone: the next call says so at once
     assert L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st)) == N.IZPI_ERR_INVALID
