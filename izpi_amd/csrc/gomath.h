@@ -255,6 +255,17 @@ IZPI_HD double pow(double x, double y) {
     const double ax = abs(x);
     if (ax >= 0x1p-511 || ax == 0) return x * x;  // (NaN: Go returns its own NaN bits, below)
   }
+  // Pow(x, 5) (PBR's Schlick term, pbr.go:102): the loop takes frexp's mantissa m and makes
+  // a1 = m, x1 = rn(m*m), x1 = rn(x1*x1), a1 = rn(a1*x1) with exact doublings in between,
+  // then ldexp: the same roundings as x * ((x*x) * (x*x)) whenever x^2, x^4 and x^5 are
+  // normal numbers (2^-204 <= |x| <= 2^204), and the same signed zero for x = +-0
+  if (y == 5.0) {
+    const double ax = abs(x);
+    if ((ax >= 0x1p-204 && ax <= 0x1p+204) || ax == 0) {
+      const double x2 = x * x, x4 = x2 * x2;
+      return x * x4;
+    }
+  }
   if (y == 0 || x == 1) return 1;
   if (y == 1) return x;
   if (is_nan(x) || is_nan(y)) return nan();

@@ -436,7 +436,19 @@ struct PathSt {               // register form
   double lambda, lpdf;        // wavelength and its pdf (spectral)
   double pend[3];             // dielectric hit point while its path-length ray is traced
   uint32_t rng, depth, unit, rslot, blk;
+  uint32_t zf;                // ZF_*: what unwinding its records does to a zero radiance (finish)
 };
+// What the unwinding of a path's records (finish) makes of a terminal radiance of +0, kept
+// up to date as the records are written (rec_zero_track), so that finish can skip the
+// record reads for such paths (open-box escapes, max depth into a black background):
+//   ZF_UNSAFE: some level may turn a zero into a non-zero or a NaN (an infinite or NaN
+//              attenuation or scattering pdf, or a pdf of 0 or NaN);
+//   ZF_RESET:  a non-specular level was written: 0.0 + (att * (L * s)) / p maps +-0 to +0,
+//              so the levels written after it (applied before it) cannot change the sign;
+//   ZF_SIGN:   bit c = the sign of component c after unwinding a +0: the XOR of the
+//              attenuation signs of the specular levels below the first non-specular one.
+// Stored in the high half of PathHot::depth.
+enum : uint32_t { ZF_UNSAFE = 1, ZF_RESET = 2, ZF_SIGN_SHIFT = 2 };
 // rslot: the path's record slot; blk: 1 + the overflow record block holding its
 // unwinding records at depths >= ShadeParams::rec_dense (0 = none yet), see pool_alloc.
 struct alignas(16) PathHot { uint32_t rng, depth, unit, rslot; };
@@ -1372,6 +1384,22 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
   rp[RecLayout<SAMPLER, MATSET>::S] = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
 }
 IZPI_DEV bool rec_is_spec(double s) { return (uint64_t)__double_as_longlong(s) == REC_SPEC_BITS; }
+// Update P.zf (ZF_*) for the record of the level being written: attenuation att (colour
+// xyz, spectral x), and for a non-specular level its scattering pdf s and pdf p.
+template <int SAMPLER>
+IZPI_DEV void rec_zero_track(uint32_t& zf, bool spec, V3 att, double s, double p) {
+  const bool colour = SAMPLER == IZPI_SAMPLER_COLOUR;
+  bool ok = isfinite(att.x) && (!colour || (isfinite(att.y) && isfinite(att.z)));
+  if (!spec) ok = ok && isfinite(s) && p != 0.0 && !isnan(p);
+  if (!ok) zf |= ZF_UNSAFE;
+  if (zf & ZF_RESET) return;
+  if (spec) {
+    zf ^= (signbit(att.x) ? 1u : 0u) << ZF_SIGN_SHIFT;
+    if (colour) zf ^= ((signbit(att.y) ? 2u : 0u) | (signbit(att.z) ? 4u : 0u)) << ZF_SIGN_SHIFT;
+  } else {
+    zf |= ZF_RESET;
+  }
+}
 
 // The materials' constant RGB values (DevScene::mat_const) and texture slots (mt_lds)
 // staged in LDS by k_shade and k_tail when there are at most MC_LDS materials: the compact
@@ -1429,6 +1457,16 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
     out[0] = 0.0; out[1] = 0.0; out[2] = 0.0;
     return;
   }
+  // A terminal radiance of +0 through levels that all keep a zero a zero (P.zf): the
+  // unwinding ends in a signed zero per component that zf already holds, so the records
+  // need not be read (C5 / C4: paths escaping the box or ending at max depth into a black
+  // background; the levels' arithmetic on +-0 is exact: see ZF_*)
+  const bool zero_term = gm::bits(L.x) == 0 && (SAMPLER != IZPI_SAMPLER_COLOUR || (gm::bits(L.y) == 0 && gm::bits(L.z) == 0));
+  const bool skip = zero_term && !(P.zf & ZF_UNSAFE);
+  if (skip) {
+    const uint32_t sg = P.zf >> ZF_SIGN_SHIFT;
+    L = mk((sg & 1u) ? -0.0 : 0.0, (sg & 2u) ? -0.0 : 0.0, (sg & 4u) ? -0.0 : 0.0);
+  }
   // The records are read four levels at a time (one batch of independent loads, then
   // the levels applied in order), so a path of depth d waits ~d/4 memory round trips.
   constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
@@ -1439,7 +1477,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
 #else
   constexpr int RB = IZPI_FIN_RB;
 #endif
-  for (int dd = (int)P.depth - 1; dd >= 0; dd -= RB) {
+  for (int dd = skip ? -1 : (int)P.depth - 1; dd >= 0; dd -= RB) {
     double rv[RB][D];
     if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {
       // (material, s, p): the attenuation is the material's constant albedo
@@ -1555,6 +1593,7 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
   cam.s = (uint32_t)splitmix64(sp.seed ^ key ^ IZPI_CAMERA_STREAM_SALT);
   P.unit = unit;
   P.depth = 0;
+  P.zf = 0;
   P.blk = 0;
   P.lambda = 0;
   P.lpdf = 1;
@@ -1608,7 +1647,7 @@ IZPI_DEV void store_entry(const WaveBuf& b, uint32_t pos, const PathSt& P, const
   r[2] = make_double2(R.d[1], R.d[2]);
   b.kind[pos] = R.kind;
   if (b.time) b.time[pos] = R.time;
-  b.path[pos] = PathHot{P.rng, P.depth, P.unit, P.rslot};
+  b.path[pos] = PathHot{P.rng, P.depth | P.zf << 16, P.unit, P.rslot};
   if (b.blk) b.blk[pos] = P.blk;
   if (b.cold) {
     double2* c = reinterpret_cast<double2*>(b.cold + pos);
@@ -1646,7 +1685,7 @@ IZPI_DEV void load_entry(const WaveBuf& b, uint32_t i, EntryIn& E) {
 template <int SAMPLER>
 IZPI_DEV void load_path(const WaveBuf& b, uint32_t i, PathSt& P) {
   const PathHot ph = b.path[i];
-  P.rng = ph.rng; P.depth = ph.depth; P.unit = ph.unit; P.rslot = ph.rslot;
+  P.rng = ph.rng; P.depth = ph.depth & 0xFFFFu; P.zf = ph.depth >> 16; P.unit = ph.unit; P.rslot = ph.rslot;
   P.blk = b.blk ? b.blk[i] : 0u;
   P.lambda = 0; P.lpdf = 1;
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { const double2 c = *reinterpret_cast<const double2*>(b.cold + i); P.lambda = c.x; P.lpdf = c.y; }
@@ -1717,7 +1756,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
 // `unit_want` lanes get consecutive output entries, `put` lanes first. A granted lane
 // whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
 IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
-                             uint32_t& pos, uint32_t& parity, bool& exhausted) {
+                             uint32_t& pos, uint32_t& parity, bool& exhausted, uint32_t key = 0) {
   __shared__ uint32_t s_p[2][SHADE_WAVES], s_u[2][SHADE_WAVES];
   __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2], s_nent[2];
   const uint32_t b = parity;
@@ -1726,6 +1765,17 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   const uint64_t lt = (1ull << lane) - 1;
   const uint64_t mp = __ballot(put), mu = __ballot(unit_want);
   if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); }
+#ifdef IZPI_SORT_OCT
+  // experiment: the block's continuing paths grouped by `key` in its output range
+  __shared__ uint32_t s_k[2][SHADE_WAVES][8];
+  uint64_t mine = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; k++) {
+    const uint64_t m = __ballot(put && key == k);
+    if (lane == 0) s_k[b][w][k] = (uint32_t)__popcll(m);
+    if (key == k) mine = m;
+  }
+#endif
   __syncthreads();
   if (threadIdx.x == 0) {
     // both atomics in flight together: entries are reserved for every unit_want lane
@@ -1750,6 +1800,16 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   __syncthreads();
   uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
   for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
+#ifdef IZPI_SORT_OCT
+  if (put) {
+    uint32_t off = (uint32_t)__popcll(mine & lt);
+    for (uint32_t i = 0; i < SHADE_WAVES; i++) {
+      for (uint32_t k = 0; k < key; k++) off += s_k[b][i][k];
+      if (i < w) off += s_k[b][i][key];
+    }
+    pr = off;
+  }
+#endif
   const bool has_entry = unit_want && s_nput[b] + ur < s_nent[b];
   const bool granted = unit_want && ur < s_granted[b];
   unit = granted ? s_ubase[b] + ur : 0xFFFFFFFFu;
@@ -2020,9 +2080,11 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         const double pdf_val = 0.5 * lights_pdf(sc, st, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         SCLK_ADD(SCLK_LPDF, sc3);
         rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
+        if constexpr (ms_spec(MATSET) || SAMPLER == IZPI_SAMPLER_SPECTRAL) rec_zero_track<SAMPLER>(P.zf, false, att, spdf, pdf_val);
         next_d = dir;
       } else {
         rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, true, att, 0, rec_mat);
+        rec_zero_track<SAMPLER>(P.zf, true, att, 0.0, 0.0);
       }
       SCLK_ADD(SCLK_MIX, sc2);
       P.depth++;
@@ -2129,7 +2191,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 #endif
     PathSt P;
     RayRec R;
-    P.rslot = 0; P.blk = 0; P.depth = 0;
+    P.rslot = 0; P.blk = 0; P.depth = 0; P.zf = 0;
     uint32_t kind = RAY_DEAD;
     EntryIn E;
     if (valid) {
@@ -2158,7 +2220,12 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     // one reservation phase: output entries for continuing and parked paths, new units
     // (and their entries) for finished ones
     uint32_t unit, pos;
+#ifdef IZPI_SORT_OCT
+    const uint32_t okey = push ? ((R.d[0] < 0 ? 1u : 0u) | (R.d[1] < 0 ? 2u : 0u) | (R.d[2] < 0 ? 4u : 0u)) : 0u;
+    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, okey);
+#else
     block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted);
+#endif
     if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
     if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS

@@ -108,6 +108,29 @@ def pow_square_inputs():
     return x, np.full_like(x, 2.0)
 
 
+def pow_fifth_inputs():
+    """x across the whole exponent range (the 2^-204 / 2^204 edges of pow's x^5 shortcut,
+    subnormal and overflowing fifth powers, the signed zeros) with y = 5."""
+    rng = np.random.default_rng(7)
+    k = np.arange(-1074, 1024)
+    x = np.ldexp(rng.uniform(1, 2, k.size), k) * np.where(rng.random(k.size) < 0.5, -1, 1)
+    lo, hi = np.ldexp(1.0, -204), np.ldexp(1.0, 204)
+    u = rng.uniform(0, 1, 4000)  # PBR's 1 - cos(theta)
+    x = np.concatenate([x, u, 1 - u, [lo, np.nextafter(lo, 0), np.nextafter(lo, 1), -lo, hi, np.nextafter(hi, 0),
+                                       np.nextafter(hi, 1e308), -hi, 5e-324, 0.0, -0.0, 1.0, -1.0,
+                                       float("inf"), float("-inf"), float("nan")]])
+    return x, np.full_like(x, 5.0)
+
+
+def test_pow_fifth_shortcut_bitwise():
+    """gomath.h's Pow(x, 5) shortcut equals the oracle's restatement of pow.go's loop."""
+    L = N.lib()
+    for a, b in zip(*pow_fifth_inputs()):
+        p = L.izpi_host_gomath(OPS["pow"], float(a), float(b))
+        o = O.gomath(OPS["pow"], float(a), float(b))
+        assert struct.pack("<d", p) == struct.pack("<d", o), (a, p, o)
+
+
 def test_pow_square_shortcut_bitwise():
     """gomath.h's Pow(x, 2) shortcut (x * x outside the subnormal-square range) equals the
     oracle's restatement of pow.go's loop on every binade."""

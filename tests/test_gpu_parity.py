@@ -56,11 +56,12 @@ def assert_parity(gpu_img, ora_img, gstats=None, ostats=None):
 
 
 def test_gomath_device_bitwise(gpu):
-    from tests.test_gomath import OPS, inputs, pow_square_inputs
+    from tests.test_gomath import OPS, inputs, pow_fifth_inputs, pow_square_inputs
     r = GPURenderer(configs.cornell_rgb(), 8, 8, 1)
     L = N.lib()
-    for name, op in list(OPS.items()) + [("pow2", OPS["pow"])]:
-        x, y = pow_square_inputs() if name == "pow2" else inputs(name, n=20000, seed=3)
+    for name, op in list(OPS.items()) + [("pow2", OPS["pow"]), ("pow5", OPS["pow"])]:
+        x, y = (pow_square_inputs() if name == "pow2" else pow_fifth_inputs() if name == "pow5"
+                else inputs(name, n=20000, seed=3))
         x = np.ascontiguousarray(x, np.float64)
         y = np.ascontiguousarray(y, np.float64)
         out = np.zeros_like(x)

@@ -216,3 +216,28 @@ def test_pbr_texture_storage_forms_bitwise(gpu):
     ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
+
+
+@pytest.mark.parametrize("albedo", [(-0.5, 0.7, -0.0), (0.9, float("inf"), 0.4), (-0.0, -0.0, -0.0)])
+def test_zero_radiance_unwinding_signs_bitwise(gpu, albedo):
+    """finish skips the record reads of a path whose terminal radiance is +0 when every
+    level keeps a zero a zero (ZF_*): the sign each component ends with comes from the
+    specular levels' attenuation signs below the first non-specular level. Metal spheres
+    with negative, -0 and infinite albedo components (an infinite attenuation turns the
+    zero into a NaN: those paths must unwind their records), glass, and an open box whose
+    escaping paths meet the black background: bit-exact against the oracle's unwinding."""
+    s = Scene("zero_signs")
+    mats = configs.rgb_box_materials(s)
+    configs.add_box(s, mats)
+    m1 = s.metal(albedo, 0.05)
+    m2 = s.metal((0.8, -0.3, 0.6), 0.0)
+    s.add_sphere((35, 20, 45), 18, m1)
+    s.add_sphere((70, 15, 30), 12, m2)
+    s.add_sphere((55, 60, 40), 10, s.dielectric(ref_idx=1.5))
+    configs.cornell_camera(s, 1.0)
+    r = GPURenderer(s, 48, 48, 16)
+    img = r.render()
+    ref, ostats = oracle_canvas(s, 48, 48, 16, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    assert np.signbit(img[1:]).any()  # negative zeros reached the canvas
+    r.close()
