@@ -431,7 +431,11 @@ struct HitOut {               // register form
   int32_t prim;               // leaf-order primitive, -1 = miss
   uint32_t pad;
 };
-struct alignas(32) HitSt { double t; int32_t prim; uint32_t pad; double u, v; };
+// A traced ray's closest hit, in two per-entry arrays (WaveBuf::hit, ::huv): (t, primitive)
+// as a double2 whose second double carries the primitive in its low word (-1: none), and
+// (u, v) (a sphere: u = the root taken, A16) only for scenes whose shading reads them.
+IZPI_DEV double2 hit_pack(double t, int32_t prim) { return make_double2(t, __hiloint2double(0, prim)); }
+IZPI_DEV int32_t hit_prim(double2 h) { return (int32_t)__double2loint(h.y); }
 struct PathSt {               // register form
   double lambda, lpdf;        // wavelength and its pdf (spectral)
   double pend[3];             // dielectric hit point while its path-length ray is traced
@@ -462,7 +466,8 @@ struct WaveBuf {
   PathHot* path;
   uint32_t* blk;      // overflow block + 1
   PathCold* cold;     // spectral / dielectric scenes, else null
-  HitSt* hit;
+  double2* hit;       // (t, primitive): hit_pack
+  double2* huv;       // (u, v) of the hit, or null when nothing reads it (WaveParams::hit_uv == 0)
   const double2* tminmax;  // izpi_gpu_trace only: per-entry (tMin, tMax) instead of the kind's
 };
 struct WaveParams {
@@ -578,7 +583,8 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
       cur = -1;
     }
   }
-  b.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, bu, bv};
+  b.hit[qi] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
+  if (b.huv) b.huv[qi] = make_double2(bu, bv);
 }
 
 // BVH4.Hit, step-scheduled variant. Each lane is in one of two modes: NODE (visit
@@ -734,7 +740,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             in_prim = false;
             bprim = -1;
             busy = cur != -1;
-            if (!busy) wp.in.hit[my] = HitSt{0.0, -1, 0u, 0.0, 0.0};
+            if (!busy) {
+              wp.in.hit[my] = hit_pack(0.0, -1);
+              if (!RL && wp.hit_uv) wp.in.huv[my] = make_double2(0.0, 0.0);
+            }
           }
         }
         c_rays += (uint64_t)__popcll(__ballot(main_ray));
@@ -1054,11 +1063,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
         const double2 uv = (!RL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        if (!RL && wp.hit_uv) {
-          wp.in.hit[qi] = HitSt{bprim >= 0 ? tmax : 0.0, bprim, 0u, uv.x, uv.y};
-        } else {  // nothing reads (u, v): half the record
-          *reinterpret_cast<double2*>(wp.in.hit + qi) = make_double2(bprim >= 0 ? tmax : 0.0, __hiloint2double(0, bprim));
-        }
+        wp.in.hit[qi] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
+        if (!RL && wp.hit_uv) wp.in.huv[qi] = uv;  // (scenes whose shading reads them)
         busy = false;
       }
     }
@@ -1121,7 +1127,7 @@ IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts) {
 }
 // defer_nmap: a PBR triangle's normal map is left to the caller (h.n stays geometric), which
 // looks the texel up together with the material's other three (one round of texel loads).
-IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, const GShade& gs, V3 o, V3 d, double time,
+IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp, const GShade& gs, V3 o, V3 d, double time,
                          bool want_uv, HitRec& h, bool mt_staged = false, bool defer_nmap = false) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
@@ -1132,7 +1138,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
     h.u = 0; h.v = 0;
     if (want_uv && sc.tritex) {  // (u,v) are read only by image textures
       const double eps = 1e-8;
-      double u = uvp->u, v = uvp->v;
+      double u = uvp->x, v = uvp->y;
       double w = 1.0 - u - v;
       double sum = u + v + w;
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
@@ -1157,7 +1163,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const HitSt* uvp, 
     V3 ctr = sph_center(pa, time);
     V3 on = sdiv(sub(h.p, ctr), pa[6]);
     V3 flipped = dot(d, on) >= 0 ? smul(on, -1) : on;
-    h.n = uvp->u == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
+    h.n = uvp->x == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
     if (want_uv) {
       double phi = gm::atan2(flipped.z, flipped.x);
       double theta = gm::asin(flipped.y);
@@ -1668,6 +1674,7 @@ IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint
   if (in.blk) out.blk[pos] = in.blk[i];
   if (in.cold) out.cold[pos] = in.cold[i];
   out.hit[pos] = in.hit[i];
+  if (in.huv) out.huv[pos] = in.huv[i];
 }
 // The path state of entry i (the ray and hit are read by shade_item).
 // What a shading pass reads of entry i besides its path state: the traced ray, the first
@@ -1679,7 +1686,7 @@ struct EntryIn {
 };
 IZPI_DEV void load_entry(const WaveBuf& b, uint32_t i, EntryIn& E) {
   E.ray = b.ray[i];
-  E.hit = *reinterpret_cast<const double2*>(b.hit + i);
+  E.hit = b.hit[i];
   E.time = b.time ? b.time[i] : 0.0;
 }
 template <int SAMPLER>
@@ -1922,7 +1929,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    hit_record(sc, H, in.hit + i, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR));
+    hit_record(sc, H, in.huv ? in.huv + i : nullptr, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR));
     hit_n = h.n;
     rec_mat = h.mat;
     next_o = h.p;
@@ -2520,19 +2527,19 @@ __global__ void k_trace_setup(const double* rays, uint32_t n, RayOD* ray, uint32
   kind[i] = RAY_PATHLEN;  // not a Sampler call
   tminmax[i] = make_double2(r[6], r[7]);
 }
-__global__ void k_trace_records(const DevScene sc, const RayOD* rr, const HitSt* hit, uint32_t n, izpi_hit* out) {
+__global__ void k_trace_records(const DevScene sc, const RayOD* rr, const double2* hit, const double2* huv, uint32_t n, izpi_hit* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   izpi_hit h;
   memset(&h, 0, sizeof(h));
   h.prim_ref = 0xFFFFFFFFu;
   HitOut c;
-  c.t = hit[i].t; c.prim = hit[i].prim; c.u = hit[i].u; c.v = hit[i].v; c.pad = 0;
+  c.t = hit[i].x; c.prim = hit_prim(hit[i]); c.u = huv[i].x; c.v = huv[i].y; c.pad = 0;
   if (c.prim >= 0) {
     const RayOD R = rr[i];
     HitRec hr;
     const GShade gs = sc.shade[c.prim];
-    hit_record(sc, c, hit + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
+    hit_record(sc, c, huv + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
     const GPrim& p = sc.prims[c.prim];
     h.hit = 1; h.t = hr.t; h.u = hr.u; h.v = hr.v;
     h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
@@ -2741,7 +2748,7 @@ int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n) {
 
 // The two sides of the wavefront state, `slots` entries each, in one allocation:
 // returns the bytes (base == nullptr) or fills b[0], b[1].
-size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, WaveBuf* b) {
+size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, bool uv, WaveBuf* b) {
   size_t off = 0;
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
@@ -2756,7 +2763,8 @@ size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, W
     w.path = (PathHot*)take((size_t)slots * sizeof(PathHot));
     w.blk = blk ? (uint32_t*)take((size_t)slots * sizeof(uint32_t)) : nullptr;
     w.cold = cold ? (PathCold*)take((size_t)slots * sizeof(PathCold)) : nullptr;
-    w.hit = (HitSt*)take((size_t)slots * sizeof(HitSt));
+    w.hit = (double2*)take((size_t)slots * sizeof(double2));
+    w.huv = uv ? (double2*)take((size_t)slots * sizeof(double2)) : nullptr;
     w.tminmax = nullptr;
     if (b) b[k] = w;
   }
@@ -3115,6 +3123,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const uint32_t rec_pool = max_depth - rec_dense;
   // PathCold (wavelength, dielectric point) is read only by the spectral sampler and glass
   const bool need_cold = spectral || !ctx->sc.no_pathlen;
+  // a hit's (u, v) array: read by (u, v)-reading textures and, for spheres, the root (A16)
+  const bool need_uv = !ctx->sc.tri_only || ctx->any_uv;
   // Paths in flight per wavefront pass. Larger = fewer k_trace/k_shade launches and
   // a smaller share of launch tails.
   // C3 per frame (round 2, tiered records): 40M slots 349 ms, 100M 334, 160M 326, 250M 320
@@ -3124,7 +3134,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   uint64_t slot_cap = 256ull << 20;
   if (tu.slots) slot_cap = std::max<uint64_t>(1024, tu.slots);
   const uint64_t per_slot = 2 * (sizeof(RayOD) + sizeof(uint32_t) + (ctx->sc.tri_only ? 0 : sizeof(double)) + sizeof(PathHot) +
-                                 sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(HitSt)) +
+                                 sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(double2) * (need_uv ? 2 : 1)) +
                             (uint64_t)rec_dense * D * sizeof(double);
   // Overflow blocks per slot. Lambert/light scenes: 1 per 16 slots (C3: ~3% of the paths
   // in flight are deeper than 8). Scenes with glass or the spectral sampler run deep
@@ -3169,7 +3179,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
       {(void**)&ctx->d_pool, &ctx->pool_cap, rec_pool ? (size_t)pool_blocks * rec_pool * D * sizeof(double) : 0},
       {(void**)&ctx->d_ring, &ctx->ring_cap, rec_pool ? (size_t)pool_blocks * sizeof(uint32_t) : 0},
       {(void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)},
-      {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, nullptr)},
+      {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, need_uv, nullptr)},
       {(void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes},
   };
   if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0])))) {
@@ -3185,7 +3195,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if ((rc = grow(ctx, (void**)&ctx->d_cpart, &ctx->cpart_cap, (size_t)cpart_rows * CNT_N * sizeof(unsigned long long)))) return rc;
   const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count();
   WaveBuf bufs[2];
-  carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, bufs);
+  carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, need_uv, bufs);
   hipStream_t st = ctx->stream;
   HIP_TRY(hipMemcpyAsync(ctx->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   if (nbg) {
@@ -3222,7 +3232,7 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = misc(ctx, 2); wp.slots = slots;
   // kind words other than plain main rays: path-length rays, parked entries
   wp.read_kind = !ctx->sc.no_pathlen ? 1u : 0u;  // parked entries: wp.in_park, per pass
-  wp.hit_uv = (!ctx->sc.tri_only || ctx->any_uv) ? 1u : 0u;
+  wp.hit_uv = need_uv ? 1u : 0u;
   wp.pool_ctr = sp.pool_ctr;
   wp.cpart = ctx->d_cpart;
   AccumParams ap{};
@@ -3899,19 +3909,20 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   DevBufs tmp;  // freed on every return
-  double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; HitSt* hh;
+  double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; double2* hh; double2* huv;
   HIP_TRY(tmp.alloc(&dr, (size_t)n * 8));
   HIP_TRY(tmp.alloc(&dh, n));
   HIP_TRY(tmp.alloc(&rr, n));
   HIP_TRY(tmp.alloc(&kk, n));
   HIP_TRY(tmp.alloc(&tm, n));
   HIP_TRY(tmp.alloc(&hh, n));
+  HIP_TRY(tmp.alloc(&huv, n));
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * MISC_STRIDE * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, misc(ctx, 3));
   WaveParams wp{};
-  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh;
+  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh; wp.in.huv = huv;
   wp.in_count = misc(ctx, 3); wp.trace_next = misc(ctx, 2); wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
   int rc = make_tracer(ctx, kDefaultTuning, true, &tr);
@@ -3919,7 +3930,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if ((rc = grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes))) return rc;
   launch_trace(ctx, ctx->sc, tr, wp, ctx->stream, ctx->d_spill);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, n, dh);
+  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, huv, n, dh);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));

@@ -241,3 +241,28 @@ def test_zero_radiance_unwinding_signs_bitwise(gpu, albedo):
     assert_parity(img, ref, r.stats, ostats)
     assert np.signbit(img[1:]).any()  # negative zeros reached the canvas
     r.close()
+
+
+def test_zero_radiance_unwinding_spectral_signs_bitwise(gpu):
+    """The Spectral sampler's zero-radiance shortcut (ZF_*): PBR surfaces with a negative
+    spectral albedo (a Gaussian of scale -0.8) make specular levels that flip the sign of a
+    zero radiance (att = albedo x 1.5, pbr.go:158-263), glass adds sign-keeping specular
+    levels, the open box's escapes meet a black background: bit-exact against the oracle."""
+    tabs = configs.spectral_tables()
+    s = Scene("spectral_zero_signs")
+    mats = {
+        "Green": s.lambert(spectral=s.spectral_gaussian(0.9, 540, 40)),
+        "Red": s.lambert(spectral=s.spectral_gaussian(0.9, 640, 40)),
+        "light": s.diffuse_light(spectral=s.spectral_spd(tabs["cie_wavelengths"],
+                                                          tabs["light_sources"]["cie_f1_daylight_fluorescent"])),
+        "White": s.pbr(s.constant((0.7, 0.7, 0.7)), spectral=s.spectral_gaussian(-0.8, 560, 80)),
+    }
+    configs.add_box(s, mats)
+    s.add_sphere((35, 20, 45), 18, s.pbr(s.constant((0.2, 0.5, 0.3)), spectral=s.spectral_gaussian(-0.5, 500, 50)))
+    s.add_sphere((70, 15, 30), 12, s.dielectric(ref_idx=1.5))
+    configs.cornell_camera(s, 1.0)
+    r = GPURenderer(s, 48, 48, 16, sampler=N.SAMPLER_SPECTRAL)
+    img = r.render()
+    ref, ostats = oracle_canvas(s, 48, 48, 16, N.SAMPLER_SPECTRAL)
+    assert_parity(img, ref, r.stats, ostats)
+    r.close()
