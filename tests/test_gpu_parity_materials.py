@@ -259,7 +259,7 @@ def test_zero_radiance_unwinding_spectral_signs_bitwise(gpu):
     }
     configs.add_box(s, mats)
     s.add_sphere((35, 20, 45), 18, s.pbr(s.constant((0.2, 0.5, 0.3)), spectral=s.spectral_gaussian(-0.5, 500, 50)))
-    s.add_sphere((70, 15, 30), 12, s.dielectric(ref_idx=1.5))
+    s.add_sphere((70, 15, 30), 12, s.dielectric(spectral_refidx=s.spectral_tabulated(configs._REFIDX_WL, configs._REFIDX_V)))
     configs.cornell_camera(s, 1.0)
     r = GPURenderer(s, 48, 48, 16, sampler=N.SAMPLER_SPECTRAL)
     img = r.render()
