@@ -466,8 +466,9 @@ struct WaveBuf {
   PathHot* path;
   uint32_t* blk;      // overflow block + 1
   PathCold* cold;     // spectral / dielectric scenes, else null
-  double2* hit;       // (t, primitive): hit_pack
-  double2* huv;       // (u, v) of the hit, or null when nothing reads it (WaveParams::hit_uv == 0)
+  double2* hit;       // (t, primitive): hit_pack; entry i at hit[i * hs]
+  double2* huv;       // (u, v) of the hit, entry i at huv[i * hs]; null when nothing reads it (WaveParams::hit_uv == 0)
+  uint32_t hs;        // 1: hit alone (16-B stride); 2: hit and (u, v) interleaved (huv = hit + 1), one 32-B record per entry
   const double2* tminmax;  // izpi_gpu_trace only: per-entry (tMin, tMax) instead of the kind's
 };
 struct WaveParams {
@@ -583,8 +584,8 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
       cur = -1;
     }
   }
-  b.hit[qi] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
-  if (b.huv) b.huv[qi] = make_double2(bu, bv);
+  b.hit[(size_t)qi * b.hs] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
+  if (b.huv) b.huv[(size_t)qi * b.hs] = make_double2(bu, bv);
 }
 
 // BVH4.Hit, step-scheduled variant. Each lane is in one of two modes: NODE (visit
@@ -741,8 +742,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             bprim = -1;
             busy = cur != -1;
             if (!busy) {
-              wp.in.hit[my] = hit_pack(0.0, -1);
-              if (!RL && wp.hit_uv) wp.in.huv[my] = make_double2(0.0, 0.0);
+              wp.in.hit[(size_t)my * wp.in.hs] = hit_pack(0.0, -1);
+              if (!RL && wp.hit_uv) wp.in.huv[(size_t)my * wp.in.hs] = make_double2(0.0, 0.0);
             }
           }
         }
@@ -1063,8 +1064,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
         const double2 uv = (!RL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        wp.in.hit[qi] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
-        if (!RL && wp.hit_uv) wp.in.huv[qi] = uv;  // (scenes whose shading reads them)
+        wp.in.hit[(size_t)qi * wp.in.hs] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
+        if (!RL && wp.hit_uv) wp.in.huv[(size_t)qi * wp.in.hs] = uv;  // (scenes whose shading reads them)
         busy = false;
       }
     }
@@ -1673,8 +1674,8 @@ IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint
   out.path[pos] = in.path[i];
   if (in.blk) out.blk[pos] = in.blk[i];
   if (in.cold) out.cold[pos] = in.cold[i];
-  out.hit[pos] = in.hit[i];
-  if (in.huv) out.huv[pos] = in.huv[i];
+  out.hit[(size_t)pos * out.hs] = in.hit[(size_t)i * in.hs];
+  if (in.huv) out.huv[(size_t)pos * out.hs] = in.huv[(size_t)i * in.hs];
 }
 // The path state of entry i (the ray and hit are read by shade_item).
 // What a shading pass reads of entry i besides its path state: the traced ray, the first
@@ -1686,7 +1687,7 @@ struct EntryIn {
 };
 IZPI_DEV void load_entry(const WaveBuf& b, uint32_t i, EntryIn& E) {
   E.ray = b.ray[i];
-  E.hit = b.hit[i];
+  E.hit = b.hit[(size_t)i * b.hs];
   E.time = b.time ? b.time[i] : 0.0;
 }
 template <int SAMPLER>
@@ -1763,7 +1764,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
 // `unit_want` lanes get consecutive output entries, `put` lanes first. A granted lane
 // whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
 IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
-                             uint32_t& pos, uint32_t& parity, bool& exhausted, uint32_t key = 0) {
+                             uint32_t& pos, uint32_t& parity, bool& exhausted) {
   __shared__ uint32_t s_p[2][SHADE_WAVES], s_u[2][SHADE_WAVES];
   __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2], s_nent[2];
   const uint32_t b = parity;
@@ -1772,17 +1773,6 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   const uint64_t lt = (1ull << lane) - 1;
   const uint64_t mp = __ballot(put), mu = __ballot(unit_want);
   if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); }
-#ifdef IZPI_SORT_OCT
-  // experiment: the block's continuing paths grouped by `key` in its output range
-  __shared__ uint32_t s_k[2][SHADE_WAVES][8];
-  uint64_t mine = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 8; k++) {
-    const uint64_t m = __ballot(put && key == k);
-    if (lane == 0) s_k[b][w][k] = (uint32_t)__popcll(m);
-    if (key == k) mine = m;
-  }
-#endif
   __syncthreads();
   if (threadIdx.x == 0) {
     // both atomics in flight together: entries are reserved for every unit_want lane
@@ -1807,16 +1797,6 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   __syncthreads();
   uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
   for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
-#ifdef IZPI_SORT_OCT
-  if (put) {
-    uint32_t off = (uint32_t)__popcll(mine & lt);
-    for (uint32_t i = 0; i < SHADE_WAVES; i++) {
-      for (uint32_t k = 0; k < key; k++) off += s_k[b][i][k];
-      if (i < w) off += s_k[b][i][key];
-    }
-    pr = off;
-  }
-#endif
   const bool has_entry = unit_want && s_nput[b] + ur < s_nent[b];
   const bool granted = unit_want && ur < s_granted[b];
   unit = granted ? s_ubase[b] + ur : 0xFFFFFFFFu;
@@ -1929,7 +1909,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   } else {
     const GShade gs = sc.shade[H.prim];
     HitRec h;
-    hit_record(sc, H, in.huv ? in.huv + i : nullptr, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR));
+    hit_record(sc, H, in.huv ? in.huv + (size_t)i * in.hs : nullptr, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR));
     hit_n = h.n;
     rec_mat = h.mat;
     next_o = h.p;
@@ -2227,12 +2207,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     // one reservation phase: output entries for continuing and parked paths, new units
     // (and their entries) for finished ones
     uint32_t unit, pos;
-#ifdef IZPI_SORT_OCT
-    const uint32_t okey = push ? ((R.d[0] < 0 ? 1u : 0u) | (R.d[1] < 0 ? 2u : 0u) | (R.d[2] < 0 ? 4u : 0u)) : 0u;
-    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, okey);
-#else
     block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted);
-#endif
     if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
     if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS
@@ -2763,8 +2738,11 @@ size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, b
     w.path = (PathHot*)take((size_t)slots * sizeof(PathHot));
     w.blk = blk ? (uint32_t*)take((size_t)slots * sizeof(uint32_t)) : nullptr;
     w.cold = cold ? (PathCold*)take((size_t)slots * sizeof(PathCold)) : nullptr;
-    w.hit = (double2*)take((size_t)slots * sizeof(double2));
-    w.huv = uv ? (double2*)take((size_t)slots * sizeof(double2)) : nullptr;
+    // with (u, v): one 32-B record per entry, (t, prim) then (u, v), so a finished ray's
+    // two stores land in one line (two separate arrays made C4 / C5 trace 6-7% slower)
+    w.hs = uv ? 2u : 1u;
+    w.hit = (double2*)take((size_t)slots * w.hs * sizeof(double2));
+    w.huv = uv && w.hit ? w.hit + 1 : nullptr;
     w.tminmax = nullptr;
     if (b) b[k] = w;
   }
@@ -3922,7 +3900,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, misc(ctx, 3));
   WaveParams wp{};
-  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh; wp.in.huv = huv;
+  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh; wp.in.huv = huv; wp.in.hs = 1;
   wp.in_count = misc(ctx, 3); wp.trace_next = misc(ctx, 2); wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
   int rc = make_tracer(ctx, kDefaultTuning, true, &tr);
