@@ -481,7 +481,8 @@ struct WaveParams {
   uint32_t read_kind;         // path-length rays or explicit tMin / tMax can occur (k_trace2 reads kind words)
   const uint32_t* in_park;    // nonzero: the pass that wrote `in` parked entries (k_trace2 reads kind words), or null
   uint32_t* out_park;         // set by k_shade when it parks an entry of `out` (zeroed by k_trace2)
-  uint32_t hit_uv;            // k_shade may read a hit's (u, v): spheres (the root) or (u,v)-reading textures
+  uint32_t hit_uv;            // k_shade may read a hit's (u, v): spheres (the root) or (u,v)-reading textures;
+                              // then the hit records are interleaved (WaveBuf::hs == 2)
   unsigned long long* cpart;  // per-wave counter rows (count_add), or null
 };
 IZPI_DEV double ray_tmin(const WaveBuf& b, uint32_t i, uint32_t kind) {
@@ -742,8 +743,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             bprim = -1;
             busy = cur != -1;
             if (!busy) {
-              wp.in.hit[(size_t)my * wp.in.hs] = hit_pack(0.0, -1);
-              if (!RL && wp.hit_uv) wp.in.huv[(size_t)my * wp.in.hs] = make_double2(0.0, 0.0);
+              if (!RL && wp.hit_uv) {  // (t, prim) and (u, v) interleaved: hs == 2
+                double2* rec = wp.in.hit + ((size_t)my << 1);
+                rec[0] = hit_pack(0.0, -1); rec[1] = make_double2(0.0, 0.0);
+              } else {
+                wp.in.hit[my] = hit_pack(0.0, -1);
+              }
             }
           }
         }
@@ -1064,8 +1069,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
         const double2 uv = (!RL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        wp.in.hit[(size_t)qi * wp.in.hs] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
-        if (!RL && wp.hit_uv) wp.in.huv[(size_t)qi * wp.in.hs] = uv;  // (scenes whose shading reads them)
+        if (!RL && wp.hit_uv) {  // (t, prim) and (u, v) in one 32-B record (hs == 2)
+          double2* rec = wp.in.hit + ((size_t)qi << 1);
+          rec[0] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim); rec[1] = uv;
+        } else {  // nothing reads (u, v): 16 B per entry (hs == 1)
+          wp.in.hit[qi] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
+        }
         busy = false;
       }
     }
@@ -2502,19 +2511,20 @@ __global__ void k_trace_setup(const double* rays, uint32_t n, RayOD* ray, uint32
   kind[i] = RAY_PATHLEN;  // not a Sampler call
   tminmax[i] = make_double2(r[6], r[7]);
 }
-__global__ void k_trace_records(const DevScene sc, const RayOD* rr, const double2* hit, const double2* huv, uint32_t n, izpi_hit* out) {
+__global__ void k_trace_records(const DevScene sc, const RayOD* rr, const double2* hit, uint32_t n, izpi_hit* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   izpi_hit h;
   memset(&h, 0, sizeof(h));
   h.prim_ref = 0xFFFFFFFFu;
   HitOut c;
-  c.t = hit[i].x; c.prim = hit_prim(hit[i]); c.u = huv[i].x; c.v = huv[i].y; c.pad = 0;
+  const double2* rec = hit + 2 * (size_t)i;  // (t, prim), (u, v)
+  c.t = rec[0].x; c.prim = hit_prim(rec[0]); c.u = rec[1].x; c.v = rec[1].y; c.pad = 0;
   if (c.prim >= 0) {
     const RayOD R = rr[i];
     HitRec hr;
     const GShade gs = sc.shade[c.prim];
-    hit_record(sc, c, huv + i, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
+    hit_record(sc, c, rec + 1, gs, mk(R.o[0], R.o[1], R.o[2]), mk(R.d[0], R.d[1], R.d[2]), 0.0, true, hr);
     const GPrim& p = sc.prims[c.prim];
     h.hit = 1; h.t = hr.t; h.u = hr.u; h.v = hr.v;
     h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
@@ -3887,20 +3897,19 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if (n == 0) return IZPI_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   DevBufs tmp;  // freed on every return
-  double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; double2* hh; double2* huv;
+  double* dr; izpi_hit* dh; RayOD* rr; uint32_t* kk; double2* tm; double2* hh;
   HIP_TRY(tmp.alloc(&dr, (size_t)n * 8));
   HIP_TRY(tmp.alloc(&dh, n));
   HIP_TRY(tmp.alloc(&rr, n));
   HIP_TRY(tmp.alloc(&kk, n));
   HIP_TRY(tmp.alloc(&tm, n));
-  HIP_TRY(tmp.alloc(&hh, n));
-  HIP_TRY(tmp.alloc(&huv, n));
+  HIP_TRY(tmp.alloc(&hh, 2 * (size_t)n));  // (t, prim) and (u, v) interleaved
   HIP_TRY(hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(ctx->d_misc, 0, 8 * MISC_STRIDE * sizeof(uint32_t), ctx->stream));
   HIP_TRY(hipMemsetAsync(ctx->d_counters, 0, CNT_N * sizeof(unsigned long long), ctx->stream));
   hipLaunchKernelGGL(k_trace_setup, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dr, n, rr, kk, tm, misc(ctx, 3));
   WaveParams wp{};
-  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh; wp.in.huv = huv; wp.in.hs = 1;
+  wp.in.ray = rr; wp.in.kind = kk; wp.in.tminmax = tm; wp.in.hit = hh; wp.in.huv = hh + 1; wp.in.hs = 2;
   wp.in_count = misc(ctx, 3); wp.trace_next = misc(ctx, 2); wp.slots = n; wp.read_kind = 1; wp.hit_uv = 1;
   Tracer tr;
   int rc = make_tracer(ctx, kDefaultTuning, true, &tr);
@@ -3908,7 +3917,7 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
   if ((rc = grow(ctx, (void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes))) return rc;
   launch_trace(ctx, ctx->sc, tr, wp, ctx->stream, ctx->d_spill);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, huv, n, dh);
+  hipLaunchKernelGGL(k_trace_records, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, rr, hh, n, dh);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipMemcpy(out, dh, (size_t)n * sizeof(izpi_hit), hipMemcpyDeviceToHost));

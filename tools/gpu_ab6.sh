@@ -6,7 +6,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pa
 tail -2 gpurun_out/t6.log
 O=gpurun_out/ab6.log
 V="timeout -k 10 300 python tools/variants.py run --frames 1"
-$V --config C5 --spp 32 base head head2 base head head2 > $O
-$V --config C4 --spp 128 base head head2 base head head2 >> $O
+$V --config C5 --spp 32 base head2 base head2 > $O
+$V --config C4 --spp 128 base head2 base head2 >> $O
 $V --config C3 --spp 128 base head2 base head2 >> $O
 cut -c1-300 $O
