@@ -352,11 +352,23 @@ def main():
         else:
             torch.cuda.synchronize()
 
-    def timed(bvh, steps, warmup):
+    def timed(bvh, steps, warmup, keep=False, reuse=None):
         """warmup untimed + `steps` timed frames; returns (elapsed, per-step stats sums of
-        this process's device(s), canvas, info)."""
+        this process's device(s), canvas, info). keep: leave the (single-GPU) renderer open
+        and return it as info["renderer"]; reuse: such a renderer, whose context and render
+        buffers take the scene again with the `bvh` tree (one workspace per process: the
+        driver clears every byte a process touched before handing it to the next one)."""
         ts = time.time()
-        if mode == "threads":
+        if reuse is not None:
+            r = reuse
+            r.use_tree(scene, bvh, bvh_leaf_max=args.bvh_leaf_max)
+            canvas_holder = {}
+
+            def step():
+                canvas, st = r.render_distributed(rank, world, post=post)
+                canvas_holder["c"] = canvas
+                return [st]
+        elif mode == "threads":
             r = MultiGPURenderer(scene, cfg.width, cfg.height, spp, list(range(n_gpus)), max_depth=cfg.max_depth,
                                  sampler=cfg.sampler, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
 
@@ -426,7 +438,10 @@ def main():
             img = r.render(post=post)
         elif rank == 0:
             img = canvas_holder["c"].cpu().numpy() if canvas_holder.get("c") is not None else None
-        r.close()
+        if keep and mode == "single":
+            info["renderer"] = r
+        else:
+            r.close()
         return elapsed, agg, img, info
 
     if args.pmc_child:  # one frame under rocprofv3 --pmc (the parent reads the counters)
@@ -434,15 +449,19 @@ def main():
         print(json.dumps({"pmc_child": True, "ms": elapsed * 1e3}), flush=True)
         return
 
-    elapsed, agg, img, info = timed(args.bvh, args.steps, args.warmup)
+    want_ref = mode == "single" and args.bvh == "gpu" and not args.no_reference_check
+    elapsed, agg, img, info = timed(args.bvh, args.steps, args.warmup, keep=want_ref)
+    kept = info.pop("renderer", None)
     samples_per_step = cfg.width * cfg.height * spp
     value = samples_per_step * args.steps / elapsed / 1e6
     ref_check = None
-    if mode == "single" and args.bvh == "gpu" and not args.no_reference_check:
+    if want_ref:
         # The same frame on hitable.NewBVH4's own tree (rebuilt bit for bit on the host):
-        # the GPU-built tree only counts if its image is the reference tree's image.
+        # the GPU-built tree only counts if its image is the reference tree's image. Same
+        # context and render buffers as the timed frames.
         rsteps = min(args.steps, 3)
-        r_elapsed, r_agg, r_img, r_info = timed("reference", rsteps, 1)
+        r_elapsed, r_agg, r_img, r_info = timed("reference", rsteps, 1, reuse=kept)
+        kept.close()
         equal = img.tobytes() == r_img.tobytes()
         rmse = float(np.sqrt(np.mean((img - r_img) ** 2)))
         ref_value = samples_per_step * rsteps / r_elapsed / 1e6

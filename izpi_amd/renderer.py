@@ -145,6 +145,21 @@ class GPURenderer:
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None
 
+    def use_tree(self, scene, bvh, bvh_seed=12345, bvh_leaf_max=None):
+        """Re-upload `scene` with another BVH (`bvh` as in __init__) into this context. Its
+        render buffers stay and are reused by the next frame of the same request: a second
+        renderer would allocate, and leave for the driver to clear, a second workspace."""
+        if bvh not in ("reference", "gpu"):
+            raise ValueError("bvh must be 'reference' or 'gpu'")
+        self.host = HostScene(scene, aspect_override=float(self.width) / float(self.height), bvh_seed=bvh_seed,
+                              skip_bvh=bvh == "gpu")
+        self.bvh_build_ms = None
+        self.bvh_leaf_max = (bvh_leaf_max or gpu_leaf_max(self.host.desc)) if bvh == "gpu" else None
+        if bvh == "gpu":
+            nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes(), self.bvh_leaf_max)
+            self.host.set_bvh(nodes, order)
+        _check(N.lib().izpi_gpu_upload_scene(self.ctx, C.byref(self.host.desc)), self.ctx, "izpi_gpu_upload_scene")
+
     def build_bvh4(self, boxes, leaf_max=4, method=None):
         """izpi_gpu_build_bvh4 over [n][6] f64 boxes: (nodes (m, 128) uint8, order, ms)."""
         return build_bvh4(self.ctx, boxes, leaf_max, method)

@@ -13,3 +13,8 @@ import json, sys
 d = json.loads(sys.stdin.read()); f = d['frames']
 print(json.dumps({'config': d['config'], 'after': 'C2 bench', 'slots': f[0]['slots'], 'workspace_gb': round(f[0]['workspace_gb'], 1), 'first_wall_ms': round(f[0]['wall_ms'], 1), 'first_alloc_ms': round(f[0]['alloc_ms'], 1), 'steady_wall_ms': round(f[1]['wall_ms'], 1), 'steady_device_ms': round(f[1]['device_ms'], 1), 'setup_s': round(d['setup_s'], 3)}))"
 done
+# the allocation rate itself after the same kind of process, at once and after a pause
+for pause in 0 5; do
+  timeout -k 10 200 python bench.py --config C2 --steps 1 --warmup 1 --no-pmc --no-cpu-baseline --no-reference-check > gpurun_out/ffb_prev.log 2>&1
+  timeout -k 10 120 python tools/alloc_probe.py --chunks 8 --gb 16 --pause $pause
+done
