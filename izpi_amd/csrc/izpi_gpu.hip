@@ -2738,6 +2738,9 @@ size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, b
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
     off += (bytes + 255) & ~(size_t)255;
+#ifdef IZPI_STATE_SKEW
+    off += (size_t)(IZPI_STATE_SKEW);  // measurement builds: arrays offset against each other
+#endif
     return p;
   };
   for (int k = 0; k < 2; k++) {
