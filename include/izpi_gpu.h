@@ -106,7 +106,8 @@ enum {
   IZPI_TUNE_NO_TAIL = 16,         /* no k_tail: wavefront passes to the end */
   IZPI_TUNE_PASS_LOG = 32,        /* diagnostics: per-pass device times on stderr */
   IZPI_TUNE_NO_LDS_BVH = 64,      /* small scenes: traverse from global memory, not the per-block LDS copy */
-  IZPI_TUNE_NO_RAY_LDS = 128      /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
+  IZPI_TUNE_NO_RAY_LDS = 128,     /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
+  IZPI_TUNE_NO_PRIM_LDS = 256     /* small scenes: shading reads the primitives' records from global memory, not the per-block LDS copy */
 };
 
 typedef struct izpi_render_req {

@@ -91,6 +91,7 @@ class RenderTuning(C.Structure):
 TUNE_NO_DIST, TUNE_GENERAL_TRACE, TUNE_NO_LEAF_SHORTCUT, TUNE_SCALAR_SLAB, TUNE_NO_TAIL, TUNE_PASS_LOG = 1, 2, 4, 8, 16, 32
 TUNE_NO_LDS_BVH = 64
 TUNE_NO_RAY_LDS = 128
+TUNE_NO_PRIM_LDS = 256
 
 
 def tuning(**kw):

@@ -1116,6 +1116,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #else
 #define IZPI_EXP_NMAP(x) (x)
 #endif
+// Small scenes' per-primitive shading data staged in LDS by every k_shade / k_tail block
+// (shade_stage, ShadeParams::prims_staged: at most PR_LDS primitives, as in C1, C2, C4, C5):
+// the closest hit's GShade, its triangle UVs and tangent frame and a sphere's record are
+// then LDS reads instead of a chain of dependent global loads (entry -> GShade -> UVs ->
+// texels -> tangent frame).
+constexpr uint32_t PR_LDS = 64;
+IZPI_DEV GShade* gs_lds() {
+  __shared__ GShade g[PR_LDS];
+  return g;
+}
+IZPI_DEV GTriTex* tt_lds() {
+  __shared__ GTriTex t[PR_LDS];
+  return t;
+}
+IZPI_DEV GPrim* gp_lds() {
+  __shared__ GPrim p[PR_LDS];
+  return p;
+}
+IZPI_DEV GShade gshade_of(const DevScene& sc, bool pst, int32_t prim) {
+  if (pst) return lds_ld(gs_lds() + prim);
+  return sc.shade[prim];
+}
 // Full hit record of the closest primitive (triangle.go:223-264, sphere.go:71-92).
 struct HitRec {
   double t, u, v;
@@ -1127,10 +1149,18 @@ struct HitRec {
 // `uvp` is the hit record, whose (u, v): read only for UV-textured triangles and for spheres.
 // A normal map's texel nts at the hit of triangle `prim` (leaf order) applied to the
 // geometric normal n through the triangle's tangent frame (triangle.go:250-264).
-IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts) {
+IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts, bool pst = false) {
   nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
-  const GTriTex& tt = sc.tritex[prim];
-  V3 tg = ld3(tt.tg), bt = ld3(tt.bt);
+  V3 tg, bt;
+  if (pst) {
+    const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds() + prim);
+    constexpr uint32_t TG = offsetof(GTriTex, tg) / 8, BT = offsetof(GTriTex, bt) / 8;
+    tg = mk(q[TG], q[TG + 1], q[TG + 2]);
+    bt = mk(q[BT], q[BT + 1], q[BT + 2]);
+  } else {
+    const GTriTex& tt = sc.tritex[prim];
+    tg = ld3(tt.tg); bt = ld3(tt.bt);
+  }
   V3 nn = mk(tg.x * nts.x + bt.x * nts.y + n.x * nts.z, tg.y * nts.x + bt.y * nts.y + n.y * nts.z,
              tg.z * nts.x + bt.z * nts.y + n.z * nts.z);
   return sdiv(nn, length(nn));
@@ -1138,7 +1168,7 @@ IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts) {
 // defer_nmap: a PBR triangle's normal map is left to the caller (h.n stays geometric), which
 // looks the texel up together with the material's other three (one round of texel loads).
 IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp, const GShade& gs, V3 o, V3 d, double time,
-                         bool want_uv, HitRec& h, bool mt_staged = false, bool defer_nmap = false) {
+                         bool want_uv, HitRec& h, bool mt_staged = false, bool defer_nmap = false, bool pst = false) {
   h.t = c.t;
   h.p = add(o, smul(d, c.t));
   h.mat = gs_mat(gs);
@@ -1152,7 +1182,13 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
       double w = 1.0 - u - v;
       double sum = u + v + w;
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
-      const double* uv = sc.tritex[c.prim].uv;  // u0,v0,u1,v1,u2,v2
+      double uv[6];  // u0,v0,u1,v1,u2,v2
+      if (pst) {
+        const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds() + c.prim);
+        for (int k = 0; k < 6; k++) uv[k] = q[k];
+      } else {
+        for (int k = 0; k < 6; k++) uv[k] = sc.tritex[c.prim].uv[k];
+      }
       h.u = w * uv[0] + u * uv[2] + v * uv[4];
       h.v = w * uv[1] + u * uv[3] + v * uv[5];
     }
@@ -1162,14 +1198,19 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
         const V3 nts = slot_rgb(sc, ns, h.u, h.v, mt_staged);
         h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
         h.nraw_ok = true;
-        n = nmap_tbn(sc, c.prim, n, nts);
+        n = nmap_tbn(sc, c.prim, n, nts, pst);
       }
     }
     h.n = n;
   } else {
-    const GPrim& pr = sc.prims[c.prim];
     double pa[9];
-    for (int q = 0; q < 9; q++) pa[q] = pr.a[q];
+    if (pst) {
+      const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(gp_lds() + c.prim);
+      for (int k = 0; k < 9; k++) pa[k] = q[k];
+    } else {
+      const GPrim& pr = sc.prims[c.prim];
+      for (int k = 0; k < 9; k++) pa[k] = pr.a[k];
+    }
     V3 ctr = sph_center(pa, time);
     V3 on = sdiv(sub(h.p, ctr), pa[6]);
     V3 flipped = dot(d, on) >= 0 ? smul(on, -1) : on;
@@ -1327,6 +1368,7 @@ struct ShadeParams {
   const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
   uint32_t num_mc, num_tex, num_spd;  // materials, textures, SPD table entries of the scene
   uint32_t staged;             // the scene's small tables are staged in LDS per block (shade_stage)
+  uint32_t prims_staged;       // so are its primitives' GShade / GTriTex / GPrim records (at most PR_LDS)
   uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
   uint32_t* head;              // next work unit
@@ -1447,6 +1489,17 @@ IZPI_DEV void shade_stage(const DevScene& sc, const ShadeParams& sp) {
       c[t] = c_cie_wl[t]; c[IZPI_CIE_N + t] = c_cie_x[t]; c[2 * IZPI_CIE_N + t] = c_cie_y[t];
       c[3 * IZPI_CIE_N + t] = c_cie_z[t]; c[4 * IZPI_CIE_N + t] = c_cie_ycum.v[t];
     }
+  }
+  if (sp.prims_staged) {
+    const uint32_t t0 = threadIdx.x, nt = blockDim.x, np = sc.num_prims;
+    constexpr uint32_t SW = sizeof(GShade) / 8, TW = sizeof(GTriTex) / 8, PW = sizeof(GPrim) / 8;
+    for (uint32_t t = t0; t < SW * np; t += nt)
+      reinterpret_cast<uint64_t*>(gs_lds())[t] = reinterpret_cast<const uint64_t*>(sc.shade)[t];
+    if (sc.tritex)
+      for (uint32_t t = t0; t < TW * np; t += nt)
+        reinterpret_cast<uint64_t*>(tt_lds())[t] = reinterpret_cast<const uint64_t*>(sc.tritex)[t];
+    for (uint32_t t = t0; t < PW * np; t += nt)
+      reinterpret_cast<uint64_t*>(gp_lds())[t] = reinterpret_cast<const uint64_t*>(sc.prims)[t];
   }
   __syncthreads();
 }
@@ -1729,6 +1782,7 @@ template <int SAMPLER>
 __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp_in, const WaveParams wp) {
   ShadeParams sp = sp_in;
   sp.staged = 0;  // k_start stages no tables: its path starts read them from global memory
+  sp.prims_staged = 0;
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   bool want = j < sp.slots;
   bool push = false;
@@ -1916,9 +1970,10 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
                : mk(bg_value(sp, P.lambda), 0, 0);
     terminal = true;
   } else {
-    const GShade gs = sc.shade[H.prim];
+    const bool pst = sp.prims_staged != 0;
+    const GShade gs = gshade_of(sc, pst, H.prim);
     HitRec h;
-    hit_record(sc, H, in.huv ? in.huv + (size_t)i * in.hs : nullptr, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR));
+    hit_record(sc, H, in.huv ? in.huv + (size_t)i * in.hs : nullptr, gs, ro, rd, R.time, (gs_cflags(gs) & 2u) != 0, h, st, ms_has(MATSET, MS_PBR), pst);
     hit_n = h.n;
     rec_mat = h.mat;
     next_o = h.p;
@@ -2004,7 +2059,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         const bool has_nmap = IZPI_EXP_NMAP(slot_set(s_nrm));
         const V3 nuv = has_nmap ? slot_rgb(sc, s_nrm, h.u, h.v, st) : mk(0, 0, 0);  // one texel for both uses
         if (has_nmap && IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
-          h.n = nmap_tbn(sc, H.prim, h.n, nuv);  // the hit record's normal (triangle.go:250-264)
+          h.n = nmap_tbn(sc, H.prim, h.n, nuv, pst);  // the hit record's normal (triangle.go:250-264)
           hit_n = h.n;
         }
         V3 normal = h.n;
@@ -3213,8 +3268,10 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.num_mc = ctx->num_materials; sp.num_tex = ctx->num_textures; sp.num_spd = ctx->num_spd;
   sp.staged = ctx->num_materials <= MC_LDS && ctx->num_materials <= MAT_LDS && sc.num_lights <= LT_LDS &&
               ctx->num_textures <= TEX_LDS && ctx->num_spd <= SPD_LDS && nbg <= BG_LDS;
+  sp.prims_staged = sc.num_prims <= PR_LDS && !(tuning_of(req).flags & IZPI_TUNE_NO_PRIM_LDS);
 #ifdef IZPI_NO_STAGING
   sp.staged = 0;  // A/B builds
+  sp.prims_staged = 0;
 #endif
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
