@@ -175,6 +175,27 @@ IZPI_HD double sin(double x) {
   return sign ? -y : y;
 }
 
+// cos(x) and sin(x) of one x >= 0 below GM_REDUCE_THRESHOLD (random directions' phi = 2 Pi r,
+// r in [0, 1)): the two share sin.go's reduction and both polynomials, so one reduction
+// and one evaluation of each polynomial give both, bit for bit as cos() and sin() above
+// (for x = +0 sin's early return and the polynomial both give +0).
+IZPI_HD void sincos_nonneg(double x, double* s, double* c) {
+  uint64_t j = (uint64_t)(x * GM_4_OVER_PI);
+  double y = (double)j;
+  if (j & 1) { j++; y++; }
+  j &= 7;
+  const double z = ((x - y * GM_PI4A) - y * GM_PI4B) - y * GM_PI4C;
+  bool csign = false, ssign = false;
+  if (j > 3) { j -= 4; csign = !csign; ssign = !ssign; }
+  if (j > 1) csign = !csign;
+  const double zz = z * z;
+  const double sp = sin_poly(z, zz), cp = cos_poly(zz);
+  const bool swap = j == 1 || j == 2;
+  const double cy = swap ? sp : cp, sy = swap ? cp : sp;
+  *c = csign ? -cy : cy;
+  *s = ssign ? -sy : sy;
+}
+
 // tan.go (Cephes)
 IZPI_HD double tan(double x) {
   if (x == 0 || is_nan(x)) return x;

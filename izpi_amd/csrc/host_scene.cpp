@@ -613,6 +613,11 @@ double izpi_host_gomath(int op, double x, double y) {
     case 8: return gm::sqrt(x);
     case 9: return x / y;
     case 10: return gm::atan(x);
+    case 11: case 12: {  // sincos_nonneg: sin, cos parts (x >= 0)
+      double sv, cv;
+      gm::sincos_nonneg(x, &sv, &cv);
+      return op == 11 ? sv : cv;
+    }
   }
   return gm::nan();
 }

@@ -85,6 +85,7 @@ constexpr int MISC_STRIDE = IZPI_MISC_STRIDE;  // words between the fields of iz
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
        CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
        CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_PARK, CNT_SCLK_MAT, CNT_SCLK_FIN, CNT_SCLK_MIX, CNT_SCLK_LPDF,
+       CNT_SCLK_ENTRY, CNT_SCLK_TEX,
        CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 // Frame counters without atomics: a render's kernels add their per-wave counts to the
@@ -1289,9 +1290,36 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
   }
   return sum;
 }
+// What Triangle.Random reads beyond the PDFValue record: v1 and v2 (6 doubles per light,
+// staged next to lt_lds), so a light sample is an LDS read instead of a dependent load.
+IZPI_DEV double* lt2_lds() {
+  __shared__ double l[LT_LDS * 6];
+  return l;
+}
 // HitableSlice.Random (hitable_slice.go:107-110) + Triangle/Sphere.Random
-IZPI_DEV V3 lights_random(const DevScene& sc, V3 o, Lcg& rng) {
+IZPI_DEV V3 lights_random(const DevScene& sc, bool staged, V3 o, Lcg& rng) {
   int64_t index = go_int(rng.next() * (double)sc.num_lights);
+#ifndef IZPI_NO_LRAND_LDS
+  if (staged) {
+    const double* r = lt_lds() + index * 16;
+    if (lds_ld(r + 15) == (double)IZPI_PRIM_TRIANGLE) {
+      const double* q = lt2_lds() + index * 6;
+      const V3 v0 = mk(lds_ld(r), lds_ld(r + 1), lds_ld(r + 2));
+      const V3 v1 = mk(lds_ld(q), lds_ld(q + 1), lds_ld(q + 2)), v2 = mk(lds_ld(q + 3), lds_ld(q + 4), lds_ld(q + 5));
+      double t1 = rng.next();
+      V3 p01 = lerp(v0, v1, t1);
+      double t2 = rng.next();
+      V3 p02 = lerp(v0, v2, t2);
+      double t3 = rng.next();
+      return sub(lerp(p01, p02, t3), o);
+    }
+    V3 dir = sub(mk(lds_ld(r + 4), lds_ld(r + 5), lds_ld(r + 6)), o);  // c0
+    double dist2 = sqlen(dir);
+    Onb uvw;
+    uvw.build(dir);
+    return uvw.local(random_to_sphere(lds_ld(r + 3), dist2, rng));
+  }
+#endif
   const GLight& L = sc.lights[index];
   if (L.kind == IZPI_PRIM_TRIANGLE) {
     double t1 = rng.next();
@@ -1477,6 +1505,11 @@ IZPI_DEV void shade_stage(const DevScene& sc, const ShadeParams& sp) {
     for (uint32_t t = t0; t < sp.num_mc; t += nt) mc_lds()[t] = sp.mat_const[t];
     for (uint32_t t = t0; t < 4 * sp.num_mc; t += nt) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
     for (uint32_t t = t0; t < 16 * sc.num_lights; t += nt) light_pack(sc.lights[t >> 4], t & 15, lt_lds() + (t & ~15u));
+    for (uint32_t t = t0; t < 6 * sc.num_lights; t += nt) {
+      const GLight& L = sc.lights[t / 6];
+      const uint32_t k = t % 6;
+      lt2_lds()[t] = L.kind == IZPI_PRIM_TRIANGLE ? (k < 3 ? L.v1[k] : L.v2[k - 3]) : 0.0;
+    }
     constexpr uint32_t MW = sizeof(izpi_material) / 8, TW = sizeof(izpi_texture) / 8;
     for (uint32_t t = t0; t < MW * sp.num_mc; t += nt)
       reinterpret_cast<uint64_t*>(mat_lds())[t] = reinterpret_cast<const uint64_t*>(sc.materials)[t];
@@ -1892,7 +1925,7 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
 // Timing builds only: wave cycles per section of shade_item, accumulated in LDS by the
 // first active lane of the wave that runs the section (so divergent sections count the
 // wave's time once), added to the CNT_SCLK_* counters at the end of the kernel.
-enum { SCLK_MAT = 0, SCLK_FIN, SCLK_MIX, SCLK_LPDF, SCLK_N };
+enum { SCLK_MAT = 0, SCLK_FIN, SCLK_MIX, SCLK_LPDF, SCLK_ENTRY, SCLK_TEX, SCLK_N };
 IZPI_DEV unsigned long long* sclk_lds() {
   __shared__ unsigned long long c[16][SCLK_N];
   return &c[(threadIdx.x >> 6) & 15][0];
@@ -1913,7 +1946,11 @@ IZPI_DEV void sclk_zero() {
 }
 #define SCLK_T(v) const uint64_t v = __builtin_readcyclecounter()
 #define SCLK_ADD(sec, t0) sclk_add(sec, __builtin_readcyclecounter() - (t0))
+// wait for every outstanding vector memory access (vmcnt(0); expcnt, lgkmcnt left alone):
+// separates a section's memory wait from the work after it
+#define SCLK_VMWAIT() __builtin_amdgcn_s_waitcnt(0x0F70)
 #else
+#define SCLK_VMWAIT() (void)0
 #define SCLK_T(v) (void)0
 #define SCLK_ADD(sec, t0) (void)0
 #endif
@@ -1932,6 +1969,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const bool st = sp.staged != 0;  // the scene's small tables are in this block's LDS
   SCLK_T(sc0);
+  SCLK_VMWAIT();
+  SCLK_ADD(SCLK_ENTRY, sc0);
   for (int k = 0; k < 3; k++) { R.o[k] = E.ray.o[k]; R.d[k] = E.ray.d[k]; }
   R.kind = kind;
   R.time = E.time;  // NewRay(hr.P, dir, r.Time()): the next ray keeps the time
@@ -2048,6 +2087,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         if constexpr (!ms_has(MATSET, MS_PBR)) { atomicOr(sp.error, 2u); terminal = true; break; }
         // the four texture slots (LDS, or one 64-B record); every lookup below is issued
         // before the first of them is used
+        SCLK_T(sct);
         const TexSlot s_alb = mat_slot(sc, st, h.mat, 0), s_nrm = mat_slot(sc, st, h.mat, 1),
                       s_rgh = mat_slot(sc, st, h.mat, 2), s_met = mat_slot(sc, st, h.mat, 3);
         double alb_s = 0;
@@ -2058,6 +2098,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v, st) : mk(0.0, 0.0, 0.0);
         const bool has_nmap = IZPI_EXP_NMAP(slot_set(s_nrm));
         const V3 nuv = has_nmap ? slot_rgb(sc, s_nrm, h.u, h.v, st) : mk(0, 0, 0);  // one texel for both uses
+        SCLK_VMWAIT();
+        SCLK_ADD(SCLK_TEX, sct);
         if (has_nmap && IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
           h.n = nmap_tbn(sc, H.prim, h.n, nuv, pst);  // the hit record's normal (triangle.go:250-264)
           hit_n = h.n;
@@ -2116,7 +2158,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       if (have_pdf) {
         // Mixture(Hitable(lights, P), Cosine(N)) (colour.go:48-51, mixture.go:17-33)
         V3 dir;
-        if (rng.next() < 0.5) dir = lights_random(sc, next_o, rng);
+        if (rng.next() < 0.5) dir = lights_random(sc, st, next_o, rng);
         else dir = cos_onb.local(random_cosine_direction(rng));
         // (evaluated in an order that frees the ONB, normal and attenuation before
         // the light-pdf loop; every value is computed exactly as in the reference)
@@ -2616,6 +2658,8 @@ __global__ void k_gomath(const DevScene sc, int op, const double* x, const doubl
     case 8: r = gm::sqrt(a); break;
     case 9: r = a / b; break;
     case 10: r = gm::atan(a); break;
+    case 11: case 12: { double sv, cv; gm::sincos_nonneg(a, &sv, &cv); r = op == 11 ? sv : cv; break; }
+    case 13: r = sdiv(mk(a, 0.0, 0.0), b).x; break;  // sdiv's shared reciprocal (= a / b)
     case 32: case 33: { double l, pdf; sample_wavelength(a, l, pdf); r = op == 32 ? l : pdf; break; }
     case 34: case 35: case 36: { double cx, cy, cz; cie_values(a, cx, cy, cz); r = op == 34 ? cx : op == 35 ? cy : cz; break; }
     case 37: r = tex_spectral(sc, (int32_t)b, a); break;
@@ -3332,9 +3376,9 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.alloc_ms = alloc_ms;
   if (rec_pool && s.parks * 64 > s.rays && pool_blocks < slots) ctx->pool_grow++;
 #ifdef IZPI_SHADE_CLOCKS
-  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu mat %llu finish %llu mix %llu lpdf %llu (wave cycles)\n",
+  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu mat %llu finish %llu mix %llu lpdf %llu entry %llu tex %llu (wave cycles)\n",
           cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL], cnt[CNT_SCLK_PUSH], cnt[CNT_SCLK_MAT], cnt[CNT_SCLK_FIN],
-          cnt[CNT_SCLK_MIX], cnt[CNT_SCLK_LPDF]);
+          cnt[CNT_SCLK_MIX], cnt[CNT_SCLK_LPDF], cnt[CNT_SCLK_ENTRY], cnt[CNT_SCLK_TEX]);
 #endif
 #ifdef IZPI_SHADOW
   fprintf(stderr, "IZPI_SHADOW spill_stores %llu spill_loads %llu (entries)\n", cnt[CNT_CLK_REFILL], cnt[CNT_CLK_NODE]);

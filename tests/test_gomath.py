@@ -168,3 +168,20 @@ def test_pow_special_cases():
                 assert math.isnan(got), (x, y, got)
             else:
                 assert got == want and math.copysign(1, got) == math.copysign(1, want), (x, y, got, want)
+
+
+def test_sincos_shared_reduction_bitwise():
+    """gomath.h's sincos_nonneg (one sin.go reduction and both polynomials, used for the
+    random directions' phi = 2 Pi r, vec3.go:119-138) returns the oracle's Sin and Cos bit
+    for bit for phi in [0, 2 Pi), at the octant boundaries and at +0."""
+    rng = np.random.default_rng(5)
+    r = np.concatenate([rng.uniform(0, 1, 20000), np.arange(0, 1, 1 / 64.0), [0.0, 5e-324, 1e-300, 0.9999999999999999]])
+    phi = 6.283185307179586 * r
+    octants = np.arange(9) * (math.pi / 4)
+    phi = np.concatenate([phi, octants, np.nextafter(octants, 0), np.nextafter(octants, 10), [0.0]])
+    phi = phi[phi >= 0]
+    L = N.lib()
+    for a in phi:
+        a = float(a)
+        assert struct.pack("<d", L.izpi_host_gomath(11, a, 0.0)) == struct.pack("<d", O.gomath(OPS["sin"], a, 0.0)), a
+        assert struct.pack("<d", L.izpi_host_gomath(12, a, 0.0)) == struct.pack("<d", O.gomath(OPS["cos"], a, 0.0)), a

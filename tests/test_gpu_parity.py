@@ -70,6 +70,38 @@ def test_gomath_device_bitwise(gpu):
         ref = np.array([O.gomath(op, float(a), float(b)) for a, b in zip(x, y)])
         mism = np.flatnonzero(out.view(np.uint64) != ref.view(np.uint64))
         assert mism.size == 0, (name, x[mism[:3]], y[mism[:3]], out[mism[:3]], ref[mism[:3]])
+    # sincos_nonneg (ops 11, 12): the shared-reduction Sin / Cos of the random directions
+    x = np.ascontiguousarray(6.283185307179586 * np.random.default_rng(9).uniform(0, 1, 20000), np.float64)
+    x[:9] = np.arange(9) * (np.pi / 4)
+    x[9] = 0.0
+    y = np.zeros_like(x)
+    for op, ref_op in ((11, OPS["sin"]), (12, OPS["cos"])):
+        out = np.zeros_like(x)
+        assert L.izpi_gpu_gomath(r.ctx, op, O.dptr(x), O.dptr(y), len(x), O.dptr(out)) == 0
+        ref = np.array([O.gomath(ref_op, float(a), 0.0) for a in x])
+        mism = np.flatnonzero(out.view(np.uint64) != ref.view(np.uint64))
+        assert mism.size == 0, (op, x[mism[:3]], out[mism[:3]], ref[mism[:3]])
+    # sdiv's shared reciprocal (op 13: sdiv((a, 0, 0), b).x) against the oracle's a / b, in
+    # and out of its 2^+-300 window: zeros, subnormals, huge, inf, NaN on either side
+    rng = np.random.default_rng(13)
+    sp = [0.0, -0.0, 5e-324, -5e-324, 2.2250738585072014e-308, 1e-300, 1e-200, 1e-90, 2.0 ** -300, 2.0 ** -301,
+          2.0 ** 300, 2.0 ** 301, 1e90, 1e200, 1.7976931348623157e308, float("inf"), float("-inf"), float("nan"), 1.0, -3.0]
+    gx, gy = np.meshgrid(sp, sp)
+    x = np.concatenate([rng.uniform(-1, 1, 20000) * 10.0 ** rng.integers(-120, 120, 20000), gx.ravel()])
+    y = np.concatenate([rng.uniform(-1, 1, 20000) * 10.0 ** rng.integers(-120, 120, 20000), gy.ravel()])
+    x, y = np.ascontiguousarray(x, np.float64), np.ascontiguousarray(y, np.float64)
+    out = np.zeros_like(x)
+    assert L.izpi_gpu_gomath(r.ctx, 13, O.dptr(x), O.dptr(y), len(x), O.dptr(out)) == 0
+    ref = np.array([O.gomath(OPS["div"], float(a), float(b)) for a, b in zip(x, y)])
+    # (NaN payloads are the platform's: a NaN quotient must be a NaN on both sides)
+    mism = np.flatnonzero((out.view(np.uint64) != ref.view(np.uint64)) & ~(np.isnan(out) & np.isnan(ref)))
+    assert mism.size == 0, ("sdiv", x[mism[:3]], y[mism[:3]], out[mism[:3]], ref[mism[:3]])
+    # inside the window every quotient takes the shared-reciprocal path: bitwise with '/'
+    # on the device itself (op 9) as well
+    out9 = np.zeros_like(x)
+    assert L.izpi_gpu_gomath(r.ctx, 9, O.dptr(x), O.dptr(y), len(x), O.dptr(out9)) == 0
+    mism = np.flatnonzero((out.view(np.uint64) != out9.view(np.uint64)) & ~(np.isnan(out) & np.isnan(out9)))
+    assert mism.size == 0, ("sdiv vs /", x[mism[:3]], y[mism[:3]], out[mism[:3]], out9[mism[:3]])
     r.close()
 
 
