@@ -1441,9 +1441,15 @@ constexpr bool ms_spec(int matset) { return (matset & (MS_DIEL | MS_METAL | MS_P
 template <int SAMPLER, int MATSET>
 struct RecLayout {
   static constexpr bool COMPACT = SAMPLER == IZPI_SAMPLER_COLOUR && MATSET == MATSET_CONST;
+#ifdef IZPI_REC6  // measurement builds: Colour records padded to 48 B (three 16-B loads per level)
+  static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 3);
+  static constexpr uint32_t P = COMPACT || SAMPLER != IZPI_SAMPLER_COLOUR ? D - 1 : 4;
+  static constexpr uint32_t S = P - 1;
+#else
   static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 5 : 3);  // doubles per record
   static constexpr uint32_t P = D - 1;                                                   // index of p
   static constexpr uint32_t S = D - 2;                                                   // index of s
+#endif
 };
 // Records are (att, s, p): att xyz for Colour, att for Spectral. A specular bounce has no
 // s or p and stores s = REC_SPEC_BITS, a signalling-NaN pattern: ScatteringPDF's
@@ -1465,9 +1471,17 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
     rp[1] = s;
     return;
   }
+  const double sv = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
+#ifdef IZPI_REC6
+  if constexpr (SAMPLER == IZPI_SAMPLER_COLOUR) {  // 48-B records: two 16-B stores
+    reinterpret_cast<double2*>(rp)[0] = make_double2(att.x, att.y);
+    reinterpret_cast<double2*>(rp)[1] = make_double2(att.z, sv);
+    return;
+  }
+#endif
   rp[0] = att.x;
   if (SAMPLER == IZPI_SAMPLER_COLOUR) { rp[1] = att.y; rp[2] = att.z; }
-  rp[RecLayout<SAMPLER, MATSET>::S] = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
+  rp[RecLayout<SAMPLER, MATSET>::S] = sv;
 }
 IZPI_DEV bool rec_is_spec(double s) { return (uint64_t)__double_as_longlong(s) == REC_SPEC_BITS; }
 // Update P.zf (ZF_*) for the record of the level being written: attenuation att (colour
@@ -1629,10 +1643,10 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
       const double* r = rv[j];
       if (SAMPLER == IZPI_SAMPLER_COLOUR) {
         V3 att = mk(r[0], r[1], r[2]);
-        if (rec_is_spec(r[3])) {
+        if (rec_is_spec(r[RecLayout<SAMPLER, MATSET>::S])) {
           L = mul(att, L);                                   // vec3.Mul(att, Sample(...))
         } else {
-          const double s = r[3], p = r[4];
+          const double s = r[RecLayout<SAMPLER, MATSET>::S], p = r[RecLayout<SAMPLER, MATSET>::P];
           V3 v1 = smul(L, s);                                // ScalarMul(Sample(...), ScatteringPDF)
           V3 v2 = mul(att, v1);
           V3 v3 = sdiv(v2, p);
@@ -1660,9 +1674,8 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
     double cx, cy, cz;  // render/spectral.go:162-166
     if (sp.staged) cie_values<true>(P.lambda, cx, cy, cz);
     else cie_values<false>(P.lambda, cx, cy, cz);
-    out[0] = (L.x * cx) / P.lpdf;
-    out[1] = (L.x * cy) / P.lpdf;
-    out[2] = (L.x * cz) / P.lpdf;
+    const V3 o = sdiv(mk(L.x * cx, L.x * cy, L.x * cz), P.lpdf);  // three divisions by lpdf
+    out[0] = o.x; out[1] = o.y; out[2] = o.z;
   }
 }
 
