@@ -1441,15 +1441,9 @@ constexpr bool ms_spec(int matset) { return (matset & (MS_DIEL | MS_METAL | MS_P
 template <int SAMPLER, int MATSET>
 struct RecLayout {
   static constexpr bool COMPACT = SAMPLER == IZPI_SAMPLER_COLOUR && MATSET == MATSET_CONST;
-#ifdef IZPI_REC6  // measurement builds: Colour records padded to 48 B (three 16-B loads per level)
-  static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 6 : 3);
-  static constexpr uint32_t P = COMPACT || SAMPLER != IZPI_SAMPLER_COLOUR ? D - 1 : 4;
-  static constexpr uint32_t S = P - 1;
-#else
   static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 5 : 3);  // doubles per record
   static constexpr uint32_t P = D - 1;                                                   // index of p
   static constexpr uint32_t S = D - 2;                                                   // index of s
-#endif
 };
 // Records are (att, s, p): att xyz for Colour, att for Spectral. A specular bounce has no
 // s or p and stores s = REC_SPEC_BITS, a signalling-NaN pattern: ScatteringPDF's
@@ -1472,13 +1466,6 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
     return;
   }
   const double sv = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
-#ifdef IZPI_REC6
-  if constexpr (SAMPLER == IZPI_SAMPLER_COLOUR) {  // 48-B records: two 16-B stores
-    reinterpret_cast<double2*>(rp)[0] = make_double2(att.x, att.y);
-    reinterpret_cast<double2*>(rp)[1] = make_double2(att.z, sv);
-    return;
-  }
-#endif
   rp[0] = att.x;
   if (SAMPLER == IZPI_SAMPLER_COLOUR) { rp[1] = att.y; rp[2] = att.z; }
   rp[RecLayout<SAMPLER, MATSET>::S] = sv;
@@ -2456,7 +2443,39 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
   double c0 = ap.running[3 * (size_t)p], c1 = ap.running[3 * (size_t)p + 1], c2 = ap.running[3 * (size_t)p + 2];
   const double* s = ap.samples + (size_t)p * ap.chunk_spp * 3;
   uint32_t k = 0;
-  if ((ap.chunk_spp & 1u) == 0) {
+#ifndef IZPI_OLD_ACCUM
+  if ((ap.chunk_spp & 3u) == 0 && blockIdx.x * 256 + 256 <= ap.num_pixels) {
+    // Staged through LDS, 4 samples (96 B) of each of the wave's 64 pixels at a time: the
+    // wave's lanes load the 64 runs as consecutive 16-B pieces (a load instruction covers
+    // ~11 neighbouring runs instead of one piece of 64 runs 12 KB apart), then each lane
+    // adds its own pixel's 4 samples from LDS in sample order (rgb.go:36).
+    __shared__ double2 st[4][64 * 6];
+    double2* w = st[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t p0 = p - lane;  // the wave's first pixel
+    const size_t run = (size_t)ap.chunk_spp * 3 / 2;  // double2 per pixel
+    const double2* s2 = reinterpret_cast<const double2*>(ap.samples) + (size_t)p0 * run;
+    for (; k < ap.chunk_spp; k += 4) {
+      double2 v[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        const uint32_t q = lane + 64 * i, j = q / 6, c = q % 6;
+        v[i] = s2[(size_t)j * run + (k >> 1) * 3 + c];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; i++) w[lane + 64 * i] = v[i];
+      __builtin_amdgcn_wave_barrier();
+      const double2 a = w[6 * lane], b = w[6 * lane + 1], c = w[6 * lane + 2];
+      const double2 d = w[6 * lane + 3], e = w[6 * lane + 4], f = w[6 * lane + 5];
+      __builtin_amdgcn_wave_barrier();
+      c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;  // sample k
+      c0 = c0 + b.y; c1 = c1 + c.x; c2 = c2 + c.y;  // sample k + 1
+      c0 = c0 + d.x; c1 = c1 + d.y; c2 = c2 + e.x;  // sample k + 2
+      c0 = c0 + e.y; c1 = c1 + f.x; c2 = c2 + f.y;  // sample k + 3
+    }
+  }
+#endif
+  if ((ap.chunk_spp & 1u) == 0 && k == 0) {
     // two samples (48 B, 16-B aligned for an even chunk_spp) per three 16-B loads: the
     // lanes' runs lie chunk_spp * 24 B apart, so every load instruction touches 64 lines
     // and the instruction count, not the bytes, bounds this loop
