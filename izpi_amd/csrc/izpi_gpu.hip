@@ -186,6 +186,26 @@ IZPI_DEV V3 image_rgb(const double* texels, uint64_t off, uint32_t w, uint32_t h
   const double2 rg = *reinterpret_cast<const double2*>(px);  // 32-B aligned texel: one 16-B load + one 8-B load
   return mk(rg.x, rg.y, px[2]);
 }
+// The texel index image_rgb computes, and the lookup at a given index: a PBR hit's
+// image textures usually share their size, so one index serves its four lookups.
+IZPI_DEV uint64_t image_index(uint32_t w, uint32_t h, double u, double v) {
+  int64_t i = go_int(u * (double)w);
+  int64_t j = go_int((1 - v) * ((double)h - 0.001));
+  if (i < 0) i = 0;
+  if (j < 0) j = 0;
+  if (i > (int64_t)w - 1) i = (int64_t)w - 1;
+  if (j > (int64_t)h - 1) j = (int64_t)h - 1;
+  return (uint64_t)j * w + (uint64_t)i;
+}
+IZPI_DEV V3 image_at(const double* texels, uint64_t off, uint32_t fmt, uint64_t k) {
+  if (fmt == TEXF_GRAY) {
+    const double g = texels[off + k];
+    return mk(g, g, g);
+  }
+  const double* px = texels + off + k * 4;
+  const double2 rg = *reinterpret_cast<const double2*>(px);
+  return mk(rg.x, rg.y, px[2]);
+}
 // texture.Constant / texture.ImageTxt (constant.go:20, image.go:73-101); the device copy
 // of an IMAGE texture has pad0 = its storage format
 IZPI_DEV V3 tex_rgb(const DevScene& sc, int32_t id, double u, double v, bool st = false) {
@@ -201,6 +221,22 @@ IZPI_DEV V3 slot_rgb(const DevScene& sc, const TexSlot& s, double u, double v, b
   return tex_rgb(sc, (int32_t)s.off, u, v, st);
 }
 IZPI_DEV bool slot_set(const TexSlot& s) { return (s.hf >> 30) != TEXF_NONE; }
+// slot_rgb with the texel index k0 of a w0 x h0 image at the same (u, v) (image_index):
+// reused when this slot's image has that size, else computed.
+IZPI_DEV V3 slot_rgb_k(const DevScene& sc, const TexSlot& s, double u, double v, bool st, uint32_t w0, uint32_t h0, uint64_t k0) {
+  const uint32_t fmt = s.hf >> 30, h = s.hf & 0x3FFFFFFFu;
+#ifndef IZPI_EXP_TEX_NOLOAD
+  if (fmt <= TEXF_GRAY) {
+    uint64_t k = k0;
+    if (s.w != w0 || h != h0) k = image_index(s.w, h, u, v);
+#ifdef IZPI_EXP_TEX_HOT
+    k &= 7;
+#endif
+    return image_at(sc.texels, s.off, fmt, k);
+  }
+#endif
+  return slot_rgb(sc, s, u, v, st);
+}
 // The materials' texture slots staged in LDS next to their constants (mc_stage): a PBR
 // hit reads its slots with an LDS read instead of a dependent L2 load.
 constexpr uint32_t MT_LDS = 64;
@@ -2090,14 +2126,17 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         SCLK_T(sct);
         const TexSlot s_alb = mat_slot(sc, st, h.mat, 0), s_nrm = mat_slot(sc, st, h.mat, 1),
                       s_rgh = mat_slot(sc, st, h.mat, 2), s_met = mat_slot(sc, st, h.mat, 3);
+        // one texel index for the images of the normal map's size (C4: all four)
+        const uint32_t w0 = s_nrm.w, h0 = s_nrm.hf & 0x3FFFFFFFu;
+        const uint64_t k0 = (s_nrm.hf >> 30) <= TEXF_GRAY ? image_index(w0, h0, h.u, h.v) : 0;
         double alb_s = 0;
-        if (COLOUR) att = slot_rgb(sc, s_alb, h.u, h.v, st);
+        if (COLOUR) att = slot_rgb_k(sc, s_alb, h.u, h.v, st, w0, h0, k0);
         else if (m.spectral_tex >= 0) alb_s = tex_spectral(sc, m.spectral_tex, P.lambda, h.u, h.v, st);
-        else { V3 c = slot_rgb(sc, s_alb, h.u, h.v, st); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
-        V3 rough = slot_set(s_rgh) ? slot_rgb(sc, s_rgh, h.u, h.v, st) : mk(0.5, 0.5, 0.5);
-        V3 metal = slot_set(s_met) ? slot_rgb(sc, s_met, h.u, h.v, st) : mk(0.0, 0.0, 0.0);
+        else { V3 c = slot_rgb_k(sc, s_alb, h.u, h.v, st, w0, h0, k0); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
+        V3 rough = slot_set(s_rgh) ? slot_rgb_k(sc, s_rgh, h.u, h.v, st, w0, h0, k0) : mk(0.5, 0.5, 0.5);
+        V3 metal = slot_set(s_met) ? slot_rgb_k(sc, s_met, h.u, h.v, st, w0, h0, k0) : mk(0.0, 0.0, 0.0);
         const bool has_nmap = IZPI_EXP_NMAP(slot_set(s_nrm));
-        const V3 nuv = has_nmap ? slot_rgb(sc, s_nrm, h.u, h.v, st) : mk(0, 0, 0);  // one texel for both uses
+        const V3 nuv = has_nmap ? slot_rgb_k(sc, s_nrm, h.u, h.v, st, w0, h0, k0) : mk(0, 0, 0);  // one texel for both uses
         SCLK_VMWAIT();
         SCLK_ADD(SCLK_TEX, sct);
         if (has_nmap && IZPI_PRIM_KIND(gs.ref) == IZPI_PRIM_TRIANGLE) {
