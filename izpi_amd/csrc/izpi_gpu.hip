@@ -2160,8 +2160,9 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         double mv = (metal.x + metal.y + metal.z) / 3.0;
         cos_onb.build(normal);  // the scatter's ONB and the sampler's Cosine(normal) pdf: one build (onb.go:38-67)
         const Onb& uvw = cos_onb;
-        V3 reflected = reflect(unit(rd), normal);
-        double cosTheta = gm::abs(dot(unit(rd), normal));
+        const V3 urd = unit(rd);  // (one evaluation for both uses)
+        V3 reflected = reflect(urd, normal);
+        double cosTheta = gm::abs(dot(urd, normal));
         double fresnel = 0.04 + (1.0 - 0.04) * gm::pow(1.0 - cosTheta, 5.0);
         fresnel = fresnel + (mv * 0.5);
         double sprob = fresnel * (1.0 - rv);
