@@ -124,10 +124,11 @@ typedef struct izpi_render_req {
   double background[3];       /* Colour background (leader.go:140: black) */
   uint64_t seed;              /* master seed of the per-sample LCG streams */
   uint32_t post;              /* IZPI_POST_*: post-processing of a whole-frame IZPI_OUT_CANVAS render */
-  uint32_t abi_version;       /* IZPI_ABI_VERSION (2); 0 = a request laid out by ABI 1, which ends before `tuning`:
-                                 the library then reads no further and uses the default tuning */
+  uint32_t abi_version;       /* IZPI_ABI_VERSION (2); 0 = a request laid out by ABI 1 (this field was padding):
+                                 its tuning, when set, is read as ABI 1's izpi_render_tuning, which ended at
+                                 tail_paths; the later fields keep their defaults */
   double exposure;            /* XYZToRGB exposure (Scene.Exposure = camera exposure) */
-  const izpi_render_tuning* tuning; /* NULL = defaults; read only when abi_version >= 2 */
+  const izpi_render_tuning* tuning; /* NULL = defaults */
 } izpi_render_req;
 
 /* Post-processing applied by Render for the Spectral sampler (renderer.go:215-219):
@@ -283,7 +284,8 @@ int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_
  * callable from another thread while it runs (RendererImpl.Render's per-tile progress
  * bar, renderer.go:119-121, rgb.go:54-56): samples (pixels x spp) whose paths have
  * finished, as of the library's last queue poll (every <= 8 wavefront passes, a lower
- * bound), and the request's samples. After the call returns, done == total. The multi
+ * bound), and the request's samples. After the call returns, done == total (both 0 when
+ * the request failed its checks), whether or not it succeeded. The multi
  * form sums the contexts of `m` (their shares of one frame). */
 int izpi_gpu_progress(izpi_ctx* ctx, uint64_t* samples_done, uint64_t* samples_total);
 int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* samples_total);
@@ -291,7 +293,9 @@ int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* sam
 /* Test hook (fault injection): where = 1 makes izpi_gpu_render_rank fail this rank's local
  * checks, 2 makes every render on this context fail as a device fault would, 3 makes this
  * rank's stream stall before the gather as a rank waiting on a dead peer does (released
- * once the call has given up on it); 0 = off. */
+ * once the call has given up on it), 4 makes izpi_gpu_render_rank's collective waits see a
+ * failed stream (a sticky device error): the rank aborts its communicator and returns
+ * IZPI_ERR_PEER; 0 = off. */
 int izpi_gpu_debug_fault(izpi_ctx* ctx, int where);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
@@ -304,7 +308,10 @@ int izpi_gpu_trace(izpi_ctx* ctx, const double* rays, uint32_t n, izpi_hit* out)
  * rays [n][7] f32: org[3], invdir[3], tmax. */
 int izpi_gpu_ray_aabb4(izpi_ctx* ctx, const float* boxes, const float* rays, uint32_t n, uint8_t* masks);
 /* Go-math on device, op codes in izpi_amd/csrc/gomath.h order: 0 sin 1 cos 2 tan 3 exp
- * 4 log 5 pow(x,y) 6 atan2(x,y) 7 asin 8 sqrt 9 div(x,y) 10 atan; spectral helpers:
+ * 4 log 5 pow(x,y) 6 atan2(x,y) 7 asin 8 sqrt 9 div(x,y) 10 atan, 11/12 sin/cos from one
+ * shared reduction (x >= 0), 13 the shared-reciprocal vector division (= x / y); 14
+ * calculatePathLength's clamped |exit - p| (dielectric.go:141-150) with x the hit points
+ * and y the exit points as [n][3]; spectral helpers:
  * 32/33 SampleWavelength(x) lambda/pdf (spectral.go:184-224), 34/35/36 GetCIEValues(x)
  * x/y/z (spectral.go:227-253); 37 SpectralConstant.Value(x) of the uploaded scene's texture
  * number y (spectral_constant.go:65-106, needs a scene). */

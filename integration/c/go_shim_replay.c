@@ -18,8 +18,14 @@
  *      spiral order): one izpi_gpu_render with IZPI_OUT_PACKED, tile list in malloc'ed
  *      memory, the packed tiles written out
  *
+ *   With --ref-bvh the scene keeps the host's NewBVH4 tree (Options.BVH != BVHGPU): no
+ *   SKIP_BVH flag and no GPU build.
+ *   The replay is written in the subset tests/go_shim_sequence.py reads (calls of the
+ *   library in plain statements and if conditions, no call inside a ?: arm), which checks
+ *   that its call sequence is the shim's in every branch.
+ *
  *   usage: go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices 0,0,...]
- *                         [--bg-spd] [--tiles N]
+ *                         [--bg-spd] [--tiles N] [--ref-bvh]
  * Exit status 0 on success; the canvas is written as raw little-endian float64.
  */
 #include <stdint.h>
@@ -38,10 +44,11 @@ static int fail(const char* what, const char* msg) {
 int main(int argc, char** argv) {
   if (argc < 6) return fail("usage", "go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices a,b,..]");
   const uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]), spp = (uint32_t)atoi(argv[4]);
-  int png = 0, devices[16], ndev = 0, bg_spd = 0, ntiles = 0;
+  int png = 0, devices[16], ndev = 0, bg_spd = 0, ntiles = 0, ref_bvh = 0;
   for (int i = 6; i < argc; i++) {
     if (!strcmp(argv[i], "--png-pipeline")) png = 1;
     else if (!strcmp(argv[i], "--bg-spd")) bg_spd = 1;
+    else if (!strcmp(argv[i], "--ref-bvh")) ref_bvh = 1;
     else if (!strcmp(argv[i], "--tiles") && i + 1 < argc) ntiles = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--devices") && i + 1 < argc) {
       for (char* t = strtok(argv[++i], ","); t && ndev < 16; t = strtok(NULL, ",")) devices[ndev++] = atoi(t);
@@ -71,7 +78,8 @@ int main(int argc, char** argv) {
   const izpi_scene_input* in = NULL;
   if (izpi_scene_to_input(ps, (double)W / (double)H, 12345, &in)) return fail("izpi_scene_to_input", izpi_host_last_error());
   izpi_host_scene* host = NULL;
-  if (izpi_host_build_scene_ex(in, IZPI_HOST_SKIP_BVH, &host)) return fail("izpi_host_build_scene_ex", izpi_host_last_error());
+  const uint32_t flags = ref_bvh ? 0u : (uint32_t)IZPI_HOST_SKIP_BVH;
+  if (izpi_host_build_scene_ex(in, flags, &host)) return fail("izpi_host_build_scene_ex", izpi_host_last_error());
   /* 4. device(s), GPU BVH4 */
   izpi_ctx* ctx = NULL;
   izpi_multi* m = NULL;
@@ -81,24 +89,30 @@ int main(int argc, char** argv) {
   } else if (izpi_gpu_open(ndev ? devices[0] : 0, &ctx)) {
     return fail("izpi_gpu_open", "");
   }
-  const izpi_scene_desc* desc = izpi_host_scene_desc(host);
-  const uint32_t np = desc->num_tris + desc->num_spheres;
-  if (np > 0) {
-    double* boxes = (double*)malloc(sizeof(double) * 6 * np);
-    izpi_bvh4_node* nodes = (izpi_bvh4_node*)malloc(sizeof(izpi_bvh4_node) * 2 * np);
-    uint32_t* order = (uint32_t*)malloc(sizeof(uint32_t) * np);
-    uint32_t num_nodes = 0;
-    double ms = 0;
-    if (izpi_host_scene_prim_boxes(host, boxes)) return fail("izpi_host_scene_prim_boxes", izpi_host_last_error());
-    if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes, 2 * np, &num_nodes, order, &ms))
-      return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
-    if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
-    free(boxes); free(nodes); free(order);
+  const izpi_scene_desc* desc;
+  if (!ref_bvh) {  /* Options.BVH == BVHGPU */
+    desc = izpi_host_scene_desc(host);
+    const uint32_t np = desc->num_tris + desc->num_spheres;
+    if (np > 0) {
+      double* boxes = (double*)malloc(sizeof(double) * 6 * np);
+      izpi_bvh4_node* nodes = (izpi_bvh4_node*)malloc(sizeof(izpi_bvh4_node) * 2 * np);
+      uint32_t* order = (uint32_t*)malloc(sizeof(uint32_t) * np);
+      uint32_t num_nodes = 0;
+      double ms = 0;
+      if (izpi_host_scene_prim_boxes(host, boxes)) return fail("izpi_host_scene_prim_boxes", izpi_host_last_error());
+      if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes, 2 * np, &num_nodes, order, &ms))
+        return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
+      if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
+      free(boxes); free(nodes); free(order);
+    }
   }
   /* 5. upload and the request */
+  if (m) {
+    if (izpi_gpu_multi_upload_scene(m, izpi_host_scene_desc(host))) return fail("upload", izpi_gpu_multi_last_error(m));
+  } else if (izpi_gpu_upload_scene(ctx, izpi_host_scene_desc(host))) {
+    return fail("upload", izpi_gpu_last_error(ctx));
+  }
   desc = izpi_host_scene_desc(host);
-  if (m ? izpi_gpu_multi_upload_scene(m, desc) : izpi_gpu_upload_scene(ctx, desc))
-    return fail("upload", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
   izpi_render_req req;
   memset(&req, 0, sizeof req);
   req.abi_version = IZPI_ABI_VERSION;
@@ -141,8 +155,11 @@ int main(int argc, char** argv) {
     free(all);
   } else {
     pix = (double*)calloc(nout, sizeof(double));
-    if (m ? izpi_gpu_multi_render(m, &req, pix, NULL) : izpi_gpu_render(ctx, &req, pix, &st))
-      return fail("render", m ? izpi_gpu_multi_last_error(m) : izpi_gpu_last_error(ctx));
+    if (m) {
+      if (izpi_gpu_multi_render(m, &req, pix, NULL)) return fail("render", izpi_gpu_multi_last_error(m));
+    } else if (izpi_gpu_render(ctx, &req, pix, &st)) {
+      return fail("render", izpi_gpu_last_error(ctx));
+    }
   }
   FILE* o = fopen(argv[5], "wb");
   if (!o || fwrite(pix, sizeof(double), nout, o) != nout) return fail("write", argv[5]);
@@ -154,7 +171,7 @@ int main(int argc, char** argv) {
   else izpi_gpu_close(ctx);
   izpi_host_scene_free(host);
   izpi_scene_free(ps);
-  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u, \"bg_spd\": %u, \"tiles\": %d}\n",
-         req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour", ndev > 1 ? ndev : 1, post, req.num_bg_spd, ntiles);
+  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u, \"bg_spd\": %u, \"tiles\": %d, \"ref_bvh\": %d}\n",
+         req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour", ndev > 1 ? ndev : 1, post, req.num_bg_spd, ntiles, ref_bvh);
   return 0;
 }

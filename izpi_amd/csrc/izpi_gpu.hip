@@ -85,7 +85,7 @@ constexpr int MISC_STRIDE = IZPI_MISC_STRIDE;  // words between the fields of iz
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
        CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
        CNT_SCLK_ITEM, CNT_SCLK_REFILL, CNT_SCLK_PUSH, CNT_PARK, CNT_SCLK_MAT, CNT_SCLK_FIN, CNT_SCLK_MIX, CNT_SCLK_LPDF,
-       CNT_SCLK_ENTRY, CNT_SCLK_TEX,
+       CNT_SCLK_ENTRY, CNT_SCLK_TEX, CNT_SCLK_RB1, CNT_SCLK_RATOM, CNT_SCLK_RB2,
        CNT_N };  // SCLK_*: -DIZPI_SHADE_CLOCKS builds only  // CLK_*: -DIZPI_TRACE_CLOCKS builds only
 
 // Frame counters without atomics: a render's kernels add their per-wave counts to the
@@ -100,6 +100,61 @@ IZPI_DEV void count_add(unsigned long long* cpart, unsigned long long* counters,
   if (v == 0) return;
   if (cpart) cpart[(size_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * CNT_N + k] += v;
   else atomicAdd(counters + k, v);
+}
+
+// Loads and stores of the wavefront's streamed state (rays, kind words, path state, hit
+// records, unwinding records, per-sample results). Each pass moves far more of it than the
+// 256-MiB Infinity Cache holds, so it never comes back from there; with IZPI_NT_STREAM=1 it
+// is accessed non-temporally (the `nt` bit), so it need not displace the BVH's lines, which
+// every pass re-reads. Results are unchanged either way.
+#ifndef IZPI_NT_STREAM
+#define IZPI_NT_STREAM 0
+#endif
+template <class T>
+IZPI_DEV T sld(const T* p) {
+  if constexpr (IZPI_NT_STREAM == 0) {
+    return *p;
+  } else {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    T r;
+    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+      v4u w[sizeof(T) / 16];
+#pragma unroll
+      for (uint32_t i = 0; i < sizeof(T) / 16; i++) w[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p) + i);
+      __builtin_memcpy(&r, w, sizeof(T));
+    } else if constexpr (sizeof(T) == 8) {
+      const uint64_t w = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+      __builtin_memcpy(&r, &w, 8);
+    } else {
+      static_assert(sizeof(T) == 4, "streamed loads of 4, 8 or 16k bytes");
+      const uint32_t w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+      __builtin_memcpy(&r, &w, 4);
+    }
+    return r;
+  }
+}
+template <class T>
+IZPI_DEV void sst(T* p, const T& v) {
+  if constexpr (IZPI_NT_STREAM == 0) {
+    *p = v;
+  } else {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+      v4u w[sizeof(T) / 16];
+      __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+      for (uint32_t i = 0; i < sizeof(T) / 16; i++) __builtin_nontemporal_store(w[i], reinterpret_cast<v4u*>(p) + i);
+    } else if constexpr (sizeof(T) == 8) {
+      uint64_t w;
+      __builtin_memcpy(&w, &v, 8);
+      __builtin_nontemporal_store(w, reinterpret_cast<uint64_t*>(p));
+    } else {
+      static_assert(sizeof(T) == 4, "streamed stores of 4, 8 or 16k bytes");
+      uint32_t w;
+      __builtin_memcpy(&w, &v, 4);
+      __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(p));
+    }
+  }
 }
 
 
@@ -649,6 +704,9 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
 // usually left the XCD's L2 by then; the (u, v) arrays it does not need make room for it
 // (31.8 KB of LDS per block: still 5 blocks per CU).
 constexpr uint32_t BVH_LDS_BYTES = 4096;
+#ifndef IZPI_TRACE_STATIC
+#define IZPI_TRACE_STATIC 0
+#endif
 template <int S, int WPE, bool DIST, bool TRI, bool LB, bool RL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
@@ -704,7 +762,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // dequeue atomic on the one counter word (~88/us chip-wide).
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t chunk = min(tchunk, max(16u, (n + nwaves - 1u) / nwaves));
-  if ((uint64_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk >= n) return;
+  // each wave's first range is its own, without an atomic: IZPI_TRACE_STATIC sixteenths of
+  // the queue split evenly (at least one chunk); the rest is dequeued in chunks
+  const uint32_t first = max(chunk, (uint32_t)((uint64_t)n * IZPI_TRACE_STATIC / 16u / nwaves));
+  if ((uint64_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * first >= n) return;
   uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
   uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
   bool busy = false, in_prim = false;
@@ -725,8 +786,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint32_t sh_acc = 0;
 #endif
   // wave-private range [c_pos, c_end) of the input queue; the first one is the wave's own
-  uint32_t c_pos = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * chunk);  // (uniform: SGPR)
-  uint32_t c_end = c_pos + chunk < n ? c_pos + chunk : n;
+  uint32_t c_pos = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * first);  // (uniform: SGPR)
+  uint32_t c_end = c_pos + first < n ? c_pos + first : n;
 #ifdef IZPI_TRACE_CLOCKS
   uint64_t k_refill = 0, k_node = 0, k_prim = 0, k_adv = 0, k0 = 0, k1 = 0;
 #define IZPI_CLK(v) (v) = __builtin_readcyclecounter()
@@ -745,7 +806,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         // atomic: a pass of at most nwaves chunks (the tail passes) dequeues without any.
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(wp.trace_next, chunk);
-        b = __builtin_amdgcn_readfirstlane(b) + nwaves * chunk;
+        b = __builtin_amdgcn_readfirstlane(b) + nwaves * first;
         if (b >= n) exhausted = true;
         c_pos = b;
         c_end = b + chunk < n ? b + chunk : n;
@@ -758,13 +819,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
         const uint32_t my = base + rank;
         if (!busy && rank < take) {
-          const uint32_t k = read_kind ? wp.in.kind[my] : (uint32_t)RAY_MAIN;
+          const uint32_t k = read_kind ? sld(wp.in.kind + my) : (uint32_t)RAY_MAIN;
           // a parked entry is not traced: its hit record (copied by k_shade) stays for the retry
-          const RayOD& r = wp.in.ray[my];
+          // (RL: the ray is read once, here, so it is a streamed load; otherwise primitive
+          // steps read it again)
+          RayOD r;
           if constexpr (RL) {
+            r = sld(wp.in.ray + my);
             const double2* rp = reinterpret_cast<const double2*>(&r);
             const double2 r0 = rp[0], r1 = rp[1], r2 = rp[2];
             ray_lds[3 * threadIdx.x] = r0; ray_lds[3 * threadIdx.x + 1] = r1; ray_lds[3 * threadIdx.x + 2] = r2;
+          } else {
+            r = wp.in.ray[my];
           }
           if (!(k & (RAY_PARKED | RAY_DEAD)) && (uint64_t)__double_as_longlong(r.o[0]) != DEAD_BITS) {
             qi = my;
@@ -782,9 +848,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (!busy) {
               if (!RL && wp.hit_uv) {  // (t, prim) and (u, v) interleaved: hs == 2
                 double2* rec = wp.in.hit + ((size_t)my << 1);
-                rec[0] = hit_pack(0.0, -1); rec[1] = make_double2(0.0, 0.0);
+                sst(rec, hit_pack(0.0, -1)); sst(rec + 1, make_double2(0.0, 0.0));
               } else {
-                wp.in.hit[my] = hit_pack(0.0, -1);
+                sst(wp.in.hit + my, hit_pack(0.0, -1));
               }
             }
           }
@@ -1108,9 +1174,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
         const double2 uv = (!RL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
         if (!RL && wp.hit_uv) {  // (t, prim) and (u, v) in one 32-B record (hs == 2)
           double2* rec = wp.in.hit + ((size_t)qi << 1);
-          rec[0] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim); rec[1] = uv;
+          sst(rec, hit_pack(bprim >= 0 ? tmax : 0.0, bprim)); sst(rec + 1, uv);
         } else {  // nothing reads (u, v): 16 B per entry (hs == 1)
-          wp.in.hit[qi] = hit_pack(bprim >= 0 ? tmax : 0.0, bprim);
+          sst(wp.in.hit + qi, hit_pack(bprim >= 0 ? tmax : 0.0, bprim));
         }
         busy = false;
       }
@@ -1215,7 +1281,10 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
     h.u = 0; h.v = 0;
     if (want_uv && sc.tritex) {  // (u,v) are read only by image textures
       const double eps = 1e-8;
-      double u = uvp->x, v = uvp->y;
+      // (the host keeps huv for every scene that can get here: need_uv = !tri_only || any_uv;
+      // a null record reads as (0, 0) rather than faulting)
+      const double2 huv = uvp ? *uvp : make_double2(0.0, 0.0);
+      double u = huv.x, v = huv.y;
       double w = 1.0 - u - v;
       double sum = u + v + w;
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
@@ -1251,7 +1320,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
     V3 ctr = sph_center(pa, time);
     V3 on = sdiv(sub(h.p, ctr), pa[6]);
     V3 flipped = dot(d, on) >= 0 ? smul(on, -1) : on;
-    h.n = uvp->x == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
+    h.n = (uvp ? uvp->x : 0.0) == 0.0 ? flipped : on;  // second root keeps the unflipped normal (A16)
     if (want_uv) {
       double phi = gm::atan2(flipped.z, flipped.x);
       double theta = gm::asin(flipped.y);
@@ -1497,14 +1566,14 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
                         uint32_t mat) {
   double* rp = rec_ptr<SAMPLER, MATSET>(sp, rslot, blk, depth);
   if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {  // never specular
-    rp[0] = (double)mat;
-    rp[1] = s;
+    sst(rp, (double)mat);
+    sst(rp + 1, s);
     return;
   }
   const double sv = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
-  rp[0] = att.x;
-  if (SAMPLER == IZPI_SAMPLER_COLOUR) { rp[1] = att.y; rp[2] = att.z; }
-  rp[RecLayout<SAMPLER, MATSET>::S] = sv;
+  sst(rp, att.x);
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) { sst(rp + 1, att.y); sst(rp + 2, att.z); }
+  sst(rp + RecLayout<SAMPLER, MATSET>::S, sv);
 }
 IZPI_DEV bool rec_is_spec(double s) { return (uint64_t)__double_as_longlong(s) == REC_SPEC_BITS; }
 // Update P.zf (ZF_*) for the record of the level being written: attenuation att (colour
@@ -1593,7 +1662,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
     // 0.0 + (att*(0*s))/p, which is +0 or NaN, and DeNAN maps NaN to +0 (rgb.go:36),
     // so the result is +0 without reading the records
     double* out = sample_out(sp, P.unit);
-    out[0] = 0.0; out[1] = 0.0; out[2] = 0.0;
+    sst(out, 0.0); sst(out + 1, 0.0); sst(out + 2, 0.0);
     return;
   }
   // A terminal radiance of +0 through levels that all keep a zero a zero (P.zf): the
@@ -1625,7 +1694,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
       for (int j = 0; j < RB; j++) {
         if (dd - j >= 0) {
           const double* r = rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j));
-          rv[j][0] = r[0]; rv[j][1] = r[1]; rv[j][2] = r[2];
+          rv[j][0] = sld(r); rv[j][1] = sld(r + 1); rv[j][2] = sld(r + 2);
         }
       }
 #pragma unroll
@@ -1653,10 +1722,10 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
         if constexpr (D % 2 == 0) {
           const double2* r2 = reinterpret_cast<const double2*>(rp);
 #pragma unroll
-          for (uint32_t q = 0; q < D / 2; q++) { const double2 v = r2[q]; rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
+          for (uint32_t q = 0; q < D / 2; q++) { const double2 v = sld(r2 + q); rv[j][2 * q] = v.x; rv[j][2 * q + 1] = v.y; }
         } else {
 #pragma unroll
-          for (uint32_t q = 0; q < D; q++) rv[j][q] = rp[q];
+          for (uint32_t q = 0; q < D; q++) rv[j][q] = sld(rp + q);
         }
       }
     }
@@ -1692,13 +1761,13 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   double* out = sample_out(sp, P.unit);
   if (SAMPLER == IZPI_SAMPLER_COLOUR) {
     V3 c = denan(L);  // rgb.go:36 DeNAN per sample
-    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+    sst(out, c.x); sst(out + 1, c.y); sst(out + 2, c.z);
   } else {
     double cx, cy, cz;  // render/spectral.go:162-166
     if (sp.staged) cie_values<true>(P.lambda, cx, cy, cz);
     else cie_values<false>(P.lambda, cx, cy, cz);
     const V3 o = sdiv(mk(L.x * cx, L.x * cy, L.x * cz), P.lpdf);  // three divisions by lpdf
-    out[0] = o.x; out[1] = o.y; out[2] = o.z;
+    sst(out, o.x); sst(out + 1, o.y); sst(out + 2, o.z);
   }
 }
 
@@ -1741,7 +1810,7 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
     else sample_wavelength<false>(r, P.lambda, P.lpdf);
     if (P.lpdf == 0) {  // render/spectral.go:78-80: skipped, still counted in 1/spp
       double* out = sample_out(sp, unit);
-      out[0] = 0; out[1] = 0; out[2] = 0;
+      sst(out, 0.0); sst(out + 1, 0.0); sst(out + 2, 0.0);
       return false;
     }
   }
@@ -1780,23 +1849,23 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
 template <int SAMPLER>
 IZPI_DEV void store_entry(const WaveBuf& b, uint32_t pos, const PathSt& P, const RayRec& R) {
   double2* r = reinterpret_cast<double2*>(b.ray + pos);
-  r[0] = make_double2(R.o[0], R.o[1]);
-  r[1] = make_double2(R.o[2], R.d[0]);
-  r[2] = make_double2(R.d[1], R.d[2]);
-  b.kind[pos] = R.kind;
-  if (b.time) b.time[pos] = R.time;
-  b.path[pos] = PathHot{P.rng, P.depth | P.zf << 16, P.unit, P.rslot};
-  if (b.blk) b.blk[pos] = P.blk;
+  sst(r, make_double2(R.o[0], R.o[1]));
+  sst(r + 1, make_double2(R.o[2], R.d[0]));
+  sst(r + 2, make_double2(R.d[1], R.d[2]));
+  sst(b.kind + pos, R.kind);
+  if (b.time) sst(b.time + pos, R.time);
+  sst(b.path + pos, PathHot{P.rng, P.depth | P.zf << 16, P.unit, P.rslot});
+  if (b.blk) sst(b.blk + pos, P.blk);
   if (b.cold) {
     double2* c = reinterpret_cast<double2*>(b.cold + pos);
-    if (SAMPLER == IZPI_SAMPLER_SPECTRAL) c[0] = make_double2(P.lambda, P.lpdf);
-    if (kind_of(R.kind) == RAY_PATHLEN) { c[1] = make_double2(P.pend[0], P.pend[1]); c[2] = make_double2(P.pend[2], 0.0); }
+    if (SAMPLER == IZPI_SAMPLER_SPECTRAL) sst(c, make_double2(P.lambda, P.lpdf));
+    if (kind_of(R.kind) == RAY_PATHLEN) { sst(c + 1, make_double2(P.pend[0], P.pend[1])); sst(c + 2, make_double2(P.pend[2], 0.0)); }
   }
 }
 // A parked entry moves to the output unchanged (its hit record too), flagged RAY_PARKED.
 IZPI_DEV void dead_entry(const WaveBuf& out, uint32_t pos) {
-  out.kind[pos] = RAY_DEAD;
-  out.ray[pos].o[0] = __longlong_as_double((long long)DEAD_BITS);
+  sst(out.kind + pos, (uint32_t)RAY_DEAD);
+  sst(&out.ray[pos].o[0], __longlong_as_double((long long)DEAD_BITS));
 }
 IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint32_t pos) {
   out.ray[pos] = in.ray[i];
@@ -1817,17 +1886,17 @@ struct EntryIn {
   double time;
 };
 IZPI_DEV void load_entry(const WaveBuf& b, uint32_t i, EntryIn& E) {
-  E.ray = b.ray[i];
-  E.hit = b.hit[(size_t)i * b.hs];
-  E.time = b.time ? b.time[i] : 0.0;
+  E.ray = sld(b.ray + i);
+  E.hit = sld(b.hit + (size_t)i * b.hs);
+  E.time = b.time ? sld(b.time + i) : 0.0;
 }
 template <int SAMPLER>
 IZPI_DEV void load_path(const WaveBuf& b, uint32_t i, PathSt& P) {
-  const PathHot ph = b.path[i];
+  const PathHot ph = sld(b.path + i);
   P.rng = ph.rng; P.depth = ph.depth & 0xFFFFu; P.zf = ph.depth >> 16; P.unit = ph.unit; P.rslot = ph.rslot;
-  P.blk = b.blk ? b.blk[i] : 0u;
+  P.blk = b.blk ? sld(b.blk + i) : 0u;
   P.lambda = 0; P.lpdf = 1;
-  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { const double2 c = *reinterpret_cast<const double2*>(b.cold + i); P.lambda = c.x; P.lpdf = c.y; }
+  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) { const double2 c = sld(reinterpret_cast<const double2*>(b.cold + i)); P.lambda = c.x; P.lpdf = c.y; }
 }
 
 // Take units for the lanes that ask (one atomic per wave); returns UINT32_MAX when drained.
@@ -1890,6 +1959,40 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
   if (j == 0) *wp.out_count = fill;
 }
 
+#ifdef IZPI_SHADE_CLOCKS
+// Timing builds only: wave cycles per section of shade_item, accumulated in LDS by the
+// first active lane of the wave that runs the section (so divergent sections count the
+// wave's time once), added to the CNT_SCLK_* counters at the end of the kernel.
+enum { SCLK_MAT = 0, SCLK_FIN, SCLK_MIX, SCLK_LPDF, SCLK_ENTRY, SCLK_TEX, SCLK_RB1, SCLK_RATOM, SCLK_RB2, SCLK_N };
+IZPI_DEV unsigned long long* sclk_lds() {
+  __shared__ unsigned long long c[16][SCLK_N];
+  return &c[(threadIdx.x >> 6) & 15][0];
+}
+IZPI_DEV void sclk_add(int sec, uint64_t dt) {
+  const uint64_t act = __ballot(1);
+  if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)act) - 1)) sclk_lds()[sec] += dt;
+}
+IZPI_DEV void sclk_flush(unsigned long long* counters) {
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < SCLK_N; k++) atomicAdd(counters + CNT_SCLK_MAT + k, sclk_lds()[k]);
+}
+IZPI_DEV void sclk_zero() {
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < SCLK_N; k++) sclk_lds()[k] = 0;
+  __syncthreads();
+}
+#define SCLK_T(v) const uint64_t v = __builtin_readcyclecounter()
+#define SCLK_ADD(sec, t0) sclk_add(sec, __builtin_readcyclecounter() - (t0))
+// wait for every outstanding vector memory access (vmcnt(0); expcnt, lgkmcnt left alone):
+// separates a section's memory wait from the work after it
+#define SCLK_VMWAIT() __builtin_amdgcn_s_waitcnt(0x0F70)
+#else
+#define SCLK_VMWAIT() (void)0
+#define SCLK_T(v) (void)0
+#define SCLK_ADD(sec, t0) (void)0
+#endif
+
 // One block-wide reservation phase for a shading iteration (ONE pair of barriers, two
 // atomics by one thread): `unit_want` lanes get consecutive work units from the unit
 // head (the units past total_units are not granted); lanes with `put` and granted
@@ -1905,28 +2008,37 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   const uint64_t lt = (1ull << lane) - 1;
   const uint64_t mp = __ballot(put), mu = __ballot(unit_want);
   if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); }
+  SCLK_T(rb0);
   __syncthreads();
+  SCLK_ADD(SCLK_RB1, rb0);
+  SCLK_T(rb1);
+  // both atomics in flight together: entries are reserved for every unit_want lane
+  // until this block has seen the unit head run out (`exhausted`, thread 0's register);
+  // a lane reserved an entry but denied a unit leaves a dead entry (at most one
+  // iteration per block, in the frame's last passes)
+  uint32_t np = 0, nu = 0, u0 = 0, pb = 0;
   if (threadIdx.x == 0) {
-    // both atomics in flight together: entries are reserved for every unit_want lane
-    // until this block has seen the unit head run out (`exhausted`, thread 0's register);
-    // a lane reserved an entry but denied a unit leaves a dead entry (at most one
-    // iteration per block, in the frame's last passes)
-    uint32_t np = 0, nu = 0;
 #pragma unroll
     for (uint32_t k = 0; k < SHADE_WAVES; k++) { np += s_p[b][k]; nu += s_u[b][k]; }
     if (exhausted) nu = 0;
+    u0 = nu ? atomicAdd(sp.head, nu) : sp.total_units;
+    pb = np + nu ? atomicAdd(out_count, np + nu) : 0u;
+  }
+  if (threadIdx.x == 0) {
     const uint32_t ne = np + nu;
-    const uint32_t u0 = nu ? atomicAdd(sp.head, nu) : sp.total_units;
     // (an iteration without finished paths asks for nothing and learns nothing: it must
     // not mark the block exhausted, or the block's later finished paths lose their slots)
     if (nu && u0 + nu >= sp.total_units) exhausted = true;
-    s_pbase[b] = ne ? atomicAdd(out_count, ne) : 0u;
+    s_pbase[b] = pb;
     s_ubase[b] = u0;
     s_granted[b] = u0 >= sp.total_units ? 0u : min(nu, sp.total_units - u0);
     s_nput[b] = np;
     s_nent[b] = ne;
+    SCLK_VMWAIT();
+    SCLK_ADD(SCLK_RATOM, rb1);
   }
   __syncthreads();
+  SCLK_ADD(SCLK_RB2, rb1);
   uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
   for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
   const bool has_entry = unit_want && s_nput[b] + ur < s_nent[b];
@@ -1957,39 +2069,15 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
 }
 
 
-#ifdef IZPI_SHADE_CLOCKS
-// Timing builds only: wave cycles per section of shade_item, accumulated in LDS by the
-// first active lane of the wave that runs the section (so divergent sections count the
-// wave's time once), added to the CNT_SCLK_* counters at the end of the kernel.
-enum { SCLK_MAT = 0, SCLK_FIN, SCLK_MIX, SCLK_LPDF, SCLK_ENTRY, SCLK_TEX, SCLK_N };
-IZPI_DEV unsigned long long* sclk_lds() {
-  __shared__ unsigned long long c[16][SCLK_N];
-  return &c[(threadIdx.x >> 6) & 15][0];
+
+// calculatePathLength's length of a found exit point (dielectric.go:141-150): |exit - p|
+// clamped to [0.1, 100]
+IZPI_DEV double path_length(V3 hp, V3 exit_p) {
+  double len = length(sub(exit_p, hp));
+  if (len < 0.1) len = 0.1;
+  if (len > 100.0) len = 100.0;
+  return len;
 }
-IZPI_DEV void sclk_add(int sec, uint64_t dt) {
-  const uint64_t act = __ballot(1);
-  if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)act) - 1)) sclk_lds()[sec] += dt;
-}
-IZPI_DEV void sclk_flush(unsigned long long* counters) {
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0)
-    for (int k = 0; k < SCLK_N; k++) atomicAdd(counters + CNT_SCLK_MAT + k, sclk_lds()[k]);
-}
-IZPI_DEV void sclk_zero() {
-  if ((threadIdx.x & 63) == 0)
-    for (int k = 0; k < SCLK_N; k++) sclk_lds()[k] = 0;
-  __syncthreads();
-}
-#define SCLK_T(v) const uint64_t v = __builtin_readcyclecounter()
-#define SCLK_ADD(sec, t0) sclk_add(sec, __builtin_readcyclecounter() - (t0))
-// wait for every outstanding vector memory access (vmcnt(0); expcnt, lgkmcnt left alone):
-// separates a section's memory wait from the work after it
-#define SCLK_VMWAIT() __builtin_amdgcn_s_waitcnt(0x0F70)
-#else
-#define SCLK_VMWAIT() (void)0
-#define SCLK_T(v) (void)0
-#define SCLK_ADD(sec, t0) (void)0
-#endif
 
 // One shading pass of `slot` (its ray was traced): Colour.Sample / SampleSpectral
 // one bounce deep (colour.go:33-65, sampler/spectral.go:47-80). Sets `push` when the path
@@ -2026,13 +2114,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
     // calculatePathLength result (dielectric.go:135-152) -> finish the glass bounce
     const PathCold& pc = in.cold[i];
     const V3 hp = mk(pc.pend[0], pc.pend[1], pc.pend[2]);
-    double len = 10.0;
-    if (H.prim >= 0) {
-      V3 exit_p = add(ro, smul(rd, H.t));
-      len = length(sub(exit_p, hp));
-      if (len < 0.1) len = 0.1;
-      if (len > 100.0) len = 100.0;
-    }
+    const double len = H.prim >= 0 ? path_length(hp, add(ro, smul(rd, H.t))) : 10.0;  // no exit: dielectric.go:152
     const uint32_t mat_id = R.kind >> KIND_MAT_SHIFT;  // dielectric material stashed by the glass bounce
     const izpi_material gm_ = mat_rec(sc, st, mat_id);
     if (COLOUR) att = mk(gm::exp(-gm_.rgb[0] * len), gm::exp(-gm_.rgb[1] * len), gm::exp(-gm_.rgb[2] * len));
@@ -2212,7 +2294,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         SCLK_T(sc3);
         const double pdf_val = 0.5 * lights_pdf(sc, st, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         SCLK_ADD(SCLK_LPDF, sc3);
-        rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth)[RecLayout<SAMPLER, MATSET>::P] = pdf_val;
+        sst(rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth) + RecLayout<SAMPLER, MATSET>::P, pdf_val);
         if constexpr (ms_spec(MATSET) || SAMPLER == IZPI_SAMPLER_SPECTRAL) rec_zero_track<SAMPLER>(P.zf, false, att, spdf, pdf_val);
         next_d = dir;
       } else {
@@ -2331,7 +2413,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       // the kind word, path state, ray and hit record in one round of loads (a dead entry's
       // path and hit are read too, and ignored): waiting for the kind word first, then the
       // path, then the ray put three memory round trips in front of every item
-      kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
+      kind = sld(wp.in.kind + i) & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
       load_path<SAMPLER>(wp.in, i, P);
       load_entry(wp.in, i, E);
     }
@@ -2500,7 +2582,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
 #pragma unroll
       for (int i = 0; i < 6; i++) {
         const uint32_t q = lane + 64 * i, j = q / 6, c = q % 6;
-        v[i] = s2[(size_t)j * run + (k >> 1) * 3 + c];
+        v[i] = sld(s2 + (size_t)j * run + (k >> 1) * 3 + c);
       }
 #pragma unroll
       for (int i = 0; i < 6; i++) w[lane + 64 * i] = v[i];
@@ -2717,6 +2799,10 @@ __global__ void k_aabb4(const float* boxes, const float* rays, uint32_t n, uint8
 __global__ void k_gomath(const DevScene sc, int op, const double* x, const double* y, uint32_t n, double* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
+  if (op == 14) {  // path_length(hit point x[i], exit point y[i]): 3 doubles each
+    out[i] = path_length(mk(x[3 * i], x[3 * i + 1], x[3 * i + 2]), mk(y[3 * i], y[3 * i + 1], y[3 * i + 2]));
+    return;
+  }
   double a = x[i], b = y ? y[i] : 0.0, r;
   switch (op) {
     case 0: r = gm::sin(a); break;
@@ -2975,10 +3061,16 @@ struct Tracer {
   size_t spill_bytes = 0;  // the per-thread traversal-stack spill area this launch needs
 };
 
+// The request's tuning. ABI 1's izpi_render_tuning ended at tail_paths (an ABI-1 request,
+// abi_version 0, has its tuning pointer at the same place): its fields are read and the
+// later ones keep their defaults.
 const izpi_render_tuning kDefaultTuning{};
-inline const izpi_render_tuning& tuning_of(const izpi_render_req* req) {
-  // an ABI-1 request (abi_version 0) ends before `tuning`: nothing past it is read
-  return req && req->abi_version >= 2 && req->tuning ? *req->tuning : kDefaultTuning;
+inline izpi_render_tuning tuning_of(const izpi_render_req* req) {
+  izpi_render_tuning t{};
+  if (!req || !req->tuning) return t;
+  if (req->abi_version >= 2) return *req->tuning;
+  memcpy(&t, req->tuning, offsetof(izpi_render_tuning, tail_paths) + sizeof(t.tail_paths));
+  return t;
 }
 
 #define IZPI_T2_LIST(X)                                                                                      \
@@ -3204,7 +3296,18 @@ int apply_post(izpi_ctx* ctx, const izpi_render_req* req, double* canvas_dev) {
   return IZPI_OK;
 }
 
+int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev);
+// One render on one context. The progress counters (izpi_gpu_progress) start at 0/0 before
+// any check and read done == total on every return, failed calls included.
 int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
+  ctx->prog_done.store(0, std::memory_order_relaxed);
+  ctx->prog_total.store(0, std::memory_order_relaxed);
+  const int rc = render_body(ctx, req, out_dev);
+  ctx->prog_done.store(ctx->prog_total.load(std::memory_order_relaxed), std::memory_order_relaxed);
+  return rc;
+}
+
+int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (ctx->fault_inject == 2) { ctx->err = "injected render fault (izpi_gpu_debug_fault)"; return IZPI_ERR_DEVICE; }
   if (!ctx->have_scene) { ctx->err = "render before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
@@ -3230,7 +3333,6 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const uint64_t num_pixels64 = (uint64_t)ntiles * tw * th;
   if (num_pixels64 > (1ull << 30)) { ctx->err = "too many pixels in one request"; return IZPI_ERR_INVALID; }
   const uint32_t num_pixels = (uint32_t)num_pixels64;
-  ctx->prog_done.store(0, std::memory_order_relaxed);
   ctx->prog_total.store(num_pixels64 * req->spp, std::memory_order_relaxed);
   if (ctx->stack_needed > 64) { ctx->err = "BVH deeper than the 64-entry traversal stack (bvh4.go:71)"; return IZPI_ERR_UNSUPPORTED; }
   const izpi_render_tuning& tu = tuning_of(req);
@@ -3448,9 +3550,11 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.alloc_ms = alloc_ms;
   if (rec_pool && s.parks * 64 > s.rays && pool_blocks < slots) ctx->pool_grow++;
 #ifdef IZPI_SHADE_CLOCKS
-  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu mat %llu finish %llu mix %llu lpdf %llu entry %llu tex %llu (wave cycles)\n",
+  fprintf(stderr, "IZPI_SHADE_CLOCKS item %llu refill %llu push %llu mat %llu finish %llu mix %llu lpdf %llu entry %llu tex %llu "
+          "res_barrier1 %llu res_atomics %llu res_barrier2 %llu (wave cycles; res_atomics: thread 0 only)\n",
           cnt[CNT_SCLK_ITEM], cnt[CNT_SCLK_REFILL], cnt[CNT_SCLK_PUSH], cnt[CNT_SCLK_MAT], cnt[CNT_SCLK_FIN],
-          cnt[CNT_SCLK_MIX], cnt[CNT_SCLK_LPDF], cnt[CNT_SCLK_ENTRY], cnt[CNT_SCLK_TEX]);
+          cnt[CNT_SCLK_MIX], cnt[CNT_SCLK_LPDF], cnt[CNT_SCLK_ENTRY], cnt[CNT_SCLK_TEX], cnt[CNT_SCLK_RB1],
+          cnt[CNT_SCLK_RATOM], cnt[CNT_SCLK_RB2]);
 #endif
 #ifdef IZPI_SHADOW
   fprintf(stderr, "IZPI_SHADOW spill_stores %llu spill_loads %llu (entries)\n", cnt[CNT_CLK_REFILL], cnt[CNT_CLK_NODE]);
@@ -3659,6 +3763,48 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       }
     }
   }
+#ifdef IZPI_NODE_ORDER
+  // measurement builds: inner nodes renumbered depth-first (1: pre-order in slot order, the
+  // order a ray's first-hit-child descent takes; 2: treelets of 3 levels stored together,
+  // breadth-first inside, treelets in depth-first order). Traversal order, floats and
+  // counters are unchanged: only the addresses move.
+  if (n_inner > 1 && ref[0] >= 0) {
+    std::vector<int32_t> perm(n_inner, -1);  // old -> new
+    uint32_t next = 0;
+    if (IZPI_NODE_ORDER == 1) {
+      std::vector<int32_t> st{ref[0]};
+      while (!st.empty()) {
+        const int32_t o = st.back(); st.pop_back();
+        perm[(size_t)o] = (int32_t)next++;
+        for (int i = 3; i >= 0; i--) if (inner[(size_t)o].child[i] >= 0) st.push_back(inner[(size_t)o].child[i]);
+      }
+    } else {
+      std::vector<int32_t> roots{ref[0]};
+      while (!roots.empty()) {
+        const int32_t tr = roots.back(); roots.pop_back();
+        std::vector<int32_t> lvl{tr}, below;
+        for (int depth = 0; depth < 3 && !lvl.empty(); depth++) {
+          std::vector<int32_t> nx;
+          for (int32_t o : lvl) {
+            perm[(size_t)o] = (int32_t)next++;
+            for (int i = 0; i < 4; i++) if (inner[(size_t)o].child[i] >= 0) nx.push_back(inner[(size_t)o].child[i]);
+          }
+          lvl.swap(nx);
+        }
+        for (auto it = lvl.rbegin(); it != lvl.rend(); ++it) roots.push_back(*it);
+      }
+    }
+    std::vector<GInner> re(inner.size());
+    for (uint32_t o = 0; o < n_inner; o++) {
+      if (perm[o] < 0) { ctx->err = "unreachable inner node"; return IZPI_ERR_INVALID; }
+      GInner g = inner[o];
+      for (int i = 0; i < 4; i++) if (g.child[i] >= 0) g.child[i] = perm[(size_t)g.child[i]];
+      re[(size_t)perm[o]] = g;
+    }
+    inner.swap(re);
+    for (uint32_t k = 0; k < d->num_nodes; k++) if (ref[k] >= 0) ref[k] = perm[(size_t)ref[k]];
+  }
+#endif
   // ---- primitives in leaf order
   std::vector<GPrim> prims(d->num_prims);
   std::vector<GShade> shade(d->num_prims);
@@ -4127,15 +4273,17 @@ int izpi_gpu_gomath(izpi_ctx* ctx, int op, const double* x, const double* y, uin
     for (uint32_t i = 0; i < n; i++)
       if (!(y[i] >= 0 && y[i] < (double)ctx->num_textures)) { ctx->err = "texture number out of range"; return IZPI_ERR_INVALID; }
   }
+  if (op == 14 && !y) { ctx->err = "path length without exit points"; return IZPI_ERR_INVALID; }
+  const size_t nin = op == 14 ? 3 * (size_t)n : n;  // op 14 reads 3-vectors
   HIP_TRY(hipSetDevice(ctx->device));
   DevBufs tmp;  // freed on every return
   double *dx, *dy = nullptr, *dout;
-  HIP_TRY(tmp.alloc(&dx, n));
+  HIP_TRY(tmp.alloc(&dx, nin));
   HIP_TRY(tmp.alloc(&dout, n));
-  HIP_TRY(hipMemcpy(dx, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dx, x, nin * sizeof(double), hipMemcpyHostToDevice));
   if (y) {
-    HIP_TRY(tmp.alloc(&dy, n));
-    HIP_TRY(hipMemcpy(dy, y, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(tmp.alloc(&dy, nin));
+    HIP_TRY(hipMemcpy(dy, y, nin * sizeof(double), hipMemcpyHostToDevice));
   }
   hipLaunchKernelGGL(k_gomath, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->sc, op, dx, dy, n, dout);
   HIP_TRY(hipGetLastError());
@@ -4309,23 +4457,29 @@ __global__ void k_stall(const volatile uint32_t* release) {
 }
 
 // Wait for this context's stream (a collective step) as a rank that may outlive its peers:
-// poll the stream and the communicator's asynchronous error; an RCCL error or a wait past
-// the deadline aborts the communicator and returns IZPI_ERR_PEER (render/remote.go:40-55
-// logs a failed remote tile and carries on; here the call returns instead of hanging).
+// poll the stream and the communicator's asynchronous error; an RCCL error, a HIP error of
+// this rank's stream or a wait past the deadline aborts the communicator and returns
+// IZPI_ERR_PEER (render/remote.go:40-55 logs a failed remote tile and carries on; here the
+// call returns instead of hanging). After a local HIP error this rank cannot join the
+// remaining collectives, and peers blocked in them would never return: aborting the
+// communicator ends their waits too (they see the async error), and the communicator is
+// gone on this rank (izpi_gpu_comm_init makes a new one).
 int wait_peers(izpi_ctx* ctx, uint32_t timeout_ms, const char* step) {
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t naps = 0;
   for (;;) {
-    const hipError_t q = hipStreamQuery(ctx->stream);
+    hipError_t q = hipStreamQuery(ctx->stream);
+    if (ctx->fault_inject == 4 && q != hipErrorNotReady) q = hipErrorLaunchFailure;  // test hook: a failed stream
     if (q == hipSuccess) return IZPI_OK;
-    if (q != hipErrorNotReady) { ctx->err = std::string(step) + ": " + hipGetErrorString(q); return IZPI_ERR_HIP; }
     ncclResult_t ae = ncclSuccess;
-    const ncclResult_t qr = ncclCommGetAsyncError(ctx->comm, &ae);
+    const ncclResult_t qr = q == hipErrorNotReady ? ncclCommGetAsyncError(ctx->comm, &ae) : ncclSuccess;
     const bool failed = qr != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (failed || (timeout_ms && ms > timeout_ms)) {
-      ctx->err = std::string(step) + (failed ? ": RCCL reported " + std::string(ncclGetErrorString(qr != ncclSuccess ? qr : ae))
-                                             : ": no answer from the other ranks within " + std::to_string(timeout_ms) + " ms") +
+    if (q != hipErrorNotReady || failed || (timeout_ms && ms > timeout_ms)) {
+      ctx->err = std::string(step) +
+                 (q != hipErrorNotReady ? ": this rank's stream failed: " + std::string(hipGetErrorString(q))
+                  : failed ? ": RCCL reported " + std::string(ncclGetErrorString(qr != ncclSuccess ? qr : ae))
+                           : ": no answer from the other ranks within " + std::to_string(timeout_ms) + " ms") +
                  "; communicator aborted";
       // test hook: let the stall drain first (ncclCommAbort waits for the operations it
       // aborts, which sit behind it on the stream)
@@ -4392,6 +4546,8 @@ int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_
   // without a communicator no collective can run: every rank in this state returns here
   if (!ctx->comm || !ctx->d_status) { ctx->err = "render_rank before izpi_gpu_comm_init"; return IZPI_ERR_INVALID; }
   memset(&ctx->last, 0, sizeof(ctx->last));
+  ctx->prog_done.store(0, std::memory_order_relaxed);  // (no stale count while the ranks agree)
+  ctx->prog_total.store(0, std::memory_order_relaxed);
   if (stats) *stats = ctx->last;
   const uint32_t timeout_ms = tuning_of(req).peer_timeout_ms;
   // ---- 1 (local failures, HIP ones included, are recorded and agreed on, not returned early)
@@ -4493,7 +4649,7 @@ int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* sam
 }
 
 int izpi_gpu_debug_fault(izpi_ctx* ctx, int where) {
-  if (!ctx) return IZPI_ERR_INVALID;
+  if (!ctx || where < 0 || where > 4) return IZPI_ERR_INVALID;
   ctx->fault_inject = where;
   return IZPI_OK;
 }

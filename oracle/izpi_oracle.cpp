@@ -662,6 +662,15 @@ struct Hitable {
   uint32_t ref = 0;  // IZPI_PRIM_REF in transport order
 };
 
+struct Mat3 { double A11, A12, A13, A21, A22, A23, A31, A32, A33; };  // mat3.go:6-16
+// mat3.go:19-31: the tangent, bitangent and normal as the matrix's columns
+Mat3 NewTBN(Vec3 t, Vec3 b, Vec3 n) { return Mat3{t.X, b.X, n.X, t.Y, b.Y, n.Y, t.Z, b.Z, n.Z}; }
+// mat3.go:34-40 (no FMA: Go on amd64 rounds each product and sum)
+Vec3 MatrixVectorMul(const Mat3& a, Vec3 v) {
+  return V(a.A11 * v.X + a.A12 * v.Y + a.A13 * v.Z, a.A21 * v.X + a.A22 * v.Y + a.A23 * v.Z,
+           a.A31 * v.X + a.A32 * v.Y + a.A33 * v.Z);
+}
+
 struct Triangle : Hitable {  // triangle.go
   Vec3 vertex0, vertex1, vertex2, edge1, edge2, normal, tangent, bitangent;
   double area = 0, u0 = 0, u1 = 0, u2 = 0, v0 = 0, v1 = 0, v2 = 0;
@@ -721,10 +730,7 @@ struct Triangle : Hitable {  // triangle.go
     if (!nm) { rec = NewHR(t, uu, vv, PointAtParameter(r, t), nrm); return true; }
     Vec3 nts = nm->Value(uu, vv, Vec3());
     nts.X = 2 * nts.X - 1.0; nts.Y = 2 * nts.Y - 1.0; nts.Z = 2 * nts.Z - 1.0;
-    // mat3.NewTBN(t, b, n) columns; MatrixVectorMul (mat3.go:19-40)
-    Vec3 nn = V(tangent.X * nts.X + bitangent.X * nts.Y + nrm.X * nts.Z,
-                tangent.Y * nts.X + bitangent.Y * nts.Y + nrm.Y * nts.Z,
-                tangent.Z * nts.X + bitangent.Z * nts.Y + nrm.Z * nts.Z);
+    Vec3 nn = MatrixVectorMul(NewTBN(tangent, bitangent, nrm), nts);  // triangle.go:260-261
     rec = NewHR(t, uu, vv, PointAtParameter(r, t), MakeUnitVector(nn));
     return true;
   }
@@ -1751,6 +1757,33 @@ int oracle_triangle_hit(const double* tri, const double* ray, double* out) {
   }
   delete t;
   return hit ? 1 : 0;
+}
+
+/* mat3_test.go:10-54: MatrixVectorMul(NewTBN(t, b, n), v); in = t[3] b[3] n[3] v[3]. */
+void oracle_tbn_mul(const double* in, double* out3) {
+  const Vec3 r = MatrixVectorMul(NewTBN(Load(in), Load(in + 3), Load(in + 6)), Load(in + 9));
+  out3[0] = r.X; out3[1] = r.Y; out3[2] = r.Z;
+}
+
+/* dielectric_test.go:47-84: Dielectric.calculatePathLength against a world whose Hit
+ * always returns the exit point `exit3` (mockSceneGeometry); in = hit point p[3], normal
+ * n[3], ray o[3] d[3], scattered direction s[3]. */
+double oracle_path_length(const double* in, const double* exit3) {
+  struct Mock : SceneGeometry {
+    Vec3 exit;
+    bool Hit(const Ray&, double, double, HitRecord& rec, const Material*& mat) const override {
+      rec = NewHR(2.0, 0.0, 0.0, exit, V(0, 0, 1));
+      mat = nullptr;
+      return true;
+    }
+  } world;
+  world.exit = Load(exit3);
+  Dielectric d;
+  d.refIdx = 1.5;
+  d.world = &world;
+  const HitRecord hr = NewHR(1.0, 0.0, 0.0, Load(in), Load(in + 3));
+  const Ray r = NewRay(Load(in + 6), Load(in + 9), 0.0), scattered = NewRay(Load(in + 6), Load(in + 12), 0.0);
+  return d.calculatePathLength(r, hr, scattered);
 }
 
 double oracle_gomath(int op, double x, double y) {

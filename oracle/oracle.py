@@ -81,6 +81,9 @@ def lib():
     L.oracle_spectral_value.restype = C.c_double
     L.oracle_spd_tabulated_value.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_double]
     L.oracle_spd_tabulated_value.restype = C.c_double
+    L.oracle_tbn_mul.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.oracle_path_length.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.oracle_path_length.restype = C.c_double
     _lib = L
     return L
 

@@ -7,6 +7,13 @@ Sources (read-only reference, /root/reference/internal):
   hitable/triangle_test.go:15-134    NewTriangleWithUV fields; Triangle.Hit 4 cases
   grid/grid_test.go:9-77             spiral tile order 3x3, 4x4, 5x5
   material/dielectric_test.go:28-45  Beer-Lambert exp(-0.5*1) = 0.6065 +- 1e-3
+  material/dielectric_test.go:47-84  calculatePathLength against mockSceneGeometry (its Hit
+                                     always returns the exit point (0.5, 0.5, 1.5)): the hit
+                                     point (0.5, 0.5, 0.5) is 1.0 from it, inside the
+                                     [0.1, 10] bounds the test asserts; the exact 1.0 is
+                                     Length(exit - p) by dielectric.go:141-150
+  mat3/mat3_test.go:10-54            MatrixVectorMul of the identity and of NewTBN(t, b, n)
+                                     for the XY, XZ and YZ planes, exact (cmp.Diff)
   fastrandom/fastrandom.go:41-47     LCG seed 12345 (dielectric_test.go:108): derived
                                      here by exact integer arithmetic.
 Run: python tests/golden/make_golden.py
@@ -70,6 +77,16 @@ def main():
         "spiral": spiral,
         "beer_lambert": {"peak": 0.5, "center": 480.0, "width": 60.0, "lambda": 480.0, "path": 1.0, "expected": 0.6065, "tol": 1e-3},
         "lcg_seed_12345": {"values": vals, "states": states},
+        # mat3_test.go: (t, b, n) are the matrix's columns (NewTBN, mat3.go:19-31); the
+        # identity case is Mat3{A11: 1, A22: 1, A33: 1}, i.e. columns x, y, z
+        "mat3_tbn": [
+            {"name": "Multiply by identity", "t": [1, 0, 0], "b": [0, 1, 0], "n": [0, 0, 1], "v": [1, 2, 3], "want": [1, 2, 3]},
+            {"name": "TBN XY plane", "t": [-1, 0, 0], "b": [0, 1, 0], "n": [0, 0, -1], "v": [0, 0, 1], "want": [0, 0, -1]},
+            {"name": "TBN XZ plane", "t": [-1, 0, 0], "b": [0, 0, 1], "n": [0, 1, 0], "v": [0, 0, 1], "want": [0, 1, 0]},
+            {"name": "TBN YZ plane", "t": [0, 0, 1], "b": [0, 1, 0], "n": [-1, 0, 0], "v": [0, 0, 1], "want": [-1, 0, 0]},
+        ],
+        "path_length": {"hit_p": [0.5, 0.5, 0.5], "hit_n": [0.577, 0.577, 0.577], "ray_o": [0, 0, -2], "ray_d": [0, 0, 1],
+                        "scattered_d": [0, 0, 1], "mock_exit": [0.5, 0.5, 1.5], "bounds": [0.1, 10.0], "expected": 1.0},
     }
     (Path(__file__).parent / "reference_kats.json").write_text(json.dumps(out, indent=1))
 

@@ -694,6 +694,63 @@ def test_render_rank_stalled_peer_hits_the_deadline(gpu):
     r.close()
 
 
+def test_render_rank_failed_stream_aborts_the_communicator(gpu):
+    """A rank whose stream fails in a collective step (izpi_gpu_debug_fault 4: the polls of
+    the step see a HIP error, as after a sticky device fault) cannot join the remaining
+    collectives: it aborts the communicator, so that peers blocked in them see the abort
+    instead of waiting forever (peer_timeout_ms 0, the default), and returns IZPI_ERR_PEER;
+    the communicator is gone, and after a new izpi_gpu_comm_init the context renders
+    bit-exact again."""
+    import ctypes as C
+    import torch
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 64, 64, 4)
+    L = N.lib()
+    cid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    assert L.izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    canvas = torch.zeros((64, 64, 4), dtype=torch.float64, device="cuda:0")
+    req = r.request()
+    st = N.RenderStats()
+    assert L.izpi_gpu_debug_fault(r.ctx, 5) == N.IZPI_ERR_INVALID
+    assert L.izpi_gpu_debug_fault(r.ctx, 4) == 0
+    rc = L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st))
+    assert rc == N.IZPI_ERR_PEER, (rc, L.izpi_gpu_last_error(r.ctx))
+    assert b"this rank's stream failed" in L.izpi_gpu_last_error(r.ctx)
+    assert b"communicator aborted" in L.izpi_gpu_last_error(r.ctx)
+    assert L.izpi_gpu_debug_fault(r.ctx, 0) == 0
+    assert L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st)) == N.IZPI_ERR_INVALID
+    assert L.izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    assert L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st)) == 0
+    torch.cuda.synchronize()
+    ref, _ = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(canvas.cpu().numpy(), ref)
+    r.close()
+
+
+def test_abi1_request_tuning_prefix_is_honoured(gpu):
+    """An ABI-1 request (abi_version 0: the field was padding) has its tuning pointer in the
+    same place, and ABI 1's izpi_render_tuning ended at tail_paths: those fields are read
+    (here a 2000-path cap), the later ones keep their defaults, and the image is the
+    oracle's."""
+    import ctypes as C
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 32, 32, 4)
+    L = N.lib()
+    req = r.request()
+    tu = N.tuning(slots=2000, peer_timeout_ms=1)  # peer_timeout_ms lies past the ABI-1 struct
+    req.tuning = C.pointer(tu)
+    req.abi_version = 0
+    canvas = np.zeros((32, 32, 4))
+    st = N.RenderStats()
+    assert L.izpi_gpu_render(r.ctx, C.byref(req), canvas.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)) == 0
+    assert st.slots == 2000
+    ref, _ = oracle_canvas(scene, 32, 32, 4, N.SAMPLER_COLOUR)
+    assert_parity(canvas, ref)
+    r.close()
+
+
 def test_multi_render_device_failure_is_reported(gpu):
     """izpi_gpu_multi_render with one failing device (a render fault injected on context 1,
     then a context without a scene): the call returns that device's status and names it,

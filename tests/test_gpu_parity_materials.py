@@ -266,3 +266,55 @@ def test_zero_radiance_unwinding_spectral_signs_bitwise(gpu):
     ref, ostats = oracle_canvas(s, 48, 48, 16, N.SAMPLER_SPECTRAL)
     assert_parity(img, ref, r.stats, ostats)
     r.close()
+
+
+def test_normal_map_tbn_kats_device(gpu):
+    """mat3_test.go:10-54 on the device: each KAT's (t, b, n) as a normal-mapped PBR triangle
+    (tests/test_oracle_kats.tbn_kat_scene); izpi_gpu_trace's hit normal (Triangle.Hit with
+    its TBN, triangle.go:250-264) is the oracle's bit for bit and unit(MatrixVectorMul)."""
+    import ctypes as C
+    from oracle import oracle as O
+    from tests.test_oracle_kats import KATS, tbn_kat_scene
+    s, rays = tbn_kat_scene()
+    r8 = np.zeros((len(rays), 8))
+    r8[:, :6], r8[:, 6], r8[:, 7] = rays, 0.001, np.finfo(np.float64).max
+    r = GPURenderer(s, 16, 16, 1)
+    got = (N.Hit * len(r8))()
+    assert N.lib().izpi_gpu_trace(r.ctx, r8.ctypes.data_as(C.POINTER(C.c_double)), len(r8), got) == 0
+    o = O.OracleScene(s)
+    want = o.trace(r8)
+    for i, k in enumerate(KATS["mat3_tbn"]):
+        assert got[i].hit and got[i].prim_ref == want[i].prim_ref
+        assert bytes(got[i])[:72] == bytes(want[i])[:72], (i, list(got[i].normal), list(want[i].normal))
+        w = np.array(k["want"], float)
+        assert list(got[i].normal) == list(w / np.sqrt(np.dot(w, w)))
+    o.close()
+    r.close()
+
+
+
+def test_dielectric_path_length_kat_device(gpu):
+    """dielectric_test.go:47-84 on the device: calculatePathLength's length and clamps
+    (dielectric.go:141-150, the code k_shade runs when a path-length ray returns) for the
+    KAT's hit point and mock exit point (exactly 1.0), the clamps' ends and random pairs,
+    bit for bit against the oracle's Dielectric.calculatePathLength (device op 14)."""
+    import ctypes as C
+    from oracle import oracle as O
+    from tests.test_oracle_kats import KATS
+    k = KATS["path_length"]
+    rng = np.random.default_rng(14)
+    hp = [k["hit_p"], k["hit_p"], k["hit_p"]] + list(rng.uniform(-20, 20, (200, 3)))
+    ex = [k["mock_exit"], [0.5, 0.5, 0.55], [0.5, 0.5, 500.0]] + list(rng.uniform(-80, 80, (200, 3)))
+    hp, ex = np.ascontiguousarray(hp, np.float64), np.ascontiguousarray(ex, np.float64)
+    n = len(hp)
+    r = GPURenderer(configs.cornell_rgb(), 8, 8, 1)
+    out = np.zeros(n)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    assert N.lib().izpi_gpu_gomath(r.ctx, 14, dp(hp), dp(ex), n, dp(out)) == 0
+    r.close()
+    assert out[0] == k["expected"] and out[1] == 0.1 and out[2] == 100.0
+    dirs = np.tile(np.array(k["hit_n"] + k["ray_o"] + k["ray_d"] + k["scattered_d"], np.float64), 1)
+    for i in range(n):
+        a = np.concatenate([hp[i], dirs])
+        want = O.lib().oracle_path_length(O.dptr(a), O.dptr(np.ascontiguousarray(ex[i])))
+        assert out[i].tobytes() == np.float64(want).tobytes(), (i, out[i], want)
