@@ -298,6 +298,13 @@ int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* sam
  * IZPI_ERR_PEER; 0 = off. */
 int izpi_gpu_debug_fault(izpi_ctx* ctx, int where);
 
+/* Measurement hook: re-allocate the render workspace buffers selected by `mask` (bit 0
+ * per-sample results, 1 unwinding records, 2 overflow record blocks, 3 their free rings,
+ * 4 running sums, 5 wavefront state, 6 traversal-stack spill) on other pages: each new
+ * buffer is allocated while the old one is still held, then the old one is freed. The
+ * contents are not kept (every render rewrites them). */
+int izpi_gpu_debug_realloc(izpi_ctx* ctx, uint32_t mask);
+
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);
 

@@ -186,7 +186,11 @@ IZPI_DEV T tld(const T* p) {
 // SPD and the CIE tables. Shading then reads them with LDS reads instead of dependent
 // global loads (the compiler cannot use scalar loads for scene arrays it cannot prove
 // unwritten): the light records alone took C3's shading from 128 to 114 ms.
+#ifdef IZPI_LDS_SMALL  // measurement builds: small staging tables (scenes like C3 only)
+constexpr uint32_t MAT_LDS = 16, TEX_LDS = 16, SPD_LDS = 8, BG_LDS = 8;
+#else
 constexpr uint32_t MAT_LDS = 64, TEX_LDS = 64, SPD_LDS = 384, BG_LDS = 128;
+#endif
 IZPI_DEV izpi_material* mat_lds() {
   __shared__ izpi_material m[MAT_LDS];
   return m;
@@ -294,7 +298,11 @@ IZPI_DEV V3 slot_rgb_k(const DevScene& sc, const TexSlot& s, double u, double v,
 }
 // The materials' texture slots staged in LDS next to their constants (mc_stage): a PBR
 // hit reads its slots with an LDS read instead of a dependent L2 load.
+#ifdef IZPI_LDS_SMALL
+constexpr uint32_t MT_LDS = 16;
+#else
 constexpr uint32_t MT_LDS = 64;
+#endif
 IZPI_DEV MatTex* mt_lds() {
   __shared__ MatTex t[MT_LDS];
   return t;
@@ -1224,7 +1232,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 // the closest hit's GShade, its triangle UVs and tangent frame and a sphere's record are
 // then LDS reads instead of a chain of dependent global loads (entry -> GShade -> UVs ->
 // texels -> tangent frame).
+#ifdef IZPI_LDS_SMALL
+constexpr uint32_t PR_LDS = 2;
+#else
 constexpr uint32_t PR_LDS = 64;
+#endif
 IZPI_DEV GShade* gs_lds() {
   __shared__ GShade g[PR_LDS];
   return g;
@@ -1340,7 +1352,11 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
 // at most LT_LDS lights): the light loop then reads LDS broadcasts instead of one
 // dependent global load per light (the compiler cannot use scalar loads for the GLight
 // records, which it cannot prove unwritten).
+#ifdef IZPI_LDS_SMALL
+constexpr uint32_t LT_LDS = 8;
+#else
 constexpr uint32_t LT_LDS = 64;
+#endif
 IZPI_DEV double* lt_lds() {
   __shared__ double l[LT_LDS * 16];
   return l;
@@ -1543,12 +1559,20 @@ constexpr bool ms_has(int matset, int feature) { return (matset & feature) != 0;
 constexpr bool ms_spec(int matset) { return (matset & (MS_DIEL | MS_METAL | MS_PBR)) != 0; }
 // Record: Colour (flag, att xyz, s, p); Colour + MATSET_CONST (material, s, p); Spectral
 // (flag, att, s, p). p is always last.
+#ifndef IZPI_REC_PAD
+#define IZPI_REC_PAD 0  // measurement builds: 1 pads the 24-B records to 32 B
+#endif
+#ifndef IZPI_SMP_PAD
+#define IZPI_SMP_PAD 0  // measurement builds: 1 pads the 24-B per-sample results to 32 B
+#endif
+constexpr uint32_t SMP_D = IZPI_SMP_PAD ? 4 : 3;  // doubles per per-sample result
 template <int SAMPLER, int MATSET>
 struct RecLayout {
   static constexpr bool COMPACT = SAMPLER == IZPI_SAMPLER_COLOUR && MATSET == MATSET_CONST;
-  static constexpr uint32_t D = COMPACT ? 3 : (SAMPLER == IZPI_SAMPLER_COLOUR ? 5 : 3);  // doubles per record
-  static constexpr uint32_t P = D - 1;                                                   // index of p
-  static constexpr uint32_t S = D - 2;                                                   // index of s
+  static constexpr bool THREE = COMPACT || SAMPLER != IZPI_SAMPLER_COLOUR;             // (material or att, s, p)
+  static constexpr uint32_t D = THREE ? 3 + IZPI_REC_PAD : 5;                          // doubles per record
+  static constexpr uint32_t P = THREE ? 2 : 4;                                         // index of p
+  static constexpr uint32_t S = THREE ? 1 : 3;                                         // index of s
 };
 // Records are (att, s, p): att xyz for Colour, att for Spectral. A specular bounce has no
 // s or p and stores s = REC_SPEC_BITS, a signalling-NaN pattern: ScatteringPDF's
@@ -1650,7 +1674,7 @@ IZPI_DEV double4 mat_const_of(const ShadeParams& sp, uint32_t m) {
 // Result slot of work unit `unit` (= pixel * chunk_spp + sample). Unit-major: paths of
 // neighbouring units finish close in time and fill whole lines (a sample-major layout
 // made k_accumulate coalesced but cost k_shade 16% in scattered partial-line stores).
-IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.out + (size_t)unit * 3; }
+IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.out + (size_t)unit * SMP_D; }
 
 // Write the finished path's radiance after unwinding the recursion of
 // colour.go:44-57 / sampler/spectral.go:60-72 from depth-1 down to 0.
@@ -2563,10 +2587,17 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
   const uint32_t p = blockIdx.x * 256 + threadIdx.x;
   if (p >= ap.num_pixels) return;
   double c0 = ap.running[3 * (size_t)p], c1 = ap.running[3 * (size_t)p + 1], c2 = ap.running[3 * (size_t)p + 2];
-  const double* s = ap.samples + (size_t)p * ap.chunk_spp * 3;
+  const double* s = ap.samples + (size_t)p * ap.chunk_spp * SMP_D;
   uint32_t k = 0;
+  if constexpr (SMP_D == 4) {  // padded results: (x, y), (z, pad) per sample
+    const double2* s2 = reinterpret_cast<const double2*>(s);
+    for (; k < ap.chunk_spp; k++) {
+      const double2 a = s2[2 * k], b = s2[2 * k + 1];
+      c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;
+    }
+  }
 #ifndef IZPI_OLD_ACCUM
-  if ((ap.chunk_spp & 3u) == 0 && blockIdx.x * 256 + 256 <= ap.num_pixels) {
+  if (SMP_D == 3 && (ap.chunk_spp & 3u) == 0 && blockIdx.x * 256 + 256 <= ap.num_pixels) {
     // Staged through LDS, 4 samples (96 B) of each of the wave's 64 pixels at a time: the
     // wave's lanes load the 64 runs as consecutive 16-B pieces (a load instruction covers
     // ~11 neighbouring runs instead of one piece of 64 runs 12 KB apart), then each lane
@@ -3418,7 +3449,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // case (C4 at 256M slots otherwise took 271 GB of the 288). C3 keeps its 256M slots
   // (135 GB); C5 at 128 spp ran 1.4% faster at 64M slots than at 118M (less state, better
   // cache and TLB reach in k_shade), so the smaller budget costs the deep-path scenes nothing.
-  const uint64_t samples_bytes = (uint64_t)num_pixels * chunk * 3 * sizeof(double);
+  const uint64_t samples_bytes = (uint64_t)num_pixels * chunk * SMP_D * sizeof(double);
   const uint64_t budget = avail / 32 * 15;
   if (avail > 0)
     slot_cap = std::min<uint64_t>(slot_cap, std::max<uint64_t>(1024, (budget > samples_bytes ? budget - samples_bytes : 0) /
@@ -3438,7 +3469,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // sizing above counted every one of them as available).
   const auto t_alloc0 = std::chrono::steady_clock::now();
   RenderBuf need[] = {
-      {(void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * 3 * sizeof(double)},
+      {(void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * SMP_D * sizeof(double)},
       {(void**)&ctx->d_recs, &ctx->recs_cap, (size_t)rec_dense * D * slots * sizeof(double)},
       {(void**)&ctx->d_pool, &ctx->pool_cap, rec_pool ? (size_t)pool_blocks * rec_pool * D * sizeof(double) : 0},
       {(void**)&ctx->d_ring, &ctx->ring_cap, rec_pool ? (size_t)pool_blocks * sizeof(uint32_t) : 0},
@@ -4644,6 +4675,24 @@ int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* sam
     uint64_t d = 0, t = 0;
     izpi_gpu_progress(c, &d, &t);
     *samples_done += d; *samples_total += t;
+  }
+  return IZPI_OK;
+}
+
+int izpi_gpu_debug_realloc(izpi_ctx* ctx, uint32_t mask) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  struct { void** p; size_t cap; } bufs[] = {{(void**)&ctx->d_samples, ctx->samples_cap}, {(void**)&ctx->d_recs, ctx->recs_cap},
+                                             {(void**)&ctx->d_pool, ctx->pool_cap}, {(void**)&ctx->d_ring, ctx->ring_cap},
+                                             {(void**)&ctx->d_running, ctx->running_cap}, {(void**)&ctx->d_state, ctx->state_cap},
+                                             {(void**)&ctx->d_spill, ctx->spill_cap}};
+  for (uint32_t k = 0; k < sizeof(bufs) / sizeof(bufs[0]); k++) {
+    if (!(mask >> k & 1u) || !*bufs[k].p || !bufs[k].cap) continue;
+    void* fresh = nullptr;  // allocated while the old buffer is still held: other pages
+    HIP_TRY(hipMalloc(&fresh, bufs[k].cap));
+    HIP_TRY(hipFree(*bufs[k].p));
+    *bufs[k].p = fresh;
   }
   return IZPI_OK;
 }

@@ -127,3 +127,25 @@ def test_go_shim_render_tiles_bitwise(gpu, tmp_path, which):
     assert got.size == want.size
     assert got[known].tobytes() == want[known].tobytes()
     assert np.all(got.reshape(-1, 4)[:, 3] == 1.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_go_shim_reference_bvh_bitwise(gpu, tmp_path, devices):
+    """Options.BVH != BVHGPU: the shim keeps the host's NewBVH4 tree (no SKIP_BVH flag, no
+    GPU build; replay --ref-bvh), and the canvas equals the Python host's on the reference
+    tree and the oracle's own render bit for bit."""
+    text = configs.cornell_rgb_pbtxt(1.0)
+    info, got, izpi = _replay(tmp_path, text, False, devices, ["--ref-bvh"])
+    assert info["ref_bvh"] == 1
+    got = got.reshape(40, 40, 4)
+    s = ingest.ProtoScene.from_file(izpi)
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="reference")
+    want = r.render()
+    r.close()
+    assert got.tobytes() == want.tobytes()
+    o = O.OracleScene(s, aspect_override=1.0)
+    req = N.RenderReq(width=40, height=40, spp=4, max_depth=50, sampler=s.sampler, seed=12345)
+    canvas, _ = o.render(req, threads=8)
+    o.close()
+    assert got.tobytes() == np.asarray(canvas).reshape(40, 40, 4).tobytes()

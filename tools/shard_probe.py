@@ -21,9 +21,13 @@ def main():
     ap.add_argument("--bvh", default="gpu")
     ap.add_argument("--pass-log", action="store_true", help="per-pass trace/shade times and queue lengths on stderr")
     ap.add_argument("--tail-paths", type=int, default=0, help="tuning: k_tail takes over at <= this many paths")
+    ap.add_argument("--variant", default=None, help="a library built by tools/variants.py build NAME")
+    ap.add_argument("--share-slots", default="", help="comma list: tuning slot caps tried for the shares of W > 1 (the W = 1 frame keeps the default)")
     a = ap.parse_args()
     import torch
     from izpi_amd import _native as N
+    if a.variant:
+        N.LIB_PATH = Path(__file__).resolve().parents[1] / "izpi_amd" / "_lib" / "variants" / a.variant / "libizpi_gpu.so"
     from izpi_amd import configs, sharding
     from izpi_amd.renderer import GPURenderer, common_tiles
     cfg = configs.configs()[a.config]
@@ -37,7 +41,14 @@ def main():
                     tuning=N.tuning(**tune) if tune else None)
     all_tiles = common_tiles(cfg.width, cfg.height)
     t1 = None
-    for w in [int(x) for x in a.worlds.split(",")]:
+    base_tuning = r.tuning
+    runs = [(int(x), None) for x in a.worlds.split(",")]
+    if a.share_slots:
+        runs = [(w, sl) for w, _ in runs for sl in ([None] if w == 1 else [None] + [int(v) for v in a.share_slots.split(",")])]
+    for w, sl in runs:
+        r.tuning = base_tuning
+        if sl:
+            r.tuning = N.tuning(**dict(tune, slots=sl))
         worst, times = 0.0, []
         for rank in range(w):
             mine = sharding.shard_tiles(all_tiles, rank, w)
@@ -50,13 +61,13 @@ def main():
             ms = (time.perf_counter() - t) * 1e3
             worst = max(worst, ms)
             times.append(ms)
-            print("W=%d rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f tail %.1f, %d passes)" %
-                  (w, rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["tail_ms"], st["launches"]), flush=True)
+            print("W=%d%s rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f tail %.1f, %d passes)" %
+                  (w, " slots=%d" % sl if sl else "", rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["tail_ms"], st["launches"]), flush=True)
         if t1 is None:
             t1 = worst
         mean = sum(times) / len(times)
-        print("W=%d implied efficiency %.3f (imbalance max/mean %.3f, overhead W*mean/T1 %.3f)" %
-              (w, t1 / (w * worst), worst / mean, w * mean / t1), flush=True)
+        print("W=%d%s implied efficiency %.3f (imbalance max/mean %.3f, overhead W*mean/T1 %.3f)" %
+              (w, " slots=%d" % sl if sl else "", t1 / (w * worst), worst / mean, w * mean / t1), flush=True)
 
 
 if __name__ == "__main__":
