@@ -94,6 +94,18 @@ struct alignas(64) MatTex {
   TexSlot s[4];
 };
 
+// Byte offsets of the tables k_shade / k_tail stage per block (shade_stage) in their dynamic
+// LDS arena, sized per render to what the scene and the request use (a table the render does
+// not stage takes no space). At offset 0: the CIE tables and then the background SPD in
+// Spectral renders (has_cie), the materials' constant colours in Colour renders (places the
+// kernels derive without this struct, izpi_gpu.hip cie_lds / bg_lds / mc_lds); then the
+// materials' texture slots, the lights' records, the material and texture records, the
+// tabulated SPDs (wavelengths, then values), and the primitives' shading records when they
+// are staged too. `bytes` = the arena's size.
+struct LdsLayout {
+  uint32_t mt, lt, lt2, mat, tex, spd, spdv, gs, tt, gp, bytes, has_cie;
+};
+
 struct DevScene {
   const GInner* inner;
   const GLeaf* leaves;
@@ -117,6 +129,7 @@ struct DevScene {
   uint32_t num_inner;           // GInner records
   uint32_t num_prims;           // GPrim records (and GLeaf slots, indexed by first primitive)
   izpi_camera cam;
+  LdsLayout lds;                // per render (render_body), for k_shade / k_tail
 #ifdef IZPI_SHADOW
   // measurement builds only (byte breakdown): copies of the traversal arrays that
   // k_trace2 reads beside the real ones, so a class's bytes past L2 show as extra FETCH_SIZE

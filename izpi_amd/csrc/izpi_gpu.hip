@@ -191,32 +191,31 @@ constexpr uint32_t MAT_LDS = 16, TEX_LDS = 16, SPD_LDS = 8, BG_LDS = 8;
 #else
 constexpr uint32_t MAT_LDS = 64, TEX_LDS = 64, SPD_LDS = 384, BG_LDS = 128;
 #endif
-IZPI_DEV izpi_material* mat_lds() {
-  __shared__ izpi_material m[MAT_LDS];
-  return m;
+// The staged tables live in the block's dynamic LDS arena at the offsets of izd::LdsLayout
+// (DevScene::lds and ShadeParams::lds hold the same layout), sized per render.
+IZPI_DEV char* lds_arena() {
+  extern __shared__ __attribute__((aligned(16))) char izpi_lds_arena[];
+  return izpi_lds_arena;
 }
-IZPI_DEV izpi_texture* tex_lds() {
-  __shared__ izpi_texture t[TEX_LDS];
-  return t;
-}
-IZPI_DEV double* spd_lds() {  // wavelengths [0, SPD_LDS), values [SPD_LDS, 2 SPD_LDS)
-  __shared__ double d[2 * SPD_LDS];
-  return d;
-}
-IZPI_DEV double* bg_lds() {   // the background SPD: wavelengths, then values
-  __shared__ double d[2 * BG_LDS];
-  return d;
-}
-IZPI_DEV double* cie_lds() {  // wavelengths, x, y, z, running sums of y: IZPI_CIE_N each
-  __shared__ double d[5 * IZPI_CIE_N];
-  return d;
-}
+IZPI_DEV izpi_material* mat_lds(const LdsLayout& L) { return (izpi_material*)(lds_arena() + L.mat); }
+IZPI_DEV izpi_texture* tex_lds(const LdsLayout& L) { return (izpi_texture*)(lds_arena() + L.tex); }
+IZPI_DEV double* spd_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.spd); }    // wavelengths
+IZPI_DEV double* spdv_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.spdv); }  // values
+// The CIE tables (wavelengths, x, y, z, running sums of y: IZPI_CIE_N each) at offset 0 and the
+// background SPD (wavelengths, then values) right after them, in Spectral renders; in Colour
+// renders the materials' constant colours (mc_lds) are at offset 0. These places follow from
+// the sampler and the background's length alone, so code that has only the ShadeParams finds
+// them (render_body lays the arena out this way).
+constexpr uint32_t LDS_CIE_BYTES = (5 * IZPI_CIE_N * sizeof(double) + 31) & ~31u;
+IZPI_DEV double* cie_lds() { return (double*)lds_arena(); }
+IZPI_DEV double* bg_lds() { return (double*)(lds_arena() + LDS_CIE_BYTES); }
+IZPI_DEV double* bgv_lds(uint32_t nbg) { return (double*)(lds_arena() + LDS_CIE_BYTES + ((nbg * sizeof(double) + 31) & ~31u)); }
 IZPI_DEV izpi_material mat_rec(const DevScene& sc, bool st, uint32_t m) {
-  if (st) return lds_ld(mat_lds() + m);
+  if (st) return lds_ld(mat_lds(sc.lds) + m);
   return sc.materials[m];
 }
 IZPI_DEV izpi_texture tex_rec(const DevScene& sc, bool st, int32_t id) {
-  if (st) return lds_ld(tex_lds() + id);
+  if (st) return lds_ld(tex_lds(sc.lds) + id);
   return sc.textures[id];
 }
 
@@ -303,13 +302,10 @@ constexpr uint32_t MT_LDS = 16;
 #else
 constexpr uint32_t MT_LDS = 64;
 #endif
-IZPI_DEV MatTex* mt_lds() {
-  __shared__ MatTex t[MT_LDS];
-  return t;
-}
+IZPI_DEV MatTex* mt_lds(const LdsLayout& L) { return (MatTex*)(lds_arena() + L.mt); }
 // Slot k of material m: from LDS when staged (`staged`), else from DevScene::mat_tex.
 IZPI_DEV TexSlot mat_slot(const DevScene& sc, bool staged, uint32_t m, int k) {
-  if (staged) return lds_ld(&mt_lds()[m].s[k]);
+  if (staged) return lds_ld(&mt_lds(sc.lds)[m].s[k]);
   return sc.mat_tex[m].s[k];
 }
 // First interval [wl[i], wl[i+1]] of a NON-DECREASING table that holds w, for
@@ -409,7 +405,7 @@ IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda, doub
   const izpi_texture t = tex_rec(sc, st, id);
   if (t.kind == IZPI_TEX_SPECTRAL_IMAGE) return tex_spectral_image(sc, t, u, v, lambda);
   if (t.kind == IZPI_TEX_SPECTRAL_TABULATED) {
-    if (st) return tab_value<true>(spd_lds() + t.spd_offset, spd_lds() + SPD_LDS + t.spd_offset, t, lambda);
+    if (st) return tab_value<true>(spd_lds(sc.lds) + t.spd_offset, spdv_lds(sc.lds) + t.spd_offset, t, lambda);
     return tab_value<false>(sc.spd_wl + t.spd_offset, sc.spd_val + t.spd_offset, t, lambda);
   }
   double exponent = -gm::pow((lambda - t.center) / t.width_nm, 2);
@@ -1237,20 +1233,11 @@ constexpr uint32_t PR_LDS = 2;
 #else
 constexpr uint32_t PR_LDS = 64;
 #endif
-IZPI_DEV GShade* gs_lds() {
-  __shared__ GShade g[PR_LDS];
-  return g;
-}
-IZPI_DEV GTriTex* tt_lds() {
-  __shared__ GTriTex t[PR_LDS];
-  return t;
-}
-IZPI_DEV GPrim* gp_lds() {
-  __shared__ GPrim p[PR_LDS];
-  return p;
-}
+IZPI_DEV GShade* gs_lds(const LdsLayout& L) { return (GShade*)(lds_arena() + L.gs); }
+IZPI_DEV GTriTex* tt_lds(const LdsLayout& L) { return (GTriTex*)(lds_arena() + L.tt); }
+IZPI_DEV GPrim* gp_lds(const LdsLayout& L) { return (GPrim*)(lds_arena() + L.gp); }
 IZPI_DEV GShade gshade_of(const DevScene& sc, bool pst, int32_t prim) {
-  if (pst) return lds_ld(gs_lds() + prim);
+  if (pst) return lds_ld(gs_lds(sc.lds) + prim);
   return sc.shade[prim];
 }
 // Full hit record of the closest primitive (triangle.go:223-264, sphere.go:71-92).
@@ -1268,7 +1255,7 @@ IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts, bool pst = 
   nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
   V3 tg, bt;
   if (pst) {
-    const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds() + prim);
+    const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds(sc.lds) + prim);
     constexpr uint32_t TG = offsetof(GTriTex, tg) / 8, BT = offsetof(GTriTex, bt) / 8;
     tg = mk(q[TG], q[TG + 1], q[TG + 2]);
     bt = mk(q[BT], q[BT + 1], q[BT + 2]);
@@ -1302,7 +1289,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
       double uv[6];  // u0,v0,u1,v1,u2,v2
       if (pst) {
-        const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds() + c.prim);
+        const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds(sc.lds) + c.prim);
         for (int k = 0; k < 6; k++) uv[k] = q[k];
       } else {
         for (int k = 0; k < 6; k++) uv[k] = sc.tritex[c.prim].uv[k];
@@ -1323,7 +1310,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
   } else {
     double pa[9];
     if (pst) {
-      const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(gp_lds() + c.prim);
+      const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(gp_lds(sc.lds) + c.prim);
       for (int k = 0; k < 9; k++) pa[k] = q[k];
     } else {
       const GPrim& pr = sc.prims[c.prim];
@@ -1357,10 +1344,7 @@ constexpr uint32_t LT_LDS = 8;
 #else
 constexpr uint32_t LT_LDS = 64;
 #endif
-IZPI_DEV double* lt_lds() {
-  __shared__ double l[LT_LDS * 16];
-  return l;
-}
+IZPI_DEV double* lt_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.lt); }
 IZPI_DEV void light_pack(const GLight& L, uint32_t k, double* out) {  // k = 0..15
   double v = 0;
   if (L.kind == IZPI_PRIM_TRIANGLE) {
@@ -1380,7 +1364,7 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
     double r[16];
     if (staged) {
 #pragma unroll
-      for (int k = 0; k < 16; k++) r[k] = lds_ld(lt_lds() + i * 16 + k);
+      for (int k = 0; k < 16; k++) r[k] = lds_ld(lt_lds(sc.lds) + i * 16 + k);
     } else {
 #pragma unroll
       for (int k = 0; k < 16; k++) light_pack(sc.lights[i], k, r);
@@ -1413,18 +1397,15 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
 }
 // What Triangle.Random reads beyond the PDFValue record: v1 and v2 (6 doubles per light,
 // staged next to lt_lds), so a light sample is an LDS read instead of a dependent load.
-IZPI_DEV double* lt2_lds() {
-  __shared__ double l[LT_LDS * 6];
-  return l;
-}
+IZPI_DEV double* lt2_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.lt2); }
 // HitableSlice.Random (hitable_slice.go:107-110) + Triangle/Sphere.Random
 IZPI_DEV V3 lights_random(const DevScene& sc, bool staged, V3 o, Lcg& rng) {
   int64_t index = go_int(rng.next() * (double)sc.num_lights);
 #ifndef IZPI_NO_LRAND_LDS
   if (staged) {
-    const double* r = lt_lds() + index * 16;
+    const double* r = lt_lds(sc.lds) + index * 16;
     if (lds_ld(r + 15) == (double)IZPI_PRIM_TRIANGLE) {
-      const double* q = lt2_lds() + index * 6;
+      const double* q = lt2_lds(sc.lds) + index * 6;
       const V3 v0 = mk(lds_ld(r), lds_ld(r + 1), lds_ld(r + 2));
       const V3 v1 = mk(lds_ld(q), lds_ld(q + 1), lds_ld(q + 2)), v2 = mk(lds_ld(q + 3), lds_ld(q + 4), lds_ld(q + 5));
       double t1 = rng.next();
@@ -1588,6 +1569,9 @@ IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t rslot, uint32_t blk, ui
 template <int SAMPLER, int MATSET>
 IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth, bool spec, V3 att, double s,
                         uint32_t mat) {
+#ifdef IZPI_EXP_NOREC  // timing only (wrong images): the first levels' records are not stored
+  if (depth < IZPI_EXP_NOREC) return;
+#endif
   double* rp = rec_ptr<SAMPLER, MATSET>(sp, rslot, blk, depth);
   if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {  // never specular
     sst(rp, (double)mat);
@@ -1622,47 +1606,48 @@ IZPI_DEV void rec_zero_track(uint32_t& zf, bool spec, V3 att, double s, double p
 // records' unwinding (finish) and constant-albedo hits read them with an LDS read instead
 // of a dependent L2 load.
 constexpr uint32_t MC_LDS = MT_LDS;
-IZPI_DEV double4* mc_lds() {
-  __shared__ double4 c[MC_LDS];
-  return c;
-}
+IZPI_DEV double4* mc_lds() { return (double4*)lds_arena(); }  // Colour renders: at offset 0
 // Copy the scene's small tables into this block's LDS (ShadeParams::staged): the
 // materials' constant colours and texture slots, the lights' PDFValue records, the
 // material and texture records, the tabulated SPDs, the background SPD, the CIE tables.
 IZPI_DEV void shade_stage(const DevScene& sc, const ShadeParams& sp) {
+  const LdsLayout& Ly = sc.lds;
   if (sp.staged) {
     const uint32_t t0 = threadIdx.x, nt = blockDim.x;
-    for (uint32_t t = t0; t < sp.num_mc; t += nt) mc_lds()[t] = sp.mat_const[t];
-    for (uint32_t t = t0; t < 4 * sp.num_mc; t += nt) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
-    for (uint32_t t = t0; t < 16 * sc.num_lights; t += nt) light_pack(sc.lights[t >> 4], t & 15, lt_lds() + (t & ~15u));
+    if (!Ly.has_cie)  // Colour renders (the only ones that read them)
+      for (uint32_t t = t0; t < sp.num_mc; t += nt) mc_lds()[t] = sp.mat_const[t];
+    for (uint32_t t = t0; t < 4 * sp.num_mc; t += nt) mt_lds(Ly)[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
+    for (uint32_t t = t0; t < 16 * sc.num_lights; t += nt) light_pack(sc.lights[t >> 4], t & 15, lt_lds(Ly) + (t & ~15u));
     for (uint32_t t = t0; t < 6 * sc.num_lights; t += nt) {
       const GLight& L = sc.lights[t / 6];
       const uint32_t k = t % 6;
-      lt2_lds()[t] = L.kind == IZPI_PRIM_TRIANGLE ? (k < 3 ? L.v1[k] : L.v2[k - 3]) : 0.0;
+      lt2_lds(Ly)[t] = L.kind == IZPI_PRIM_TRIANGLE ? (k < 3 ? L.v1[k] : L.v2[k - 3]) : 0.0;
     }
     constexpr uint32_t MW = sizeof(izpi_material) / 8, TW = sizeof(izpi_texture) / 8;
     for (uint32_t t = t0; t < MW * sp.num_mc; t += nt)
-      reinterpret_cast<uint64_t*>(mat_lds())[t] = reinterpret_cast<const uint64_t*>(sc.materials)[t];
+      reinterpret_cast<uint64_t*>(mat_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.materials)[t];
     for (uint32_t t = t0; t < TW * sp.num_tex; t += nt)
-      reinterpret_cast<uint64_t*>(tex_lds())[t] = reinterpret_cast<const uint64_t*>(sc.textures)[t];
-    for (uint32_t t = t0; t < sp.num_spd; t += nt) { spd_lds()[t] = sc.spd_wl[t]; spd_lds()[SPD_LDS + t] = sc.spd_val[t]; }
-    for (uint32_t t = t0; t < sp.num_bg_spd; t += nt) { bg_lds()[t] = sp.bg_wl[t]; bg_lds()[BG_LDS + t] = sp.bg_val[t]; }
-    for (uint32_t t = t0; t < IZPI_CIE_N; t += nt) {
-      double* c = cie_lds();
-      c[t] = c_cie_wl[t]; c[IZPI_CIE_N + t] = c_cie_x[t]; c[2 * IZPI_CIE_N + t] = c_cie_y[t];
-      c[3 * IZPI_CIE_N + t] = c_cie_z[t]; c[4 * IZPI_CIE_N + t] = c_cie_ycum.v[t];
+      reinterpret_cast<uint64_t*>(tex_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.textures)[t];
+    for (uint32_t t = t0; t < sp.num_spd; t += nt) { spd_lds(Ly)[t] = sc.spd_wl[t]; spdv_lds(Ly)[t] = sc.spd_val[t]; }
+    if (Ly.has_cie) {
+      for (uint32_t t = t0; t < sp.num_bg_spd; t += nt) { bg_lds()[t] = sp.bg_wl[t]; bgv_lds(sp.num_bg_spd)[t] = sp.bg_val[t]; }
+      for (uint32_t t = t0; t < IZPI_CIE_N; t += nt) {
+        double* c = cie_lds();
+        c[t] = c_cie_wl[t]; c[IZPI_CIE_N + t] = c_cie_x[t]; c[2 * IZPI_CIE_N + t] = c_cie_y[t];
+        c[3 * IZPI_CIE_N + t] = c_cie_z[t]; c[4 * IZPI_CIE_N + t] = c_cie_ycum.v[t];
+      }
     }
   }
   if (sp.prims_staged) {
     const uint32_t t0 = threadIdx.x, nt = blockDim.x, np = sc.num_prims;
     constexpr uint32_t SW = sizeof(GShade) / 8, TW = sizeof(GTriTex) / 8, PW = sizeof(GPrim) / 8;
     for (uint32_t t = t0; t < SW * np; t += nt)
-      reinterpret_cast<uint64_t*>(gs_lds())[t] = reinterpret_cast<const uint64_t*>(sc.shade)[t];
+      reinterpret_cast<uint64_t*>(gs_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.shade)[t];
     if (sc.tritex)
       for (uint32_t t = t0; t < TW * np; t += nt)
-        reinterpret_cast<uint64_t*>(tt_lds())[t] = reinterpret_cast<const uint64_t*>(sc.tritex)[t];
+        reinterpret_cast<uint64_t*>(tt_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.tritex)[t];
     for (uint32_t t = t0; t < PW * np; t += nt)
-      reinterpret_cast<uint64_t*>(gp_lds())[t] = reinterpret_cast<const uint64_t*>(sc.prims)[t];
+      reinterpret_cast<uint64_t*>(gp_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.prims)[t];
   }
   __syncthreads();
 }
@@ -1718,6 +1703,9 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
       for (int j = 0; j < RB; j++) {
         if (dd - j >= 0) {
           const double* r = rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j));
+#ifdef IZPI_EXP_NOREC
+          if (dd - j < IZPI_EXP_NOREC) { rv[j][0] = 0.0; rv[j][1] = 1.0; rv[j][2] = 1.0; continue; }
+#endif
           rv[j][0] = sld(r); rv[j][1] = sld(r + 1); rv[j][2] = sld(r + 2);
         }
       }
@@ -1797,7 +1785,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
 
 // The background SPD at lambda (sampler/spectral.go:48-51,79), staged or not
 IZPI_DEV double bg_value(const ShadeParams& sp, double lambda) {
-  if (sp.staged) return spd_value<true>(bg_lds(), bg_lds() + BG_LDS, sp.num_bg_spd, lambda, sp.bg_sorted != 0);
+  if (sp.staged) return spd_value<true>(bg_lds(), bgv_lds(sp.num_bg_spd), sp.num_bg_spd, lambda, sp.bg_sorted != 0);
   return spd_value<false>(sp.bg_wl, sp.bg_val, sp.num_bg_spd, lambda, sp.bg_sorted != 0);
 }
 IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colour) {
@@ -2318,6 +2306,9 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         SCLK_T(sc3);
         const double pdf_val = 0.5 * lights_pdf(sc, st, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         SCLK_ADD(SCLK_LPDF, sc3);
+#ifdef IZPI_EXP_NOREC
+        if (P.depth >= IZPI_EXP_NOREC)
+#endif
         sst(rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth) + RecLayout<SAMPLER, MATSET>::P, pdf_val);
         if constexpr (ms_spec(MATSET) || SAMPLER == IZPI_SAMPLER_SPECTRAL) rec_zero_track<SAMPLER>(P.zf, false, att, spdf, pdf_val);
         next_d = dir;
@@ -3058,9 +3049,10 @@ void free_scene(izpi_ctx* ctx) {
 }
 
 template <typename K>
-int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks, int threads = 256) {
+int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks, int threads = 256, size_t dyn_lds = 0) {
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0));
+  if (dyn_lds) HIP_TRY(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, dyn_lds));
   if (per_cu < 1) per_cu = 1;
   *blocks = per_cu * ctx->num_cus;
   return IZPI_OK;
@@ -3177,13 +3169,14 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   hipStream_t st = ctx->stream;
   const izpi_render_tuning& tu = tuning_of(req);
   int shade_res = 0;
-  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res, (int)SHADE_THREADS);
+  const size_t dyn = sc.lds.bytes;  // the staged tables' LDS arena (render_body)
+  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res, (int)SHADE_THREADS, dyn);
   if (rc) return rc;
   // tail kernel: used once every unit has started and at most `tail_max` paths remain
   const bool tail_deep = ctx->stack_needed > 32;
   int tail_res = 0;
-  if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res)
-                      : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res))) return rc;
+  if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res, 256, dyn)
+                      : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res, 256, dyn))) return rc;
   if ((uint32_t)std::max({tr.blocks * 4, shade_res * (int)SHADE_WAVES, tail_res * 4}) > ctx->num_cus * CPART_BLOCKS_PER_CU * 4) {
     ctx->err = "grid larger than the counter rows";
     return IZPI_ERR_INVALID;
@@ -3236,7 +3229,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         launch_trace(ctx, sc, tr, wp, st, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
-        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(SHADE_THREADS), 0, st, sc, sp, wp);
+        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(SHADE_THREADS), dyn, st, sc, sp, wp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
@@ -3267,8 +3260,8 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
         // (the deep instance spills stack entries past 32 into k_trace2's spill area, which
         // holds 64 entries for each of k_trace2's threads, more than k_tail has)
-        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp, ctx->d_spill);
-        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), 0, st, sc, sp, wp, ctx->d_spill);
+        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), dyn, st, sc, sp, wp, ctx->d_spill);
+        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), dyn, st, sc, sp, wp, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev3, st));
         HIP_TRY(hipEventSynchronize(ctx->ev3));
@@ -3522,6 +3515,38 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.staged = 0;  // A/B builds
   sp.prims_staged = 0;
 #endif
+  {  // the per-block LDS arena of k_shade / k_tail (izd::LdsLayout): only the tables this render stages
+    LdsLayout L{};
+    uint32_t off = 0;
+    auto take = [&](uint64_t bytes) {
+      const uint32_t o = off;
+      off += (uint32_t)((bytes + 31) & ~(uint64_t)31);
+      return o;
+    };
+    if (sp.staged) {
+      const uint64_t nm = ctx->num_materials, nl = sc.num_lights;
+      if (req->sampler == IZPI_SAMPLER_SPECTRAL) {  // CIE tables at 0, the background right after (bg_lds)
+        L.has_cie = 1;
+        take(LDS_CIE_BYTES);
+        take(nbg * sizeof(double));
+        take(nbg * sizeof(double));
+      } else {
+        take(nm * sizeof(double4));  // the materials' constant colours at 0 (mc_lds)
+      }
+      L.mt = take(nm * sizeof(MatTex));
+      L.lt = take(nl * 16 * sizeof(double)); L.lt2 = take(nl * 6 * sizeof(double));
+      L.mat = take(nm * sizeof(izpi_material)); L.tex = take((uint64_t)ctx->num_textures * sizeof(izpi_texture));
+      L.spd = take((uint64_t)ctx->num_spd * sizeof(double)); L.spdv = take((uint64_t)ctx->num_spd * sizeof(double));
+    }
+    if (sp.prims_staged) {
+      const uint64_t np = sc.num_prims;
+      L.gs = take(np * sizeof(GShade));
+      L.tt = sc.tritex ? take(np * sizeof(GTriTex)) : 0;
+      L.gp = take(np * sizeof(GPrim));
+    }
+    L.bytes = off;
+    sc.lds = L;
+  }
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = misc(ctx, 1);

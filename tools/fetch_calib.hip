@@ -91,9 +91,11 @@ int main() {
   CK(hipDeviceSynchronize());
   int launch = 0;
   auto flush_all = [&]() { hipLaunchKernelGGL(k_touch, dim3(4096), dim3(256), 0, 0, flush, big / 16); launch++; };
-  auto report = [&](const char* name, const char* table, double bytes, double lines) {
-    printf("{\"launch\": %d, \"kernel\": \"%s\", \"table\": \"%s\", \"useful_bytes\": %.0f, \"line_bytes\": %.0f}\n", launch,
-           name, table, bytes, lines * 128);
+  // insts: the wave-level vector-memory load instructions the kernel issues (every lane
+  // active; to check which SQ counter counts global_load issue on gfx950)
+  auto report = [&](const char* name, const char* table, double bytes, double lines, double insts) {
+    printf("{\"launch\": %d, \"kernel\": \"%s\", \"table\": \"%s\", \"useful_bytes\": %.0f, \"line_bytes\": %.0f, "
+           "\"load_insts\": %.0f}\n", launch, name, table, bytes, lines * 128, insts);
     launch++;
   };
   for (int pass = 0; pass < 2; pass++) {  // pass 0: cold 2 GiB table, pass 1: 64 MiB table read once before
@@ -105,11 +107,11 @@ int main() {
     // stream
     if (pass == 0) flush_all(); else { hipLaunchKernelGGL(k_stream, dim3(4096), dim3(256), 0, 0, a, tb / 16, out); launch++; }
     hipLaunchKernelGGL(k_stream, dim3(4096), dim3(256), 0, 0, a, tb / 16, out);
-    report("stream", tn, (double)tb, (double)tb / 128);
+    report("stream", tn, (double)tb, (double)tb / 128, (double)(tb / 16) / 64);
     // node lines
     if (pass == 0) flush_all(); else { hipLaunchKernelGGL(k_node, dim3(grid), dim3(256), 0, 0, a, lines - 1, nt, out); launch++; }
     hipLaunchKernelGGL(k_node, dim3(grid), dim3(256), 0, 0, a, lines - 1, nt, out);
-    report("node128", tn, (double)nt * 128, (double)nt);
+    report("node128", tn, (double)nt * 128, (double)nt, 8.0 * (double)((nt + 63) / 64));
     // 80-B records: a power-of-two count of them inside the table
     uint64_t recs = 1;
     while (recs * 2 * 80 <= tb) recs *= 2;
@@ -121,16 +123,16 @@ int main() {
       const uint64_t r = (t * 0x9E3779B97F4A7C15ull) & (recs - 1);
       l80 += (double)((80 * r + 79) / 128 - (80 * r) / 128 + 1);
     }
-    report("tri80", tn, (double)nr * 80, l80);
+    report("tri80", tn, (double)nr * 80, l80, 5.0 * (double)((nr + 63) / 64));
     // 48-B consecutive records
     const uint64_t n48 = tb / 48 / 2, g48 = (n48 + 255) / 256;
     if (pass == 0) flush_all(); else { hipLaunchKernelGGL(k_rec48, dim3(g48), dim3(256), 0, 0, a, n48, out); launch++; }
     hipLaunchKernelGGL(k_rec48, dim3(g48), dim3(256), 0, 0, a, n48, out);
-    report("rec48", tn, (double)n48 * 48, (double)n48 * 48 / 128);
+    report("rec48", tn, (double)n48 * 48, (double)n48 * 48 / 128, 3.0 * (double)((n48 + 63) / 64));
     // 32 B of a random line
     if (pass == 0) flush_all(); else { hipLaunchKernelGGL(k_half32, dim3(grid), dim3(256), 0, 0, a, lines - 1, nt, out); launch++; }
     hipLaunchKernelGGL(k_half32, dim3(grid), dim3(256), 0, 0, a, lines - 1, nt, out);
-    report("half32", tn, (double)nt * 32, (double)nt);
+    report("half32", tn, (double)nt * 32, (double)nt, 2.0 * (double)((nt + 63) / 64));
   }
   CK(hipDeviceSynchronize());
   CK(hipFree(a));

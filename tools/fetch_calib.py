@@ -17,7 +17,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 EXE = ROOT / "izpi_amd" / "_lib" / "fetch_calib"
-PASSES = [["FETCH_SIZE"], ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"], ["TCC_HIT_sum", "TCC_MISS_sum"]]
+PASSES = [["FETCH_SIZE"], ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"], ["TCC_HIT_sum", "TCC_MISS_sum"],
+          # which SQ counter counts global_load issue on gfx950 (SQ_ACTIVE_INST_VMEM read 0.0 in r4's bench)
+          ["SQ_INSTS_VMEM", "SQ_INSTS_FLAT", "SQ_INSTS_VMEM_RD", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_FLAT", "SQ_WAVE_CYCLES"]]
 
 
 def main():
@@ -52,6 +54,9 @@ def main():
         if "FETCH_SIZE" in row:
             row["fetch_bytes"] = row["FETCH_SIZE"] * 1024
             row["fetch_over_lines"] = round(row["fetch_bytes"] / row["line_bytes"], 4)
+        for c in ("SQ_INSTS_VMEM", "SQ_INSTS_FLAT", "SQ_INSTS_VMEM_RD"):
+            if c in row and row.get("load_insts"):
+                row[c + "_over_loads"] = round(row[c] / row["load_insts"], 4)
         if "TCC_EA0_RDREQ_sum" in row:
             rq, r32 = row["TCC_EA0_RDREQ_sum"], row.get("TCC_EA0_RDREQ_32B_sum", 0.0)
             row["rdreq_per_line"] = round(rq / (row["line_bytes"] / 128), 4)
