@@ -55,7 +55,10 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md, L2 (per XCD): 34.5 TB/s aggregate 
 MALL_GATHER_GBS = 7650.0
 PMC_PASSES = {"fetch": ["FETCH_SIZE"], "write": ["WRITE_SIZE"], "tcc": ["TCC_HIT_sum", "TCC_MISS_sum"],
               "sq": ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
-                     "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_ANY"]}
+                     "SQ_ACTIVE_INST_FLAT", "SQ_WAIT_INST_ANY"]}
+# global loads / stores are FLAT-encoded on gfx950: SQ_ACTIVE_INST_VMEM reads 0 for them and
+# SQ_ACTIVE_INST_FLAT equals SQ_INSTS_FLAT (one issue cycle per instruction), calibrated on
+# known kernels in profiles/r5b/fetch_calib_sq.jsonl (tools/fetch_calib.py)
 KERNELS = {"k_trace2": "k_trace2<", "k_shade": "k_shade<"}
 
 
@@ -196,7 +199,7 @@ def traffic_summary(pmc):
             out[short]["wave_cycles"] = {
                 "waiting": e.get("SQ_WAIT_ANY", 0.0) / wc, "issuing_any": e.get("SQ_ACTIVE_INST_ANY", 0.0) / wc,
                 "issuing_valu": e.get("SQ_ACTIVE_INST_VALU", 0.0) / wc,
-                "issuing_vmem": e.get("SQ_ACTIVE_INST_VMEM", 0.0) / wc,
+                "issuing_flat": e.get("SQ_ACTIVE_INST_FLAT", 0.0) / wc,
                 "waiting_to_issue": e.get("SQ_WAIT_INST_ANY", 0.0) / wc}
     return out
 

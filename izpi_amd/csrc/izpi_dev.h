@@ -102,9 +102,6 @@ struct alignas(64) MatTex {
 // materials' texture slots, the lights' records, the material and texture records, the
 // tabulated SPDs (wavelengths, then values), and the primitives' shading records when they
 // are staged too. `bytes` = the arena's size.
-struct LdsLayout {
-  uint32_t mt, lt, lt2, mat, tex, spd, spdv, gs, tt, gp, bytes, has_cie;
-};
 
 struct DevScene {
   const GInner* inner;
@@ -129,7 +126,7 @@ struct DevScene {
   uint32_t num_inner;           // GInner records
   uint32_t num_prims;           // GPrim records (and GLeaf slots, indexed by first primitive)
   izpi_camera cam;
-  LdsLayout lds;                // per render (render_body), for k_shade / k_tail
+  uint32_t lds_bytes;           // per render (render_body): k_shade / k_tail's dynamic LDS arena (lds_off)
 #ifdef IZPI_SHADOW
   // measurement builds only (byte breakdown): copies of the traversal arrays that
   // k_trace2 reads beside the real ones, so a class's bytes past L2 show as extra FETCH_SIZE

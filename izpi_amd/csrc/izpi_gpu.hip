@@ -187,35 +187,53 @@ IZPI_DEV T tld(const T* p) {
 // global loads (the compiler cannot use scalar loads for scene arrays it cannot prove
 // unwritten): the light records alone took C3's shading from 128 to 114 ms.
 #ifdef IZPI_LDS_SMALL  // measurement builds: small staging tables (scenes like C3 only)
-constexpr uint32_t MAT_LDS = 16, TEX_LDS = 16, SPD_LDS = 8, BG_LDS = 8;
+constexpr uint32_t MAT_LDS = 16, TEX_LDS = 16, SPD_LDS = 8, BG_LDS = 8, MT_LDS = 16, LT_LDS = 8, PR_LDS = 2;
 #else
-constexpr uint32_t MAT_LDS = 64, TEX_LDS = 64, SPD_LDS = 384, BG_LDS = 128;
+constexpr uint32_t MAT_LDS = 64, TEX_LDS = 64, SPD_LDS = 384, BG_LDS = 128, MT_LDS = 64, LT_LDS = 64, PR_LDS = 64;
 #endif
-// The staged tables live in the block's dynamic LDS arena at the offsets of izd::LdsLayout
-// (DevScene::lds and ShadeParams::lds hold the same layout), sized per render.
+// The staged tables live at fixed offsets of the block's dynamic LDS arena, ordered so that
+// what a render stages is a prefix of it: the Colour tables, then the Spectral ones, then
+// the primitives. render_body sizes the arena to that prefix (lds_arena_bytes), so a render
+// that stages little leaves k_tail (whose traversal stacks are LDS too) more blocks per CU.
+// The offsets are compile-time: per-render offsets cost k_shade registers (the Spectral
+// instances spilled 8 more VGPRs, C5's shading +2.5%; profiles/r5a/ab_arena_c5.jsonl).
+namespace lds_off {
+constexpr uint32_t al(uint64_t b) { return (uint32_t)((b + 31) & ~31ull); }
+constexpr uint32_t MC = 0;                                        // double4 [MT_LDS]: constant colours
+constexpr uint32_t MT = MC + al(MT_LDS * sizeof(double4));        // MatTex [MT_LDS]
+constexpr uint32_t LT = MT + al(MT_LDS * sizeof(MatTex));         // double [LT_LDS][16]: light records
+constexpr uint32_t LT2 = LT + al(LT_LDS * 16 * sizeof(double));   // double [LT_LDS][6]
+constexpr uint32_t MAT = LT2 + al(LT_LDS * 6 * sizeof(double));   // izpi_material [MAT_LDS]
+constexpr uint32_t TEX = MAT + al(MAT_LDS * sizeof(izpi_material));
+constexpr uint32_t COLOUR_END = TEX + al(TEX_LDS * sizeof(izpi_texture));
+constexpr uint32_t SPD = COLOUR_END;                              // tabulated SPDs: wavelengths
+constexpr uint32_t SPDV = SPD + al(SPD_LDS * sizeof(double));     // values
+constexpr uint32_t CIE = SPDV + al(SPD_LDS * sizeof(double));     // 5 x IZPI_CIE_N: wl, x, y, z, running y
+constexpr uint32_t BG = CIE + al(5 * IZPI_CIE_N * sizeof(double));  // the background SPD: wavelengths
+constexpr uint32_t BGV = BG + al(BG_LDS * sizeof(double));        // values
+constexpr uint32_t SPECTRAL_END = BGV + al(BG_LDS * sizeof(double));
+constexpr uint32_t GS = SPECTRAL_END;                             // GShade [PR_LDS]
+constexpr uint32_t TT = GS + al(PR_LDS * sizeof(GShade));         // GTriTex [PR_LDS]
+constexpr uint32_t GP = TT + al(PR_LDS * sizeof(GTriTex));        // GPrim [PR_LDS]
+constexpr uint32_t END = GP + al(PR_LDS * sizeof(GPrim));
+}  // namespace lds_off
 IZPI_DEV char* lds_arena() {
   extern __shared__ __attribute__((aligned(16))) char izpi_lds_arena[];
   return izpi_lds_arena;
 }
-IZPI_DEV izpi_material* mat_lds(const LdsLayout& L) { return (izpi_material*)(lds_arena() + L.mat); }
-IZPI_DEV izpi_texture* tex_lds(const LdsLayout& L) { return (izpi_texture*)(lds_arena() + L.tex); }
-IZPI_DEV double* spd_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.spd); }    // wavelengths
-IZPI_DEV double* spdv_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.spdv); }  // values
-// The CIE tables (wavelengths, x, y, z, running sums of y: IZPI_CIE_N each) at offset 0 and the
-// background SPD (wavelengths, then values) right after them, in Spectral renders; in Colour
-// renders the materials' constant colours (mc_lds) are at offset 0. These places follow from
-// the sampler and the background's length alone, so code that has only the ShadeParams finds
-// them (render_body lays the arena out this way).
-constexpr uint32_t LDS_CIE_BYTES = (5 * IZPI_CIE_N * sizeof(double) + 31) & ~31u;
-IZPI_DEV double* cie_lds() { return (double*)lds_arena(); }
-IZPI_DEV double* bg_lds() { return (double*)(lds_arena() + LDS_CIE_BYTES); }
-IZPI_DEV double* bgv_lds(uint32_t nbg) { return (double*)(lds_arena() + LDS_CIE_BYTES + ((nbg * sizeof(double) + 31) & ~31u)); }
+IZPI_DEV izpi_material* mat_lds() { return (izpi_material*)(lds_arena() + lds_off::MAT); }
+IZPI_DEV izpi_texture* tex_lds() { return (izpi_texture*)(lds_arena() + lds_off::TEX); }
+IZPI_DEV double* spd_lds() { return (double*)(lds_arena() + lds_off::SPD); }
+IZPI_DEV double* spdv_lds() { return (double*)(lds_arena() + lds_off::SPDV); }
+IZPI_DEV double* cie_lds() { return (double*)(lds_arena() + lds_off::CIE); }
+IZPI_DEV double* bg_lds() { return (double*)(lds_arena() + lds_off::BG); }
+IZPI_DEV double* bgv_lds() { return (double*)(lds_arena() + lds_off::BGV); }
 IZPI_DEV izpi_material mat_rec(const DevScene& sc, bool st, uint32_t m) {
-  if (st) return lds_ld(mat_lds(sc.lds) + m);
+  if (st) return lds_ld(mat_lds() + m);
   return sc.materials[m];
 }
 IZPI_DEV izpi_texture tex_rec(const DevScene& sc, bool st, int32_t id) {
-  if (st) return lds_ld(tex_lds(sc.lds) + id);
+  if (st) return lds_ld(tex_lds() + id);
   return sc.textures[id];
 }
 
@@ -297,15 +315,10 @@ IZPI_DEV V3 slot_rgb_k(const DevScene& sc, const TexSlot& s, double u, double v,
 }
 // The materials' texture slots staged in LDS next to their constants (mc_stage): a PBR
 // hit reads its slots with an LDS read instead of a dependent L2 load.
-#ifdef IZPI_LDS_SMALL
-constexpr uint32_t MT_LDS = 16;
-#else
-constexpr uint32_t MT_LDS = 64;
-#endif
-IZPI_DEV MatTex* mt_lds(const LdsLayout& L) { return (MatTex*)(lds_arena() + L.mt); }
+IZPI_DEV MatTex* mt_lds() { return (MatTex*)(lds_arena() + lds_off::MT); }
 // Slot k of material m: from LDS when staged (`staged`), else from DevScene::mat_tex.
 IZPI_DEV TexSlot mat_slot(const DevScene& sc, bool staged, uint32_t m, int k) {
-  if (staged) return lds_ld(&mt_lds(sc.lds)[m].s[k]);
+  if (staged) return lds_ld(&mt_lds()[m].s[k]);
   return sc.mat_tex[m].s[k];
 }
 // First interval [wl[i], wl[i+1]] of a NON-DECREASING table that holds w, for
@@ -405,7 +418,7 @@ IZPI_DEV double tex_spectral(const DevScene& sc, int32_t id, double lambda, doub
   const izpi_texture t = tex_rec(sc, st, id);
   if (t.kind == IZPI_TEX_SPECTRAL_IMAGE) return tex_spectral_image(sc, t, u, v, lambda);
   if (t.kind == IZPI_TEX_SPECTRAL_TABULATED) {
-    if (st) return tab_value<true>(spd_lds(sc.lds) + t.spd_offset, spdv_lds(sc.lds) + t.spd_offset, t, lambda);
+    if (st) return tab_value<true>(spd_lds() + t.spd_offset, spdv_lds() + t.spd_offset, t, lambda);
     return tab_value<false>(sc.spd_wl + t.spd_offset, sc.spd_val + t.spd_offset, t, lambda);
   }
   double exponent = -gm::pow((lambda - t.center) / t.width_nm, 2);
@@ -1228,16 +1241,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 // the closest hit's GShade, its triangle UVs and tangent frame and a sphere's record are
 // then LDS reads instead of a chain of dependent global loads (entry -> GShade -> UVs ->
 // texels -> tangent frame).
-#ifdef IZPI_LDS_SMALL
-constexpr uint32_t PR_LDS = 2;
-#else
-constexpr uint32_t PR_LDS = 64;
-#endif
-IZPI_DEV GShade* gs_lds(const LdsLayout& L) { return (GShade*)(lds_arena() + L.gs); }
-IZPI_DEV GTriTex* tt_lds(const LdsLayout& L) { return (GTriTex*)(lds_arena() + L.tt); }
-IZPI_DEV GPrim* gp_lds(const LdsLayout& L) { return (GPrim*)(lds_arena() + L.gp); }
+IZPI_DEV GShade* gs_lds() { return (GShade*)(lds_arena() + lds_off::GS); }
+IZPI_DEV GTriTex* tt_lds() { return (GTriTex*)(lds_arena() + lds_off::TT); }
+IZPI_DEV GPrim* gp_lds() { return (GPrim*)(lds_arena() + lds_off::GP); }
 IZPI_DEV GShade gshade_of(const DevScene& sc, bool pst, int32_t prim) {
-  if (pst) return lds_ld(gs_lds(sc.lds) + prim);
+  if (pst) return lds_ld(gs_lds() + prim);
   return sc.shade[prim];
 }
 // Full hit record of the closest primitive (triangle.go:223-264, sphere.go:71-92).
@@ -1255,7 +1263,7 @@ IZPI_DEV V3 nmap_tbn(const DevScene& sc, int32_t prim, V3 n, V3 nts, bool pst = 
   nts.x = 2 * nts.x - 1.0; nts.y = 2 * nts.y - 1.0; nts.z = 2 * nts.z - 1.0;
   V3 tg, bt;
   if (pst) {
-    const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds(sc.lds) + prim);
+    const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds() + prim);
     constexpr uint32_t TG = offsetof(GTriTex, tg) / 8, BT = offsetof(GTriTex, bt) / 8;
     tg = mk(q[TG], q[TG + 1], q[TG + 2]);
     bt = mk(q[BT], q[BT + 1], q[BT + 2]);
@@ -1289,7 +1297,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
       if (gm::abs(sum - 1.0) > eps) { u /= sum; v /= sum; w /= sum; }
       double uv[6];  // u0,v0,u1,v1,u2,v2
       if (pst) {
-        const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds(sc.lds) + c.prim);
+        const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(tt_lds() + c.prim);
         for (int k = 0; k < 6; k++) uv[k] = q[k];
       } else {
         for (int k = 0; k < 6; k++) uv[k] = sc.tritex[c.prim].uv[k];
@@ -1310,7 +1318,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
   } else {
     double pa[9];
     if (pst) {
-      const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(gp_lds(sc.lds) + c.prim);
+      const __attribute__((address_space(3))) double* q = (const __attribute__((address_space(3))) double*)(gp_lds() + c.prim);
       for (int k = 0; k < 9; k++) pa[k] = q[k];
     } else {
       const GPrim& pr = sc.prims[c.prim];
@@ -1339,12 +1347,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
 // at most LT_LDS lights): the light loop then reads LDS broadcasts instead of one
 // dependent global load per light (the compiler cannot use scalar loads for the GLight
 // records, which it cannot prove unwritten).
-#ifdef IZPI_LDS_SMALL
-constexpr uint32_t LT_LDS = 8;
-#else
-constexpr uint32_t LT_LDS = 64;
-#endif
-IZPI_DEV double* lt_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.lt); }
+IZPI_DEV double* lt_lds() { return (double*)(lds_arena() + lds_off::LT); }
 IZPI_DEV void light_pack(const GLight& L, uint32_t k, double* out) {  // k = 0..15
   double v = 0;
   if (L.kind == IZPI_PRIM_TRIANGLE) {
@@ -1364,7 +1367,7 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
     double r[16];
     if (staged) {
 #pragma unroll
-      for (int k = 0; k < 16; k++) r[k] = lds_ld(lt_lds(sc.lds) + i * 16 + k);
+      for (int k = 0; k < 16; k++) r[k] = lds_ld(lt_lds() + i * 16 + k);
     } else {
 #pragma unroll
       for (int k = 0; k < 16; k++) light_pack(sc.lights[i], k, r);
@@ -1397,15 +1400,15 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
 }
 // What Triangle.Random reads beyond the PDFValue record: v1 and v2 (6 doubles per light,
 // staged next to lt_lds), so a light sample is an LDS read instead of a dependent load.
-IZPI_DEV double* lt2_lds(const LdsLayout& L) { return (double*)(lds_arena() + L.lt2); }
+IZPI_DEV double* lt2_lds() { return (double*)(lds_arena() + lds_off::LT2); }
 // HitableSlice.Random (hitable_slice.go:107-110) + Triangle/Sphere.Random
 IZPI_DEV V3 lights_random(const DevScene& sc, bool staged, V3 o, Lcg& rng) {
   int64_t index = go_int(rng.next() * (double)sc.num_lights);
 #ifndef IZPI_NO_LRAND_LDS
   if (staged) {
-    const double* r = lt_lds(sc.lds) + index * 16;
+    const double* r = lt_lds() + index * 16;
     if (lds_ld(r + 15) == (double)IZPI_PRIM_TRIANGLE) {
-      const double* q = lt2_lds(sc.lds) + index * 6;
+      const double* q = lt2_lds() + index * 6;
       const V3 v0 = mk(lds_ld(r), lds_ld(r + 1), lds_ld(r + 2));
       const V3 v1 = mk(lds_ld(q), lds_ld(q + 1), lds_ld(q + 2)), v2 = mk(lds_ld(q + 3), lds_ld(q + 4), lds_ld(q + 5));
       double t1 = rng.next();
@@ -1497,7 +1500,7 @@ struct ShadeParams {
   double* pool;                // [blocks][rec_pool][D] overflow unwinding records
   const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
   uint32_t num_mc, num_tex, num_spd;  // materials, textures, SPD table entries of the scene
-  uint32_t staged;             // the scene's small tables are staged in LDS per block (shade_stage)
+  uint32_t staged;             // the scene's small tables are staged in LDS per block (shade_stage): 1 the Colour ones, 2 + the Spectral ones
   uint32_t prims_staged;       // so are its primitives' GShade / GTriTex / GPrim records (at most PR_LDS)
   uint32_t* pool_ring;         // [blocks] free block ids: POOL_SHARDS rings of 1 << pool_shift entries
   unsigned long long* pool_ctr;  // [POOL_SHARDS][POOL_CTR_STRIDE] ring counters (pool_publish)
@@ -1606,31 +1609,29 @@ IZPI_DEV void rec_zero_track(uint32_t& zf, bool spec, V3 att, double s, double p
 // records' unwinding (finish) and constant-albedo hits read them with an LDS read instead
 // of a dependent L2 load.
 constexpr uint32_t MC_LDS = MT_LDS;
-IZPI_DEV double4* mc_lds() { return (double4*)lds_arena(); }  // Colour renders: at offset 0
+IZPI_DEV double4* mc_lds() { return (double4*)(lds_arena() + lds_off::MC); }
 // Copy the scene's small tables into this block's LDS (ShadeParams::staged): the
 // materials' constant colours and texture slots, the lights' PDFValue records, the
 // material and texture records, the tabulated SPDs, the background SPD, the CIE tables.
 IZPI_DEV void shade_stage(const DevScene& sc, const ShadeParams& sp) {
-  const LdsLayout& Ly = sc.lds;
   if (sp.staged) {
     const uint32_t t0 = threadIdx.x, nt = blockDim.x;
-    if (!Ly.has_cie)  // Colour renders (the only ones that read them)
-      for (uint32_t t = t0; t < sp.num_mc; t += nt) mc_lds()[t] = sp.mat_const[t];
-    for (uint32_t t = t0; t < 4 * sp.num_mc; t += nt) mt_lds(Ly)[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
-    for (uint32_t t = t0; t < 16 * sc.num_lights; t += nt) light_pack(sc.lights[t >> 4], t & 15, lt_lds(Ly) + (t & ~15u));
+    for (uint32_t t = t0; t < sp.num_mc; t += nt) mc_lds()[t] = sp.mat_const[t];
+    for (uint32_t t = t0; t < 4 * sp.num_mc; t += nt) mt_lds()[t >> 2].s[t & 3] = sc.mat_tex[t >> 2].s[t & 3];
+    for (uint32_t t = t0; t < 16 * sc.num_lights; t += nt) light_pack(sc.lights[t >> 4], t & 15, lt_lds() + (t & ~15u));
     for (uint32_t t = t0; t < 6 * sc.num_lights; t += nt) {
       const GLight& L = sc.lights[t / 6];
       const uint32_t k = t % 6;
-      lt2_lds(Ly)[t] = L.kind == IZPI_PRIM_TRIANGLE ? (k < 3 ? L.v1[k] : L.v2[k - 3]) : 0.0;
+      lt2_lds()[t] = L.kind == IZPI_PRIM_TRIANGLE ? (k < 3 ? L.v1[k] : L.v2[k - 3]) : 0.0;
     }
     constexpr uint32_t MW = sizeof(izpi_material) / 8, TW = sizeof(izpi_texture) / 8;
     for (uint32_t t = t0; t < MW * sp.num_mc; t += nt)
-      reinterpret_cast<uint64_t*>(mat_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.materials)[t];
+      reinterpret_cast<uint64_t*>(mat_lds())[t] = reinterpret_cast<const uint64_t*>(sc.materials)[t];
     for (uint32_t t = t0; t < TW * sp.num_tex; t += nt)
-      reinterpret_cast<uint64_t*>(tex_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.textures)[t];
-    for (uint32_t t = t0; t < sp.num_spd; t += nt) { spd_lds(Ly)[t] = sc.spd_wl[t]; spdv_lds(Ly)[t] = sc.spd_val[t]; }
-    if (Ly.has_cie) {
-      for (uint32_t t = t0; t < sp.num_bg_spd; t += nt) { bg_lds()[t] = sp.bg_wl[t]; bgv_lds(sp.num_bg_spd)[t] = sp.bg_val[t]; }
+      reinterpret_cast<uint64_t*>(tex_lds())[t] = reinterpret_cast<const uint64_t*>(sc.textures)[t];
+    if (sp.staged == 2) {  // the Spectral tables (the arena holds them: lds_arena_bytes)
+      for (uint32_t t = t0; t < sp.num_spd; t += nt) { spd_lds()[t] = sc.spd_wl[t]; spdv_lds()[t] = sc.spd_val[t]; }
+      for (uint32_t t = t0; t < sp.num_bg_spd; t += nt) { bg_lds()[t] = sp.bg_wl[t]; bgv_lds()[t] = sp.bg_val[t]; }
       for (uint32_t t = t0; t < IZPI_CIE_N; t += nt) {
         double* c = cie_lds();
         c[t] = c_cie_wl[t]; c[IZPI_CIE_N + t] = c_cie_x[t]; c[2 * IZPI_CIE_N + t] = c_cie_y[t];
@@ -1642,12 +1643,12 @@ IZPI_DEV void shade_stage(const DevScene& sc, const ShadeParams& sp) {
     const uint32_t t0 = threadIdx.x, nt = blockDim.x, np = sc.num_prims;
     constexpr uint32_t SW = sizeof(GShade) / 8, TW = sizeof(GTriTex) / 8, PW = sizeof(GPrim) / 8;
     for (uint32_t t = t0; t < SW * np; t += nt)
-      reinterpret_cast<uint64_t*>(gs_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.shade)[t];
+      reinterpret_cast<uint64_t*>(gs_lds())[t] = reinterpret_cast<const uint64_t*>(sc.shade)[t];
     if (sc.tritex)
       for (uint32_t t = t0; t < TW * np; t += nt)
-        reinterpret_cast<uint64_t*>(tt_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.tritex)[t];
+        reinterpret_cast<uint64_t*>(tt_lds())[t] = reinterpret_cast<const uint64_t*>(sc.tritex)[t];
     for (uint32_t t = t0; t < PW * np; t += nt)
-      reinterpret_cast<uint64_t*>(gp_lds(Ly))[t] = reinterpret_cast<const uint64_t*>(sc.prims)[t];
+      reinterpret_cast<uint64_t*>(gp_lds())[t] = reinterpret_cast<const uint64_t*>(sc.prims)[t];
   }
   __syncthreads();
 }
@@ -1785,7 +1786,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
 
 // The background SPD at lambda (sampler/spectral.go:48-51,79), staged or not
 IZPI_DEV double bg_value(const ShadeParams& sp, double lambda) {
-  if (sp.staged) return spd_value<true>(bg_lds(), bgv_lds(sp.num_bg_spd), sp.num_bg_spd, lambda, sp.bg_sorted != 0);
+  if (sp.staged) return spd_value<true>(bg_lds(), bgv_lds(), sp.num_bg_spd, lambda, sp.bg_sorted != 0);
   return spd_value<false>(sp.bg_wl, sp.bg_val, sp.num_bg_spd, lambda, sp.bg_sorted != 0);
 }
 IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colour) {
@@ -3169,7 +3170,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   hipStream_t st = ctx->stream;
   const izpi_render_tuning& tu = tuning_of(req);
   int shade_res = 0;
-  const size_t dyn = sc.lds.bytes;  // the staged tables' LDS arena (render_body)
+  const size_t dyn = sc.lds_bytes;  // the staged tables' LDS arena (render_body)
   int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res, (int)SHADE_THREADS, dyn);
   if (rc) return rc;
   // tail kernel: used once every unit has started and at most `tail_max` paths remain
@@ -3515,38 +3516,9 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.staged = 0;  // A/B builds
   sp.prims_staged = 0;
 #endif
-  {  // the per-block LDS arena of k_shade / k_tail (izd::LdsLayout): only the tables this render stages
-    LdsLayout L{};
-    uint32_t off = 0;
-    auto take = [&](uint64_t bytes) {
-      const uint32_t o = off;
-      off += (uint32_t)((bytes + 31) & ~(uint64_t)31);
-      return o;
-    };
-    if (sp.staged) {
-      const uint64_t nm = ctx->num_materials, nl = sc.num_lights;
-      if (req->sampler == IZPI_SAMPLER_SPECTRAL) {  // CIE tables at 0, the background right after (bg_lds)
-        L.has_cie = 1;
-        take(LDS_CIE_BYTES);
-        take(nbg * sizeof(double));
-        take(nbg * sizeof(double));
-      } else {
-        take(nm * sizeof(double4));  // the materials' constant colours at 0 (mc_lds)
-      }
-      L.mt = take(nm * sizeof(MatTex));
-      L.lt = take(nl * 16 * sizeof(double)); L.lt2 = take(nl * 6 * sizeof(double));
-      L.mat = take(nm * sizeof(izpi_material)); L.tex = take((uint64_t)ctx->num_textures * sizeof(izpi_texture));
-      L.spd = take((uint64_t)ctx->num_spd * sizeof(double)); L.spdv = take((uint64_t)ctx->num_spd * sizeof(double));
-    }
-    if (sp.prims_staged) {
-      const uint64_t np = sc.num_prims;
-      L.gs = take(np * sizeof(GShade));
-      L.tt = sc.tritex ? take(np * sizeof(GTriTex)) : 0;
-      L.gp = take(np * sizeof(GPrim));
-    }
-    L.bytes = off;
-    sc.lds = L;
-  }
+  if (sp.staged && (req->sampler == IZPI_SAMPLER_SPECTRAL || ctx->num_spd)) sp.staged = 2;  // + the Spectral tables
+  // k_shade / k_tail's LDS arena: the prefix of lds_off's layout that this render stages
+  sc.lds_bytes = sp.prims_staged ? lds_off::END : sp.staged == 2 ? lds_off::SPECTRAL_END : sp.staged ? lds_off::COLOUR_END : 0;
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = misc(ctx, 1);

@@ -70,7 +70,8 @@ __global__ void k_page(const double* a, uint64_t pages, uint32_t iters, uint64_t
 // buffer s and a random 24-B record write into the record buffer r per thread-iteration
 // RW: bytes per record (24: 3 doubles at level * 24; 32: the same 3 doubles at level * 32,
 // each record in one aligned 32-B sector; 64: one record per 64-B half line)
-template <int RW>
+// FULL: the record's whole RW / 8 bytes are written (a pad word too), not just its 24 B
+template <int RW, bool FULL = false>
 __global__ void k_mix(uint4* s, uint64_t n16, double* r, uint64_t slots, uint64_t seed) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   uint32_t k = 0;
@@ -81,6 +82,8 @@ __global__ void k_mix(uint4* s, uint64_t n16, double* r, uint64_t slots, uint64_
     const uint64_t h = mix(seed ^ (i * 0x9E3779B97F4A7C15ull));
     double* q = r + (h % slots) * (RW) + ((h >> 48) & 7) * (RW / 8);
     q[0] = (double)k; q[1] = (double)v.y; q[2] = 1.0;
+    if (FULL)
+      for (int w = 3; w < RW / 8; w++) q[w] = 0.0;
   }
 }
 
@@ -106,6 +109,8 @@ int mix_mode(double state_gb, double rec_gb, int rounds, int rw) {
       if (rw == 24) hipLaunchKernelGGL(k_mix<24>, dim3(blocks), dim3(256), 0, 0, (uint4*)S, sb / 16, (double*)R, slots, 11ull + r);
       if (rw == 32) hipLaunchKernelGGL(k_mix<32>, dim3(blocks), dim3(256), 0, 0, (uint4*)S, sb / 16, (double*)R, slots, 11ull + r);
       if (rw == 64) hipLaunchKernelGGL(k_mix<64>, dim3(blocks), dim3(256), 0, 0, (uint4*)S, sb / 16, (double*)R, slots, 11ull + r);
+      if (rw == 33) hipLaunchKernelGGL((k_mix<32, true>), dim3(blocks), dim3(256), 0, 0, (uint4*)S, sb / 16, (double*)R, slots, 11ull + r);
+      if (rw == 65) hipLaunchKernelGGL((k_mix<64, true>), dim3(blocks), dim3(256), 0, 0, (uint4*)S, sb / 16, (double*)R, slots, 11ull + r);
       CK(hipGetLastError());
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
@@ -128,7 +133,7 @@ int mix_mode(double state_gb, double rec_gb, int rounds, int rw) {
 }
 
 int main(int argc, char** argv) {
-  // place_probe mix STATE_GB REC_GB ROUNDS REC_BYTES
+  // place_probe mix STATE_GB REC_GB ROUNDS REC_BYTES (24, 32, 64; 33 / 65: 32 / 64 written whole)
   if (argc > 1 && argv[1][0] == 'm')
     return mix_mode(argc > 2 ? atof(argv[2]) : 20.0, argc > 3 ? atof(argv[3]) : 25.0, argc > 4 ? atoi(argv[4]) : 10, argc > 5 ? atoi(argv[5]) : 24);
   std::vector<double> sizes;

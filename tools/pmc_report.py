@@ -20,9 +20,9 @@ for k, a in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
         continue
     g = lambda n: a.get(n, 0.0)  # noqa: E731
     waves = max(g("SQ_WAVES"), 1)
-    print("%-44s waves %.3g  busy: wait_any %.2f active_any %.2f active_valu %.2f active_vmem %.2f wait_inst %.2f" % (
+    print("%-44s waves %.3g  busy: wait_any %.2f active_any %.2f active_valu %.2f active_flat %.2f wait_inst %.2f" % (
         k[:44], waves, g("SQ_WAIT_ANY") / wc, g("SQ_ACTIVE_INST_ANY") / wc, g("SQ_ACTIVE_INST_VALU") / wc,
-        g("SQ_ACTIVE_INST_VMEM") / wc, g("SQ_WAIT_INST_ANY") / wc))
+        g("SQ_ACTIVE_INST_FLAT") / wc, g("SQ_WAIT_INST_ANY") / wc))
     print("%-44s per wave: valu %.0f salu %.0f vmem_rd %.0f vmem_wr %.0f lds %.0f smem %.0f branch %.0f; "
           "vmem level/inst %.1f; L2 hit %.3f" % (
               "", g("SQ_INSTS_VALU") / waves, g("SQ_INSTS_SALU") / waves, g("SQ_INSTS_VMEM_RD") / waves,
