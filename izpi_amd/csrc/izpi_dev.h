@@ -201,7 +201,10 @@ IZPI_DEV bool sdiv_plain(double x) {  // exponent within 2^+-300
 }
 IZPI_DEV V3 sdiv(V3 a, double t) {
 #ifndef IZPI_NO_SHARED_DIV
-  const bool plain = sdiv_plain(t) & (sdiv_plain(a.x) | (a.x == 0.0)) & (sdiv_plain(a.y) | (a.y == 0.0)) & (sdiv_plain(a.z) | (a.z == 0.0));
+  // (bitwise: one test, no branches)
+  const int px = (int)sdiv_plain(a.x) | (int)(a.x == 0.0), py = (int)sdiv_plain(a.y) | (int)(a.y == 0.0),
+            pz = (int)sdiv_plain(a.z) | (int)(a.z == 0.0);
+  const bool plain = ((int)sdiv_plain(t) & px & py & pz) != 0;
   if (plain) {
     double r = __builtin_amdgcn_rcp(t);
     double e = __builtin_fma(-t, r, 1.0);

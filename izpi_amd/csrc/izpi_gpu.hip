@@ -77,6 +77,12 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
 // block-iteration; 384-thread blocks (6 waves, 2 per CU) take a third fewer but measured
 // C3 shade 114 -> 161 ms (the barriers of block_reserve2 wait for 6 waves), so 256 stays.
 constexpr uint32_t SHADE_THREADS = IZPI_SHADE_THREADS, SHADE_WAVES = SHADE_THREADS / 64;
+// k_shade's queue of deferred unwinding jobs per block (fin_flush): FINQ_WORDS 8-B words
+// per job; flushed once FINQ_FLUSH are queued, an iteration adds at most SHADE_THREADS.
+#ifndef IZPI_FINQ_FLUSH
+#define IZPI_FINQ_FLUSH 512  // C5 at 32 spp: shading 327.7 ms at 128, 323.1 at 256, 319.9 at 512
+#endif
+constexpr uint32_t FINQ_WORDS = 5, FINQ_FLUSH = IZPI_FINQ_FLUSH, FINQ_CAP = FINQ_FLUSH + SHADE_THREADS;
 #ifndef IZPI_MISC_STRIDE
 #define IZPI_MISC_STRIDE 64
 #endif
@@ -1497,6 +1503,7 @@ struct ShadeParams {
   uint64_t seed;
   double* out;                 // [total_units][3] per-sample result
   double* recs;                // [slots][rec_dense][D] unwinding records
+  unsigned long long* finq;    // [k_shade block][FINQ_WORDS][FINQ_CAP] deferred unwinding jobs (fin_flush)
   double* pool;                // [blocks][rec_pool][D] overflow unwinding records
   const double4* mat_const;    // DevScene::mat_const (MATSET_CONST records)
   uint32_t num_mc, num_tex, num_spd;  // materials, textures, SPD table entries of the scene
@@ -2009,10 +2016,11 @@ IZPI_DEV void sclk_zero() {
 // One block-wide reservation phase for a shading iteration (ONE pair of barriers, two
 // atomics by one thread): `unit_want` lanes get consecutive work units from the unit
 // head (the units past total_units are not granted); lanes with `put` and granted
-// `unit_want` lanes get consecutive output entries, `put` lanes first. A granted lane
+// `unit_want` lanes get consecutive output entries, `put` lanes first. want_rank: the
+// lane's rank among the block's `unit_want` lanes, want_total: their number (granted or not). A granted lane
 // whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
 IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
-                             uint32_t& pos, uint32_t& parity, bool& exhausted) {
+                             uint32_t& pos, uint32_t& parity, bool& exhausted, uint32_t& want_rank, uint32_t& want_total) {
   __shared__ uint32_t s_p[2][SHADE_WAVES], s_u[2][SHADE_WAVES];
   __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2], s_nent[2];
   const uint32_t b = parity;
@@ -2054,6 +2062,10 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   SCLK_ADD(SCLK_RB2, rb1);
   uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
   for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
+  want_total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SHADE_WAVES; k++) want_total += s_u[b][k];
+  want_rank = ur;
   const bool has_entry = unit_want && s_nput[b] + ur < s_nent[b];
   const bool granted = unit_want && ur < s_granted[b];
   unit = granted ? s_ubase[b] + ur : 0xFFFFFFFFu;
@@ -2098,8 +2110,9 @@ IZPI_DEV double path_length(V3 hp, V3 exit_p) {
 // Entry i of `in`: P is its path state (load_path), with blk set to the path's overflow
 // block when it needs one (P.depth >= rec_dense); `kind` its kind word. On return, P and
 // R hold the continuing path and its next ray (`push`), or `done` is set and `fblk` is
-// the block to free.
-template <int SAMPLER, int MATSET>
+// the block to free. DEFER: a finished path is not unwound here; R.o holds its terminal
+// radiance (Spectral: R.o[0]) for the caller's queue (fin_queue).
+template <int SAMPLER, int MATSET, bool DEFER = false>
 IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
                          const EntryIn& E, PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt,
                          uint32_t& c_ls) {
@@ -2284,7 +2297,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   if (!push) {
     if (terminal) {
       SCLK_T(sc1);
-      finish<SAMPLER, MATSET>(sp, P, L);
+      if constexpr (DEFER) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; }
+      else finish<SAMPLER, MATSET>(sp, P, L);
       SCLK_ADD(SCLK_FIN, sc1);
       done = true;
       fblk = P.blk;
@@ -2321,7 +2335,9 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       P.depth++;
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
-        finish<SAMPLER, MATSET>(sp, P, terminal_max_depth(sp, P, COLOUR));
+        const V3 Lt = terminal_max_depth(sp, P, COLOUR);
+        if constexpr (DEFER) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; }
+        else finish<SAMPLER, MATSET>(sp, P, Lt);
         done = true;
         fblk = P.blk;
       } else {
@@ -2386,6 +2402,50 @@ IZPI_DEV uint32_t pool_alloc_any(const ShadeParams& sp, uint32_t first) {
   return 0u;
 }
 
+// Deferred unwinding. A path that ends in a shading pass is unwound (finish) from its
+// records, depth - 1 down to 0; done in the finishing lane itself, a wave waits for its
+// deepest finishing lane while its other lanes idle (C5: finish took 48% of k_shade's
+// wave cycles with a few lanes of a wave finishing per iteration). Instead the finishing
+// lane queues a job in its block's queue, and the block unwinds the queued jobs with every
+// lane busy once FINQ_FLUSH are queued (and at the end of the launch). The records stay
+// put until then: the slot's next path writes its first record in the NEXT pass, after
+// its first ray is traced, and the finished path's overflow block is freed by fin_flush.
+// A job: unit | rslot << 32, blk | (depth | zf << 16) << 32, then the terminal radiance
+// (Colour) or L.x, lambda, lpdf (Spectral), word-major (word k of job j at k * FINQ_CAP + j).
+template <int SAMPLER>
+IZPI_DEV void fin_queue(unsigned long long* q, uint32_t j, const PathSt& P, const RayRec& R) {
+  const bool colour = SAMPLER == IZPI_SAMPLER_COLOUR;
+  q[j] = P.unit | (unsigned long long)P.rslot << 32;
+  q[FINQ_CAP + j] = P.blk | (unsigned long long)(P.depth | P.zf << 16) << 32;
+  q[2 * FINQ_CAP + j] = (unsigned long long)__double_as_longlong(R.o[0]);
+  q[3 * FINQ_CAP + j] = (unsigned long long)__double_as_longlong(colour ? R.o[1] : P.lambda);
+  q[4 * FINQ_CAP + j] = (unsigned long long)__double_as_longlong(colour ? R.o[2] : P.lpdf);
+}
+template <int SAMPLER, int MATSET>
+IZPI_DEV void fin_flush(const ShadeParams& sp, const unsigned long long* q, uint32_t n) {
+  const bool colour = SAMPLER == IZPI_SAMPLER_COLOUR;
+  for (uint32_t j = threadIdx.x; j < n; j += SHADE_THREADS) {
+    PathSt P;
+    const unsigned long long w0 = q[j], w1 = q[FINQ_CAP + j];
+    P.unit = (uint32_t)w0; P.rslot = (uint32_t)(w0 >> 32);
+    P.blk = (uint32_t)w1; P.depth = (uint32_t)(w1 >> 32) & 0xFFFFu; P.zf = (uint32_t)(w1 >> 48);
+    const double a = __longlong_as_double((long long)q[2 * FINQ_CAP + j]);
+    const double b = __longlong_as_double((long long)q[3 * FINQ_CAP + j]);
+    const double c = __longlong_as_double((long long)q[4 * FINQ_CAP + j]);
+    P.lambda = colour ? 0.0 : b; P.lpdf = colour ? 0.0 : c;
+    finish<SAMPLER, MATSET>(sp, P, colour ? mk(a, b, c) : mk(a, 0.0, 0.0));
+    if (sp.rec_pool && P.blk) pool_free_one(sp, P.blk);
+  }
+}
+// Which k_shade instances defer: 1 = the Spectral ones (C5 at 32 spp: shading 377 -> 324
+// ms; C4's MATSET_SURF colour instance measured the same either way, C3's compact colour
+// one 3-6% slower: its unwinding is short and mostly skipped, and the queue costs its
+// stores), 2 = all, 0 = none. Handing each wave's lanes jobs of similar depth (a counting
+// sort of a flush's jobs by depth) measured slower: C5 338 ms, C4 +1.4%.
+#ifndef IZPI_FIN_DEFER
+#define IZPI_FIN_DEFER 1
+#endif
+
 // One shading pass over the slots traced in the previous k_trace.
 #ifndef IZPI_SHADE_WPE
 #define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (168 VGPRs, 6 spilled; 4 waves spill 47 VGPRs and measured 1% slower)
@@ -2405,6 +2465,9 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * SHADE_THREADS;
+  constexpr bool DEFER = IZPI_FIN_DEFER == 2 || (IZPI_FIN_DEFER == 1 && SAMPLER == IZPI_SAMPLER_SPECTRAL);
+  unsigned long long* fq = sp.finq + (size_t)blockIdx.x * FINQ_WORDS * FINQ_CAP;
+  uint32_t fq_n = 0;  // jobs in this block's queue (the same in every thread)
 #ifdef IZPI_SHADE_CLOCKS
   uint64_t k_item = 0, k_ref = 0, k_push = 0;
   sclk_zero();
@@ -2441,8 +2504,8 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       parked = need && b == 0;
       c_park += parked ? 1u : 0u;
     }
-    if (live && !parked) shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls);
-    if (sp.rec_pool && fblk) pool_free_one(sp, fblk);
+    if (live && !parked) shade_item<SAMPLER, MATSET, DEFER>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls);
+    if (!DEFER && sp.rec_pool && fblk) pool_free_one(sp, fblk);
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t1 = __builtin_readcyclecounter();
     k_item += t1 - t0;
@@ -2450,8 +2513,10 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 #endif
     // one reservation phase: output entries for continuing and parked paths, new units
     // (and their entries) for finished ones
-    uint32_t unit, pos;
-    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted);
+    uint32_t unit, pos, frank, ftotal;
+    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, frank, ftotal);
+    if (DEFER && done) fin_queue<SAMPLER>(fq, fq_n + frank, P, R);  // (before refill_one reuses P)
+    if (DEFER) fq_n += ftotal;
     if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
     if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS
@@ -2465,6 +2530,15 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     t1 = __builtin_readcyclecounter();
     k_ref += t1 - t0;
 #endif
+    if (DEFER && fq_n >= FINQ_FLUSH) {  // (block-uniform; the next iteration's jobs wait for its reservation's barriers)
+      __syncthreads();
+      fin_flush<SAMPLER, MATSET>(sp, fq, fq_n);
+      fq_n = 0;
+    }
+  }
+  if (DEFER && fq_n) {
+    __syncthreads();
+    fin_flush<SAMPLER, MATSET>(sp, fq, fq_n);
   }
   const uint32_t lane = threadIdx.x & 63;
 #ifdef IZPI_SHADE_CLOCKS
@@ -2903,6 +2977,7 @@ struct izpi_ctx {
   uint32_t* d_misc = nullptr;              // words k * MISC_STRIDE (misc()): 0 unit head, 1 error, 2 trace cursor, 3..4 queue counts, 6..7 park flags
   unsigned long long* d_counters = nullptr;
   unsigned long long* d_cpart = nullptr; size_t cpart_cap = 0;  // per-wave counter rows of a render (count_add)
+  unsigned long long* d_finq = nullptr; size_t finq_cap = 0;  // k_shade blocks' deferred unwinding jobs (fin_flush)
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
@@ -2970,7 +3045,7 @@ int grow(izpi_ctx* ctx, void** p, size_t* cap, size_t bytes) {
 uint64_t workspace_bytes(const izpi_ctx* ctx) {
   return (uint64_t)ctx->samples_cap + ctx->recs_cap + ctx->pool_cap + ctx->ring_cap + ctx->running_cap + ctx->out_cap +
          ctx->tiles_cap + ctx->utiles_cap + ctx->bg_cap + ctx->state_cap + ctx->spill_cap + ctx->post_cap + ctx->share_cap +
-         ctx->gather_cap + ctx->cpart_cap;
+         ctx->gather_cap + ctx->cpart_cap + ctx->finq_cap;
 }
 
 // Device bytes of the buffers render_impl sizes per frame and may release to re-size
@@ -3178,8 +3253,9 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   int tail_res = 0;
   if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res, 256, dyn)
                       : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res, 256, dyn))) return rc;
-  if ((uint32_t)std::max({tr.blocks * 4, shade_res * (int)SHADE_WAVES, tail_res * 4}) > ctx->num_cus * CPART_BLOCKS_PER_CU * 4) {
-    ctx->err = "grid larger than the counter rows";
+  if ((uint32_t)std::max({tr.blocks * 4, shade_res * (int)SHADE_WAVES, tail_res * 4}) > ctx->num_cus * CPART_BLOCKS_PER_CU * 4 ||
+      (uint32_t)shade_res > ctx->num_cus * CPART_BLOCKS_PER_CU) {
+    ctx->err = "grid larger than the counter rows or the unwinding queues";
     return IZPI_ERR_INVALID;
   }
   if (tail_deep && (size_t)tail_res * 256 * (64 - TAIL_LDS_STACK) * sizeof(int32_t) > ctx->spill_cap) {
@@ -3482,6 +3558,8 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // counter rows: one per wave of the largest grid (run_chunks checks the grids against it)
   const uint32_t cpart_rows = ctx->num_cus * CPART_BLOCKS_PER_CU * 4u;
   if ((rc = grow(ctx, (void**)&ctx->d_cpart, &ctx->cpart_cap, (size_t)cpart_rows * CNT_N * sizeof(unsigned long long)))) return rc;
+  // deferred unwinding jobs: one queue per k_shade block (run_chunks checks its grid against it)
+  if ((rc = grow(ctx, (void**)&ctx->d_finq, &ctx->finq_cap, (size_t)ctx->num_cus * CPART_BLOCKS_PER_CU * FINQ_WORDS * FINQ_CAP * sizeof(unsigned long long)))) return rc;
   const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count();
   WaveBuf bufs[2];
   carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, need_uv, bufs);
@@ -3522,6 +3600,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.pool = rec_pool ? ctx->d_pool : nullptr; sp.pool_ring = rec_pool ? ctx->d_ring : nullptr;
   sp.pool_ctr = rec_pool ? ctx->d_pool_ctr : nullptr;
   sp.counters = ctx->d_counters; sp.cpart = ctx->d_cpart; sp.error = misc(ctx, 1);
+  sp.finq = ctx->d_finq;
   WaveParams wp{};
   wp.in = bufs[0]; wp.out = bufs[1]; wp.trace_next = misc(ctx, 2); wp.slots = slots;
   // kind words other than plain main rays: path-length rays, parked entries
@@ -3721,7 +3800,7 @@ int izpi_gpu_close(izpi_ctx* ctx) {
   void* bufs[] = {ctx->d_samples, ctx->d_recs, ctx->d_pool, ctx->d_ring, ctx->d_pool_ctr, ctx->d_running, ctx->d_out,
                   ctx->d_tiles, ctx->d_utiles, ctx->d_bg, ctx->d_misc, ctx->d_counters, ctx->d_state,
                   ctx->d_spill, ctx->d_post, ctx->d_share,
-                  ctx->d_gather, ctx->d_status, ctx->d_cpart};
+                  ctx->d_gather, ctx->d_status, ctx->d_cpart, ctx->d_finq};
   for (void* p : bufs) if (p) (void)hipFree(p);
   if (ctx->h_count) (void)hipHostFree(ctx->h_count);
   if (ctx->stall_host) (void)hipHostFree(ctx->stall_host);
