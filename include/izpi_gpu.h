@@ -107,7 +107,8 @@ enum {
   IZPI_TUNE_PASS_LOG = 32,        /* diagnostics: per-pass device times on stderr */
   IZPI_TUNE_NO_LDS_BVH = 64,      /* small scenes: traverse from global memory, not the per-block LDS copy */
   IZPI_TUNE_NO_RAY_LDS = 128,     /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
-  IZPI_TUNE_NO_PRIM_LDS = 256     /* small scenes: shading reads the primitives' records from global memory, not the per-block LDS copy */
+  IZPI_TUNE_NO_PRIM_LDS = 256,    /* small scenes: shading reads the primitives' records from global memory, not the per-block LDS copy */
+  IZPI_TUNE_NO_PLACE_PICK = 512   /* keep the record array's first allocation (no probe of alternative pages) */
 };
 
 typedef struct izpi_render_req {
@@ -304,6 +305,12 @@ int izpi_gpu_debug_fault(izpi_ctx* ctx, int where);
  * buffer is allocated while the old one is still held, then the old one is freed. The
  * contents are not kept (every render rewrites them). */
 int izpi_gpu_debug_realloc(izpi_ctx* ctx, uint32_t mask);
+
+/* Measurement hook: time (best of 2 launches, ms) a probe kernel over the current workspace
+ * that mixes a streamed 16-B read-modify-write of the first `state_gb` GB of the wavefront
+ * state with one random 24-B write into the unwinding records per piece, as a shading pass
+ * does. Overwrites both (scratch between renders). Needs a workspace (one render first). */
+int izpi_gpu_debug_place_probe(izpi_ctx* ctx, double state_gb, float* ms);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);

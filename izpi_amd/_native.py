@@ -201,7 +201,7 @@ EXPORTS = [
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
     "izpi_gpu_build_bvh4", "izpi_gpu_multi_open", "izpi_gpu_multi_close", "izpi_gpu_multi_last_error",
     "izpi_gpu_multi_size", "izpi_gpu_multi_context", "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render",
-    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_gpu_debug_realloc", "izpi_gpu_progress", "izpi_gpu_multi_progress", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
+    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_gpu_debug_realloc", "izpi_gpu_debug_place_probe", "izpi_gpu_progress", "izpi_gpu_multi_progress", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_share_block", "izpi_host_assemble_shares", "izpi_host_bvh_leaf_max", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_serialize", "izpi_scene_info", "izpi_scene_image_file",
@@ -260,6 +260,7 @@ def lib():
     L.izpi_gpu_render_rank.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
     L.izpi_gpu_debug_fault.argtypes = [C.c_void_p, C.c_int]
     L.izpi_gpu_debug_realloc.argtypes = [C.c_void_p, C.c_uint32]
+    L.izpi_gpu_debug_place_probe.argtypes = [C.c_void_p, C.c_double, C.POINTER(C.c_float)]
     L.izpi_gpu_progress.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.izpi_gpu_multi_progress.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]

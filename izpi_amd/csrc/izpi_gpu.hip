@@ -2977,7 +2977,8 @@ struct izpi_ctx {
   uint32_t* d_misc = nullptr;              // words k * MISC_STRIDE (misc()): 0 unit head, 1 error, 2 trace cursor, 3..4 queue counts, 6..7 park flags
   unsigned long long* d_counters = nullptr;
   unsigned long long* d_cpart = nullptr; size_t cpart_cap = 0;  // per-wave counter rows of a render (count_add)
-  unsigned long long* d_finq = nullptr; size_t finq_cap = 0;  // k_shade blocks' deferred unwinding jobs (fin_flush)
+  unsigned long long* d_finq = nullptr; size_t finq_cap = 0;
+  float place_ms[4] = {0, 0, 0, 0}; int place_pick = -1;  // pick_record_pages: the candidates' probe times, the one kept  // k_shade blocks' deferred unwinding jobs (fin_flush)
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
@@ -3063,9 +3064,10 @@ struct RenderBuf {
 
 // Make every buffer of `b` at least its `bytes`: if any must grow, free them all first,
 // then allocate each at exactly its size.
-int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n) {
+int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n, bool* fresh) {
   bool must = false;
   for (size_t i = 0; i < n; i++) must = must || *b[i].cap < b[i].bytes;
+  *fresh = must;
   if (!must) return IZPI_OK;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   for (size_t i = 0; i < n; i++) {
@@ -3083,6 +3085,81 @@ int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n) {
     }
     *b[i].cap = b[i].bytes;
   }
+  return IZPI_OK;
+}
+
+// Placement probe over the current workspace (shading-time modes): a streamed
+// 16-B read-modify-write of the first `n16` pieces of the state with, per piece, one random
+// 24-B record written into the record array, as a shading pass mixes them. The contents
+// of both arrays are scratch between renders (k_start and the shading passes write before
+// they read).
+__global__ void __launch_bounds__(256) k_place_probe(uint4* s, uint64_t n16, double* r, uint64_t nrec, uint64_t seed) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += stride) {
+    uint4 v = s[i];
+    v.x += 1u;
+    s[i] = v;
+    uint64_t h = seed ^ (i * 0x9E3779B97F4A7C15ull);
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+    double* q = r + (h % nrec) * 3;
+    q[0] = (double)v.y; q[1] = 0.0; q[2] = 1.0;
+  }
+}
+
+
+// One timing of k_place_probe over `gb` GB of the state and the record array `recs`:
+// the better of two launches, ms.
+float place_probe_ms(izpi_ctx* ctx, double* recs, double gb) {
+  const uint64_t n16 = std::min<uint64_t>(ctx->state_cap / 16, (uint64_t)(gb * 1e9) / 16);
+  hipStream_t st = ctx->stream;
+  float best = 1e30f;
+  for (int k = 0; k < 2; k++) {
+    if (hipEventRecord(ctx->evb[0], st) != hipSuccess) return 0.0f;
+    hipLaunchKernelGGL(k_place_probe, dim3(ctx->num_cus * 8), dim3(256), 0, st, (uint4*)ctx->d_state, n16, recs,
+                       (uint64_t)(ctx->recs_cap / 24), 77ull + k);
+    float t = 0;
+    if (hipEventRecord(ctx->evb[1], st) != hipSuccess || hipEventSynchronize(ctx->evb[1]) != hipSuccess ||
+        hipEventElapsedTime(&t, ctx->evb[0], ctx->evb[1]) != hipSuccess)
+      return 0.0f;
+    best = std::min(best, t);
+  }
+  return best;
+}
+
+// Pages for the record array (shading-time modes). k_shade's time depends on
+// where the driver put the record array against the state (C3 at 128 spp: 25.0 - 31.3 ms
+// of shading for the same frame over re-allocations of the records alone), and a short
+// probe of the same access mix tells the slow placements: the probe's slowest level
+// (~1.35x its fastest) came with 31.3 ms every time (`profiles/r5b/mode_place_recs.jsonl`).
+// So a fresh record array of at least 4 GB is probed on up to PLACE_CANDIDATES
+// allocations, each new one made while the others are held (other pages), and the
+// fastest is kept. Costs ~10 ms per candidate, on workspace allocations only.
+constexpr int PLACE_CANDIDATES = 3;
+int pick_record_pages(izpi_ctx* ctx) {
+  if (ctx->recs_cap < (4ull << 30) || !ctx->d_state || !ctx->d_recs) return IZPI_OK;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  double* cand[PLACE_CANDIDATES] = {ctx->d_recs};
+  int nc = 1, best = 0;
+  float best_ms = place_probe_ms(ctx, ctx->d_recs, 1.0);
+  ctx->place_ms[0] = best_ms;
+  for (; nc < PLACE_CANDIDATES; nc++) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < ctx->recs_cap + (8ull << 30)) break;
+    void* p = nullptr;
+    if (hipMalloc(&p, ctx->recs_cap) != hipSuccess) {
+      (void)hipGetLastError();
+      break;
+    }
+    cand[nc] = (double*)p;
+    const float t = place_probe_ms(ctx, cand[nc], 1.0);
+    ctx->place_ms[nc] = t;
+    if (t > 0.0f && t < best_ms) { best_ms = t; best = nc; }
+  }
+  for (int k = 0; k < nc; k++)
+    if (k != best) HIP_TRY(hipFree(cand[k]));
+  ctx->d_recs = cand[best];
+  ctx->place_pick = best;
+  HIP_TRY(hipGetLastError());
   return IZPI_OK;
 }
 
@@ -3547,7 +3624,12 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
       {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, need_uv, nullptr)},
       {(void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes},
   };
-  if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0])))) {
+  bool fresh = false;
+  if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0]), &fresh))) {
+    ctx->sizing_valid = false;
+    return rc;
+  }
+  if (fresh && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) && (rc = pick_record_pages(ctx))) {
     ctx->sizing_valid = false;
     return rc;
   }
@@ -4752,6 +4834,17 @@ int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* sam
     izpi_gpu_progress(c, &d, &t);
     *samples_done += d; *samples_total += t;
   }
+  return IZPI_OK;
+}
+
+int izpi_gpu_debug_place_probe(izpi_ctx* ctx, double state_gb, float* ms) {
+  if (!ctx || !ms) return IZPI_ERR_INVALID;
+  *ms = 0.0f;
+  if (!ctx->d_state || !ctx->d_recs || ctx->recs_cap < 64) { ctx->err = "no workspace yet (render once first)"; return IZPI_ERR_INVALID; }
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  *ms = place_probe_ms(ctx, ctx->d_recs, state_gb);
+  HIP_TRY(hipGetLastError());
   return IZPI_OK;
 }
 
