@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round measurement on the GPU box, from the repo root, in two calls:
-#   bash tools/measure_round.sh TAG c3     # C3 bench with its PMC passes + rocprof kernel trace (profiles/run_profile.sh)
+#   bash tools/measure_round.sh TAG c3     # C3 bench with its PMC passes + rocprof kernel trace (tools/run_profile.sh)
 #   bash tools/measure_round.sh TAG other  # C1, C2, C4 at full spp; C2 / C4 / C5 PMC (roofline + wave cycles)
 #   bash tools/measure_round.sh TAG c5     # C5 at full spp (one frame, ~100 s)
 # each step under its own time limit.
@@ -9,7 +9,7 @@ TAG=${1:?tag}; PART=${2:-c3}
 mkdir -p gpurun_out
 case $PART in
   c3)
-    bash profiles/run_profile.sh $TAG ;;
+    bash tools/run_profile.sh $TAG ;;
   other)
     timeout -k 10 200 python bench.py --config C1 --steps 20 --warmup 3 --no-pmc --no-cpu-baseline > gpurun_out/bench_c1_$TAG.log 2>&1
     timeout -k 10 300 python bench.py --config C2 --steps 3 --warmup 1 --no-pmc --no-cpu-baseline > gpurun_out/bench_c2_$TAG.log 2>&1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counter groups (one rocprofv3 --pmc pass each, no tracing) over one C3 frame:
-#   bash profiles/pmc_kernels.sh TAG [SPP]   -> gpurun_out/pmc_TAG/gN/...
+#   bash tools/pmc_kernels.sh TAG [SPP]   -> gpurun_out/pmc_TAG/gN/...
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r2}; SPP=${2:-512}; CFG=${CONFIG:-C3}
 OUT=gpurun_out/pmc_$TAG

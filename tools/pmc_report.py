@@ -1,4 +1,4 @@
-"""Per-kernel counter ratios from profiles/pmc_kernels.sh output:
+"""Per-kernel counter ratios from tools/pmc_kernels.sh output:
     python tools/pmc_report.py gpurun_out/pmc_TAG
 SQ_* counters are summed over the frame's dispatches of each kernel; *_CYCLES ratios are
 fractions of wave cycles; per-wave instruction counts are per wave launched."""

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profiling recipe for the bench workload (run on the GPU box from the repo root):
-#   bash profiles/run_profile.sh TAG
+#   bash tools/run_profile.sh TAG
 # 1. the bench itself (its own PMC passes, CPU baseline, reference-tree check) -> bench.json
 # 2. rocprofv3 --kernel-trace --stats over the same timed frames (no PMC children, no
 #    CPU baseline: a profiler must not run inside a profiler) -> kernel_stats.csv
