@@ -1367,6 +1367,9 @@ IZPI_DEV void light_pack(const GLight& L, uint32_t k, double* out) {  // k = 0..
 // HitableSlice.PDFValue over Scene.Lights (hitable_slice.go:98-105) from the packed
 // records (LDS when staged, else packed the same way on the fly from the GLight records).
 IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
+#ifdef IZPI_KRES_NO_LPDF  // register-pressure analysis builds only (tools/kres.py; never run)
+  return o.x + v.y;
+#endif
   const double weight = 1.0 / (double)sc.num_lights;
   double sum = 0;
   for (uint32_t i = 0; i < sc.num_lights; i++) {
@@ -1409,6 +1412,9 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
 IZPI_DEV double* lt2_lds() { return (double*)(lds_arena() + lds_off::LT2); }
 // HitableSlice.Random (hitable_slice.go:107-110) + Triangle/Sphere.Random
 IZPI_DEV V3 lights_random(const DevScene& sc, bool staged, V3 o, Lcg& rng) {
+#ifdef IZPI_KRES_NO_LRAND  // register-pressure analysis builds only
+  return mk(rng.next() - o.x, 1.0, 0.0);
+#endif
   int64_t index = go_int(rng.next() * (double)sc.num_lights);
 #ifndef IZPI_NO_LRAND_LDS
   if (staged) {
@@ -1673,6 +1679,10 @@ IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.ou
 // colour.go:44-57 / sampler/spectral.go:60-72 from depth-1 down to 0.
 template <int SAMPLER, int MATSET>
 IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
+#ifdef IZPI_KRES_NO_FINISH  // register-pressure analysis builds only
+  sst(sample_out(sp, P.unit), L.x);
+  return;
+#endif
   constexpr bool NO_SPEC = !ms_spec(MATSET);
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
     // +0 radiance through only non-specular records: every level computes
@@ -2080,6 +2090,10 @@ template <int SAMPLER>
 IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBuf& out, uint32_t unit, uint32_t pos,
                          PathSt& P) {
   RayRec R;
+#ifdef IZPI_KRES_NO_REFILL  // register-pressure analysis builds only
+  dead_entry(out, pos + unit);
+  return;
+#endif
   for (;;) {
     if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
       store_entry<SAMPLER>(out, pos, P, R);
