@@ -1801,6 +1801,16 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   }
 }
 
+// Whether finish(P, L) reads the path's records: not when it is at depth 0 or when its
+// terminal radiance is a +0 that the levels keep a zero (finish's two shortcuts).
+template <int SAMPLER, int MATSET>
+IZPI_DEV bool finish_reads(const PathSt& P, V3 L) {
+  const bool colour = SAMPLER == IZPI_SAMPLER_COLOUR;
+  const bool zero_term = gm::bits(L.x) == 0 && (!colour || (gm::bits(L.y) == 0 && gm::bits(L.z) == 0));
+  if (zero_term && ((colour && !ms_spec(MATSET)) || !(P.zf & ZF_UNSAFE))) return false;
+  return P.depth > 0;
+}
+
 // The background SPD at lambda (sampler/spectral.go:48-51,79), staged or not
 IZPI_DEV double bg_value(const ShadeParams& sp, double lambda) {
   if (sp.staged) return spd_value<true>(bg_lds(), bgv_lds(), sp.num_bg_spd, lambda, sp.bg_sorted != 0);
@@ -2026,19 +2036,22 @@ IZPI_DEV void sclk_zero() {
 // One block-wide reservation phase for a shading iteration (ONE pair of barriers, two
 // atomics by one thread): `unit_want` lanes get consecutive work units from the unit
 // head (the units past total_units are not granted); lanes with `put` and granted
-// `unit_want` lanes get consecutive output entries, `put` lanes first. want_rank: the
-// lane's rank among the block's `unit_want` lanes, want_total: their number (granted or not). A granted lane
+// `unit_want` lanes get consecutive output entries, `put` lanes first. q_rank: the
+// lane's rank among the block's `queue` lanes (deferred unwinding jobs), q_total: their number. A granted lane
 // whose new path cannot trace (start_path false) leaves a RAY_DEAD entry behind.
+// QSEP: `queue` lanes are a subset of the `unit_want` lanes with a ballot of their own;
+// otherwise they are the `unit_want` lanes.
+template <bool QSEP>
 IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool put, bool unit_want, uint32_t& unit,
-                             uint32_t& pos, uint32_t& parity, bool& exhausted, uint32_t& want_rank, uint32_t& want_total) {
-  __shared__ uint32_t s_p[2][SHADE_WAVES], s_u[2][SHADE_WAVES];
+                             uint32_t& pos, uint32_t& parity, bool& exhausted, bool queue, uint32_t& q_rank, uint32_t& q_total) {
+  __shared__ uint32_t s_p[2][SHADE_WAVES], s_u[2][SHADE_WAVES], s_q[2][SHADE_WAVES];
   __shared__ uint32_t s_pbase[2], s_ubase[2], s_granted[2], s_nput[2], s_nent[2];
   const uint32_t b = parity;
   parity ^= 1u;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1;
-  const uint64_t mp = __ballot(put), mu = __ballot(unit_want);
-  if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); }
+  const uint64_t mp = __ballot(put), mu = __ballot(unit_want), mq = QSEP ? __ballot(queue) : 0ull;
+  if (lane == 0) { s_p[b][w] = (uint32_t)__popcll(mp); s_u[b][w] = (uint32_t)__popcll(mu); if (QSEP) s_q[b][w] = (uint32_t)__popcll(mq); }
   SCLK_T(rb0);
   __syncthreads();
   SCLK_ADD(SCLK_RB1, rb0);
@@ -2072,10 +2085,20 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
   SCLK_ADD(SCLK_RB2, rb1);
   uint32_t ur = (uint32_t)__popcll(mu & lt), pr = (uint32_t)__popcll(mp & lt);
   for (uint32_t i = 0; i < w; i++) { ur += s_u[b][i]; pr += s_p[b][i]; }
-  want_total = 0;
+  if constexpr (QSEP) {
+    q_rank = (uint32_t)__popcll(mq & lt);
+    q_total = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < SHADE_WAVES; k++) want_total += s_u[b][k];
-  want_rank = ur;
+    for (uint32_t k = 0; k < SHADE_WAVES; k++) {
+      q_rank += k < w ? s_q[b][k] : 0u;
+      q_total += s_q[b][k];
+    }
+  } else {
+    q_rank = ur;
+    q_total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SHADE_WAVES; k++) q_total += s_u[b][k];
+  }
   const bool has_entry = unit_want && s_nput[b] + ur < s_nent[b];
   const bool granted = unit_want && ur < s_granted[b];
   unit = granted ? s_ubase[b] + ur : 0xFFFFFFFFu;
@@ -2124,12 +2147,15 @@ IZPI_DEV double path_length(V3 hp, V3 exit_p) {
 // Entry i of `in`: P is its path state (load_path), with blk set to the path's overflow
 // block when it needs one (P.depth >= rec_dense); `kind` its kind word. On return, P and
 // R hold the continuing path and its next ray (`push`), or `done` is set and `fblk` is
-// the block to free. DEFER: a finished path is not unwound here; R.o holds its terminal
-// radiance (Spectral: R.o[0]) for the caller's queue (fin_queue).
+// the block to free. DEFER: a finished path is not unwound here (`queued`; Colour: only
+// one whose unwinding reads records, finish_reads); R.o holds its terminal radiance
+// (Spectral: R.o[0]) for the caller's queue (fin_queue), and the caller frees its block
+// after the unwinding. (Spectral queues every finished path: the test cost the Spectral
+// instances up to 24 more spilled VGPRs, C5 shade 320 -> 352 ms.)
 template <int SAMPLER, int MATSET, bool DEFER = false>
 IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
                          const EntryIn& E, PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt,
-                         uint32_t& c_ls) {
+                         uint32_t& c_ls, bool& queued) {
   const bool COLOUR = SAMPLER == IZPI_SAMPLER_COLOUR;
   const bool st = sp.staged != 0;  // the scene's small tables are in this block's LDS
   SCLK_T(sc0);
@@ -2311,7 +2337,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   if (!push) {
     if (terminal) {
       SCLK_T(sc1);
-      if constexpr (DEFER) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; }
+      if constexpr (DEFER && !COLOUR) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; }
+      else if (DEFER && finish_reads<SAMPLER, MATSET>(P, L)) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; queued = true; }
       else finish<SAMPLER, MATSET>(sp, P, L);
       SCLK_ADD(SCLK_FIN, sc1);
       done = true;
@@ -2350,7 +2377,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
         const V3 Lt = terminal_max_depth(sp, P, COLOUR);
-        if constexpr (DEFER) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; }
+        if constexpr (DEFER && !COLOUR) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; }
+        else if (DEFER && finish_reads<SAMPLER, MATSET>(P, Lt)) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; queued = true; }
         else finish<SAMPLER, MATSET>(sp, P, Lt);
         done = true;
         fblk = P.blk;
@@ -2451,9 +2479,10 @@ IZPI_DEV void fin_flush(const ShadeParams& sp, const unsigned long long* q, uint
     if (sp.rec_pool && P.blk) pool_free_one(sp, P.blk);
   }
 }
-// Which k_shade instances defer: 1 = the Spectral ones (C5 at 32 spp: shading 377 -> 324
-// ms; C4's MATSET_SURF colour instance measured the same either way, C3's compact colour
-// one 3-6% slower: its unwinding is short and mostly skipped, and the queue costs its
+// Which k_shade instances defer: 1 = the Spectral ones and the Colour ones with specular
+// materials (C5 at 32 spp: shading 377 -> 320 ms; C4, queueing only the unwindings that
+// read records: 464.7 -> 453.7 ms), not C1-C3's Lambert-only instances (C3 +3.4% even
+// with only the record-reading unwindings queued: they are short, and the queue costs
 // stores), 2 = all, 0 = none. Handing each wave's lanes jobs of similar depth (a counting
 // sort of a flush's jobs by depth) measured slower: C5 338 ms, C4 +1.4%.
 #ifndef IZPI_FIN_DEFER
@@ -2479,7 +2508,8 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * SHADE_THREADS;
-  constexpr bool DEFER = IZPI_FIN_DEFER == 2 || (IZPI_FIN_DEFER == 1 && SAMPLER == IZPI_SAMPLER_SPECTRAL);
+  constexpr bool DEFER = IZPI_FIN_DEFER == 2 || (IZPI_FIN_DEFER == 1 && (SAMPLER == IZPI_SAMPLER_SPECTRAL || ms_spec(MATSET)));
+  constexpr bool COLOUR_DEFER = DEFER && SAMPLER == IZPI_SAMPLER_COLOUR;  // a subset of the finished paths is queued
   unsigned long long* fq = sp.finq + (size_t)blockIdx.x * FINQ_WORDS * FINQ_CAP;
   uint32_t fq_n = 0;  // jobs in this block's queue (the same in every thread)
 #ifdef IZPI_SHADE_CLOCKS
@@ -2518,8 +2548,11 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       parked = need && b == 0;
       c_park += parked ? 1u : 0u;
     }
-    if (live && !parked) shade_item<SAMPLER, MATSET, DEFER>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls);
-    if (!DEFER && sp.rec_pool && fblk) pool_free_one(sp, fblk);
+    bool queued = false;    // (DEFER) its unwinding waits in the block's queue
+    if (live && !parked) shade_item<SAMPLER, MATSET, DEFER>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls, queued);
+    if (SAMPLER == IZPI_SAMPLER_SPECTRAL) queued = DEFER && done;  // (every finished path)
+    // a queued path's overflow block is freed after its unwinding (fin_flush)
+    if ((COLOUR_DEFER ? !queued : !DEFER) && sp.rec_pool && fblk) pool_free_one(sp, fblk);
 #ifdef IZPI_SHADE_CLOCKS
     uint64_t t1 = __builtin_readcyclecounter();
     k_item += t1 - t0;
@@ -2528,9 +2561,9 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     // one reservation phase: output entries for continuing and parked paths, new units
     // (and their entries) for finished ones
     uint32_t unit, pos, frank, ftotal;
-    block_reserve2(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, frank, ftotal);
-    if (DEFER && done) fin_queue<SAMPLER>(fq, fq_n + frank, P, R);  // (before refill_one reuses P)
-    if (DEFER) fq_n += ftotal;
+    block_reserve2<COLOUR_DEFER>(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, queued, frank, ftotal);
+    if (queued) fin_queue<SAMPLER>(fq, fq_n + frank, P, R);  // (before refill_one reuses P)
+    fq_n += ftotal;
     if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
     if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS
@@ -2608,7 +2641,8 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
       uint32_t fblk = 0;
       EntryIn E;
       load_entry(wp.in, i, E);
-      shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls);
+      bool queued = false;  // (k_tail unwinds in place)
+      shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls, queued);
       if (fblk) pool_free_one(sp, fblk);
       if (!push) break;
       store_entry<SAMPLER>(wp.in, i, P, R);
