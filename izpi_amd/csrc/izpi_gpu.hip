@@ -4000,48 +4000,6 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       }
     }
   }
-#ifdef IZPI_NODE_ORDER
-  // measurement builds: inner nodes renumbered depth-first (1: pre-order in slot order, the
-  // order a ray's first-hit-child descent takes; 2: treelets of 3 levels stored together,
-  // breadth-first inside, treelets in depth-first order). Traversal order, floats and
-  // counters are unchanged: only the addresses move.
-  if (n_inner > 1 && ref[0] >= 0) {
-    std::vector<int32_t> perm(n_inner, -1);  // old -> new
-    uint32_t next = 0;
-    if (IZPI_NODE_ORDER == 1) {
-      std::vector<int32_t> st{ref[0]};
-      while (!st.empty()) {
-        const int32_t o = st.back(); st.pop_back();
-        perm[(size_t)o] = (int32_t)next++;
-        for (int i = 3; i >= 0; i--) if (inner[(size_t)o].child[i] >= 0) st.push_back(inner[(size_t)o].child[i]);
-      }
-    } else {
-      std::vector<int32_t> roots{ref[0]};
-      while (!roots.empty()) {
-        const int32_t tr = roots.back(); roots.pop_back();
-        std::vector<int32_t> lvl{tr}, below;
-        for (int depth = 0; depth < 3 && !lvl.empty(); depth++) {
-          std::vector<int32_t> nx;
-          for (int32_t o : lvl) {
-            perm[(size_t)o] = (int32_t)next++;
-            for (int i = 0; i < 4; i++) if (inner[(size_t)o].child[i] >= 0) nx.push_back(inner[(size_t)o].child[i]);
-          }
-          lvl.swap(nx);
-        }
-        for (auto it = lvl.rbegin(); it != lvl.rend(); ++it) roots.push_back(*it);
-      }
-    }
-    std::vector<GInner> re(inner.size());
-    for (uint32_t o = 0; o < n_inner; o++) {
-      if (perm[o] < 0) { ctx->err = "unreachable inner node"; return IZPI_ERR_INVALID; }
-      GInner g = inner[o];
-      for (int i = 0; i < 4; i++) if (g.child[i] >= 0) g.child[i] = perm[(size_t)g.child[i]];
-      re[(size_t)perm[o]] = g;
-    }
-    inner.swap(re);
-    for (uint32_t k = 0; k < d->num_nodes; k++) if (ref[k] >= 0) ref[k] = perm[(size_t)ref[k]];
-  }
-#endif
   // ---- primitives in leaf order
   std::vector<GPrim> prims(d->num_prims);
   std::vector<GShade> shade(d->num_prims);
