@@ -319,6 +319,23 @@ def test_record_pool_spectral_glass_bitwise(gpu, tune):
     r.close()
 
 
+@pytest.mark.parametrize("tune", [{}, {"rec_dense": 1, "pool_div": 100000},
+                                  {"rec_dense": 2, "pool_div": 100000, "flags": N.TUNE_NO_TAIL}, {"slots": 3000}])
+def test_deferred_unwinding_specular_colour_bitwise(gpu, tune):
+    """Colour shading with specular materials (Metal, PBR) queues the unwindings that read
+    records and runs them block-wide (fin_flush), frees their overflow blocks only then,
+    and unwinds the others in place: with parked slots, without k_tail and
+    with few slots (many flushes of partly filled queues), equal to the oracle bit for bit."""
+    scene = configs.cornell_pbr(1.0, res=64)
+    r = GPURenderer(scene, 48, 48, 8, tuning=N.tuning(**tune) if tune else None)
+    img = r.render()
+    ref, ostats = oracle_canvas(scene, 48, 48, 8, N.SAMPLER_COLOUR)
+    assert_parity(img, ref, r.stats, ostats)
+    if tune.get("pool_div") == 100000:
+        assert r.stats["pool_blocks"] == 4096, r.stats
+    r.close()
+
+
 def test_slow_slab_path_bitwise(gpu):
     """The NaN-free packed slab (slab4_fast) and the scalar twin give the same image."""
     scene = configs.cornell_dragon(1.0, n=60)
