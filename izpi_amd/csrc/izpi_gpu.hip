@@ -80,7 +80,7 @@ constexpr uint32_t SHADE_THREADS = IZPI_SHADE_THREADS, SHADE_WAVES = SHADE_THREA
 // k_shade's queue of deferred unwinding jobs per block (fin_flush): FINQ_WORDS 8-B words
 // per job; flushed once FINQ_FLUSH are queued, an iteration adds at most SHADE_THREADS.
 #ifndef IZPI_FINQ_FLUSH
-#define IZPI_FINQ_FLUSH 512  // C5 at 32 spp: shading 327.7 ms at 128, 323.1 at 256, 319.9 at 512
+#define IZPI_FINQ_FLUSH 1024  // C5 at 32 spp: shading 327.7 ms at 128, 323.1 at 256, 319.9 at 512, 318.3 at 1024
 #endif
 constexpr uint32_t FINQ_WORDS = 5, FINQ_FLUSH = IZPI_FINQ_FLUSH, FINQ_CAP = FINQ_FLUSH + SHADE_THREADS;
 #ifndef IZPI_MISC_STRIDE
