@@ -1590,8 +1590,12 @@ IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uin
 #endif
   double* rp = rec_ptr<SAMPLER, MATSET>(sp, rslot, blk, depth);
   if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {  // never specular
-    sst(rp, (double)mat);
-    sst(rp + 1, s);
+    if constexpr (RecLayout<SAMPLER, MATSET>::D == 4) {  // 32-B records: (material, s) in one 16-B store
+      sst(reinterpret_cast<double2*>(rp), make_double2((double)mat, s));
+    } else {
+      sst(rp, (double)mat);
+      sst(rp + 1, s);
+    }
     return;
   }
   const double sv = spec ? __longlong_as_double((long long)REC_SPEC_BITS) : s;
@@ -1724,7 +1728,12 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
 #ifdef IZPI_EXP_NOREC
           if (dd - j < IZPI_EXP_NOREC) { rv[j][0] = 0.0; rv[j][1] = 1.0; rv[j][2] = 1.0; continue; }
 #endif
-          rv[j][0] = sld(r); rv[j][1] = sld(r + 1); rv[j][2] = sld(r + 2);
+          if constexpr (D == 4) {  // 32-B records: two 16-B loads
+            const double2 a = sld(reinterpret_cast<const double2*>(r)), b = sld(reinterpret_cast<const double2*>(r) + 1);
+            rv[j][0] = a.x; rv[j][1] = a.y; rv[j][2] = b.x;
+          } else {
+            rv[j][0] = sld(r); rv[j][1] = sld(r + 1); rv[j][2] = sld(r + 2);
+          }
         }
       }
 #pragma unroll
