@@ -3686,7 +3686,11 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
     ctx->sizing_valid = false;
     return rc;
   }
-  if (fresh && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) && (rc = pick_record_pages(ctx))) {
+  // (only where it was measured to pay: a chunk whose samples all fit the slots, so that
+  // every pass after the first is a pure bounce pass; at C3's 512 spp it changed nothing and
+  // its extra allocations can cost a first frame ~0.1 s on a box with VRAM to clear)
+  const bool pure_bounce = (uint64_t)num_pixels * chunk <= slots;
+  if (fresh && pure_bounce && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) && (rc = pick_record_pages(ctx))) {
     ctx->sizing_valid = false;
     return rc;
   }
