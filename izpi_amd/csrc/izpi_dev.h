@@ -127,6 +127,7 @@ struct DevScene {
   uint32_t num_prims;           // GPrim records (and GLeaf slots, indexed by first primitive)
   izpi_camera cam;
   uint32_t lds_bytes;           // per render (render_body): k_shade / k_tail's dynamic LDS arena (lds_off)
+  uint32_t time_free;           // no sphere moves: traversal needs no ray times (upload)
 #ifdef IZPI_SHADOW
   // measurement builds only (byte breakdown): copies of the traversal arrays that
   // k_trace2 reads beside the real ones, so a class's bytes past L2 show as extra FETCH_SIZE

@@ -736,7 +736,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   static_assert(!LB || DIST, "the LDS-resident BVH instance runs the distributed leaf tests");
-  static_assert(!RL || (DIST && TRI && !LB), "the LDS-resident ray instance is the triangle-only global-BVH one");
+  static_assert(!RL || (DIST && (TRI || LB)), "the LDS-resident ray instances: triangle-only global BVH, or the BVH in LDS");
+  // (u, v) of the accepted hit: kept in lds_uv until the ray finishes (UVL), stored to the
+  // hit record at acceptance (UVS: the BVH-in-LDS ray instance, whose steps issue no global
+  // loads for the store to hold up), or not kept (C3's instance: nothing reads it)
+  constexpr bool UVL = !RL, UVS = RL && LB, DUV = !RL || LB;
   typedef float v4f __attribute__((ext_vector_type(4)));   // clang vectors: copyable out of an LDS lvalue
   typedef double v2d __attribute__((ext_vector_type(2)));
   typedef const __attribute__((address_space(3))) v4f LF4;
@@ -759,11 +763,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // test's result flags in the same word; distances and barycentrics
   // (+4: an owner reads its four entries unconditionally, past the wave's last batch entry)
   __shared__ uint32_t dist_owner[DIST ? 260 : 1];
-  __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST && !RL ? 260 : 1], dist_v[DIST && !RL ? 260 : 1];
+  __shared__ double dist_t[DIST ? 260 : 1], dist_u[DIST && DUV ? 260 : 1], dist_v[DIST && DUV ? 260 : 1];
   // (u, v) of the lane's accepted hit so far: the hit record is stored once, when the ray finishes
   // (a global store per accepted hit would hold up the wave's next load wait, since
   // vmcnt counts stores and loads in one queue)
-  __shared__ double2 lds_uv[RL ? 1 : 256];
+  __shared__ double2 lds_uv[UVL ? 256 : 1];
   // RL: the lane's ray (o, d) as three double2, written at its refill
   __shared__ double2 ray_lds[RL ? 3 * 256 : 1];
   const uint32_t wbase = threadIdx.x & ~63u;
@@ -869,7 +873,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             bprim = -1;
             busy = cur != -1;
             if (!busy) {
-              if (!RL && wp.hit_uv) {  // (t, prim) and (u, v) interleaved: hs == 2
+              if ((UVL || UVS) && wp.hit_uv) {  // (t, prim) and (u, v) interleaved: hs == 2
                 double2* rec = wp.in.hit + ((size_t)my << 1);
                 sst(rec, hit_pack(0.0, -1)); sst(rec + 1, make_double2(0.0, 0.0));
               } else {
@@ -960,13 +964,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           } else {
             // sphere: both roots now, their tMin tests as flags; tMax is applied in order
             // by the owner (sphere.go:72-92: root 0 if tMin < t0 < tMax, else root 1)
-            const double time = wp.in.time ? wp.in.time[oqi] : 0.0;
+            // (a scene whose spheres do not move: center(time) == center(time0), no load)
+            const double time = sc.time_free ? pa[7] : (wp.in.time ? wp.in.time[oqi] : 0.0);
             flags = 2u;
             if (sph_roots(sph_center(pa, time), pa[6], o, d, t, u))
               flags |= 1u | (t > otmin ? 4u : 0u) | (u > otmin ? 8u : 0u);
           }
           dist_t[wbase + lane] = t;
-          if constexpr (!RL) { dist_u[wbase + lane] = u; dist_v[wbase + lane] = v; }
+          if constexpr (DUV) { dist_u[wbase + lane] = u; dist_v[wbase + lane] = v; }
           dist_owner[wbase + lane] = flags;
         }
         const uint32_t n_sph_tests = TRI ? 0u : (uint32_t)__popcll(__ballot(lane < total && (dist_owner[wbase + lane] & 2u)));
@@ -984,7 +989,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           for (uint32_t i = 0; i < 4; i++)  // reject only `t > tMax` (triangle.go:219), in primitive order
             if (i < cnt && (f[i] & 1u) && !(tt[i] > tmax)) { tmax = tt[i]; acc = (int32_t)i; }
           if (acc >= 0) {
-            if constexpr (!RL) lds_uv[threadIdx.x] = make_double2(dist_u[j0 + acc], dist_v[j0 + acc]);
+            if constexpr (UVL) lds_uv[threadIdx.x] = make_double2(dist_u[j0 + acc], dist_v[j0 + acc]);
+            if constexpr (UVS)
+              if (wp.hit_uv) sst(wp.in.hit + ((size_t)qi << 1) + 1, make_double2(dist_u[j0 + acc], dist_v[j0 + acc]));
             bprim = pk + acc;
             clean_from = sp;
           }
@@ -1007,7 +1014,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
               else if (tb < tmax && (f & 8u)) { tmax = tb; acc = (int32_t)j; acc_u = 1.0; acc_v = 0.0; bprim = pk + (int32_t)i; }
             }
           }
-          if (acc >= 0) { lds_uv[threadIdx.x] = make_double2(acc_u, acc_v); clean_from = sp; }
+          if (acc >= 0) {
+            if constexpr (UVS) {
+              if (wp.hit_uv) sst(wp.in.hit + ((size_t)qi << 1) + 1, make_double2(acc_u, acc_v));
+            } else {
+              lds_uv[threadIdx.x] = make_double2(acc_u, acc_v);
+            }
+            clean_from = sp;
+          }
           pk = pend;
           in_prim = false;
           advance = true;
@@ -1194,10 +1208,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
       pend = lf ? leaf_start(top) + leaf_count(top) : pend;
       clean_from = (do_pop && spn < clean_from) ? spn : clean_from;
       if (do_fin) {
-        const double2 uv = (!RL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
-        if (!RL && wp.hit_uv) {  // (t, prim) and (u, v) in one 32-B record (hs == 2)
+        const double2 uv = (UVL && bprim >= 0) ? lds_uv[threadIdx.x] : make_double2(0.0, 0.0);
+        if ((UVL || UVS) && wp.hit_uv) {  // (t, prim) and (u, v) in one 32-B record (hs == 2)
           double2* rec = wp.in.hit + ((size_t)qi << 1);
-          sst(rec, hit_pack(bprim >= 0 ? tmax : 0.0, bprim)); sst(rec + 1, uv);
+          sst(rec, hit_pack(bprim >= 0 ? tmax : 0.0, bprim));
+          if (!UVS || bprim < 0) sst(rec + 1, uv);  // (UVS: an accepted hit's (u, v) is there already)
         } else {  // nothing reads (u, v): 16 B per entry (hs == 1)
           sst(wp.in.hit + qi, hit_pack(bprim >= 0 ? tmax : 0.0, bprim));
         }
@@ -3308,8 +3323,15 @@ inline izpi_render_tuning tuning_of(const izpi_render_req* req) {
 
 #define IZPI_T2_LIST(X)                                                                                      \
   X(true, false, false, false) X(true, true, false, false) X(false, false, false, false) X(false, true, false, false) \
-  X(true, false, true, false) X(true, true, true, false) X(true, true, false, true)
+  X(true, false, true, false) X(true, true, true, false) X(true, true, false, true) X(true, false, true, true)  \
+  X(true, true, true, true)
+// The BVH-in-LDS ray instances run an 8-entry stack ring: their trees (at most 4 KB) are
+// too shallow to fill it, and the 8 KB it frees hold the rays (still 5 blocks per CU).
+constexpr int ring_of(bool lb, bool rl) { return lb && rl ? 8 : TRACE_RING; }
 
+#ifndef IZPI_LB_RAY_LDS
+#define IZPI_LB_RAY_LDS 1  // the BVH-in-LDS scenes keep their rays in LDS too
+#endif
 // Pick the k_trace2 instance and its grid (no allocation: the caller grows d_spill to
 // t->spill_bytes).
 // need_uv: the caller reads the hits' (u, v) (WaveParams::hit_uv).
@@ -3328,14 +3350,14 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, bool need_uv, Trace
     t->refill_min = 40;
     t->prim_w = 24;
   }
-  t->ray_lds = t->p2 && t->tri && !t->lds_bvh && !need_uv && !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
+  t->ray_lds = t->p2 && ((t->tri && !t->lds_bvh && !need_uv) || (t->lds_bvh && IZPI_LB_RAY_LDS)) && !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
   if (tu.prim_weight) t->prim_w = tu.prim_weight;
   if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
   if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
   int rc = IZPI_ERR_INVALID;
 #define IZPI_T2_OCC(P, T, L, R)                                               \
   if (t->p2 == P && t->tri == T && t->lds_bvh == L && t->ray_lds == R) \
-    rc = resident_blocks(ctx, k_trace2<TRACE_RING, TRACE_WPE, P, T, L, R>, &t->blocks);
+    rc = resident_blocks(ctx, k_trace2<ring_of(L, R), TRACE_WPE, P, T, L, R>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
 #undef IZPI_T2_OCC
   if (rc) return rc;
@@ -3348,7 +3370,7 @@ void launch_trace(izpi_ctx* ctx, const DevScene& sc, const Tracer& t, const Wave
   const uint32_t stride = (uint32_t)t.blocks * 256;
 #define IZPI_T2_LAUNCH(P, T, L, R)                                                                             \
   if (t.p2 == P && t.tri == T && t.lds_bvh == L && t.ray_lds == R) {                                           \
-    hipLaunchKernelGGL((k_trace2<TRACE_RING, TRACE_WPE, P, T, L, R>), g, b, 0, st, sc, wp, ctx->d_counters,    \
+    hipLaunchKernelGGL((k_trace2<ring_of(L, R), TRACE_WPE, P, T, L, R>), g, b, 0, st, sc, wp, ctx->d_counters,  \
                        misc(ctx, 1), spill, stride, t.prim_w, t.tchunk, t.refill_min);                        \
     return;                                                                                                    \
   }
@@ -4265,6 +4287,21 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;
   sc.tri_only = d->num_spheres == 0 ? 1u : 0u;
+  {  // time_free: no sphere moves, so Sphere.center(time) == center(time0) for every ray time
+     // (c1 == c0 finite: (c1 - c0) * x = +0 for the x >= 0 every camera time gives)
+    bool tf = true;
+    const double tmin_cam = std::min(d->camera.time0, d->camera.time1);
+    if (!std::isfinite(d->camera.time0) || !std::isfinite(d->camera.time1)) tf = false;
+    for (uint32_t i = 0; tf && i < d->num_spheres; i++) {
+      const double* c0 = d->sph_center0 + 3 * (size_t)i;
+      const double* c1 = d->sph_center1 + 3 * (size_t)i;
+      const double t0 = d->sph_time[2 * (size_t)i], t1 = d->sph_time[2 * (size_t)i + 1];
+      for (int k = 0; k < 3; k++)
+        if (!std::isfinite(c0[k]) || memcmp(c0 + k, c1 + k, sizeof(double)) != 0) tf = false;
+      if (!std::isfinite(t0) || !std::isfinite(t1) || !(t1 > t0) || !(tmin_cam >= t0)) tf = false;
+    }
+    sc.time_free = tf ? 1u : 0u;
+  }
   sc.no_pathlen = 1;
   for (uint32_t i = 0; i < d->num_materials; i++)
     if (d->materials[i].kind == IZPI_MAT_DIELECTRIC) sc.no_pathlen = 0;

@@ -287,12 +287,13 @@ def test_kernel_variants_bitwise(gpu, tune):
     r.close()
 
 
-@pytest.mark.parametrize("flags", [0, N.TUNE_NO_LDS_BVH, N.TUNE_NO_PRIM_LDS])
+@pytest.mark.parametrize("flags", [0, N.TUNE_NO_LDS_BVH, N.TUNE_NO_PRIM_LDS, N.TUNE_NO_RAY_LDS])
 @pytest.mark.parametrize("which", ["cornell", "glass", "pbr"])
 def test_small_scene_lds_bvh_bitwise(gpu, which, flags):
     """A scene whose whole BVH4 (inner nodes, leaf records, primitives) fits in 4 KB is
-    traversed from every block's LDS copy (C1, C2, C4, C5); with IZPI_TUNE_NO_LDS_BVH from
-    global memory. Its primitives' shading records (GShade, triangle UVs and tangent frames,
+    traversed from every block's LDS copy (C1, C2, C4, C5), its rays kept in LDS too (with
+    IZPI_TUNE_NO_RAY_LDS re-read from global memory by the primitive tests); with
+    IZPI_TUNE_NO_LDS_BVH from global memory. Its primitives' shading records (GShade, triangle UVs and tangent frames,
     sphere records) are read from the shading blocks' LDS copy, or with
     IZPI_TUNE_NO_PRIM_LDS from global memory. All equal the oracle bit for bit, counters
     included (bvh4.go:49-164, triangle.go:223-264, sphere.go:71-92)."""
