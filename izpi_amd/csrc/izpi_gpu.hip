@@ -965,7 +965,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
             // sphere: both roots now, their tMin tests as flags; tMax is applied in order
             // by the owner (sphere.go:72-92: root 0 if tMin < t0 < tMax, else root 1)
             // (a scene whose spheres do not move: center(time) == center(time0), no load)
-            const double time = sc.time_free ? pa[7] : (wp.in.time ? wp.in.time[oqi] : 0.0);
+            // (the BVH-in-LDS ray instance runs only on such scenes: make_tracer)
+            const double time = (RL && LB) || sc.time_free ? pa[7] : (wp.in.time ? wp.in.time[oqi] : 0.0);
             flags = 2u;
             if (sph_roots(sph_center(pa, time), pa[6], o, d, t, u))
               flags |= 1u | (t > otmin ? 4u : 0u) | (u > otmin ? 8u : 0u);
@@ -3350,7 +3351,8 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, bool need_uv, Trace
     t->refill_min = 40;
     t->prim_w = 24;
   }
-  t->ray_lds = t->p2 && ((t->tri && !t->lds_bvh && !need_uv) || (t->lds_bvh && IZPI_LB_RAY_LDS)) && !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
+  t->ray_lds = t->p2 && ((t->tri && !t->lds_bvh && !need_uv) || (t->lds_bvh && IZPI_LB_RAY_LDS && (t->tri || ctx->sc.time_free))) &&
+               !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
   if (tu.prim_weight) t->prim_w = tu.prim_weight;
   if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
   if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
