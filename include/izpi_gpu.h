@@ -108,8 +108,8 @@ enum {
   IZPI_TUNE_NO_LDS_BVH = 64,      /* small scenes: traverse from global memory, not the per-block LDS copy */
   IZPI_TUNE_NO_RAY_LDS = 128,     /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
   IZPI_TUNE_NO_PRIM_LDS = 256,    /* small scenes: shading reads the primitives' records from global memory, not the per-block LDS copy */
-  IZPI_TUNE_NO_PLACE_PICK = 512   /* keep the record array's first allocation: no probe of alternative pages (done only
-                                     when a chunk's samples all fit the slots and the records take >= 4 GB) */
+  IZPI_TUNE_NO_PLACE_PICK = 512   /* keep the record array's first allocation: no probe of alternative pages (done when
+                                     the records take >= 4 GB: 3 candidates if a chunk's samples all fit the slots, else 2) */
 };
 
 typedef struct izpi_render_req {

@@ -3204,18 +3204,22 @@ float place_probe_ms(izpi_ctx* ctx, double* recs, double gb) {
 // of shading for the same frame over re-allocations of the records alone), and a short
 // probe of the same access mix tells the slow placements: the probe's slowest level
 // (~1.35x its fastest) came with 31.3 ms every time (`profiles/r5b/mode_place_recs.jsonl`).
-// So a fresh record array of at least 4 GB is probed on up to PLACE_CANDIDATES
-// allocations, each new one made while the others are held (other pages), and the
-// fastest is kept. Costs ~10 ms per candidate, on workspace allocations only.
+// At C3's 512 spp the same holds on boxes that show the slow mode: over six re-allocations
+// the probe read 3.37-3.41 ms with 113.6-113.8 ms of shading and 3.00-3.10 ms with
+// 104.1-105.7 (`profiles/r5b/mode_place_512.jsonl`). So a fresh record array of at least
+// 4 GB is probed on up to PLACE_CANDIDATES allocations, each new one made while the others
+// are held (other pages), and the fastest is kept. Costs ~10 ms per candidate plus the
+// allocations, on workspace allocations only.
 constexpr int PLACE_CANDIDATES = 3;
-int pick_record_pages(izpi_ctx* ctx) {
+int pick_record_pages(izpi_ctx* ctx, int candidates) {
   if (ctx->recs_cap < (4ull << 30) || !ctx->d_state || !ctx->d_recs) return IZPI_OK;
+  candidates = std::min(candidates, PLACE_CANDIDATES);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   double* cand[PLACE_CANDIDATES] = {ctx->d_recs};
   int nc = 1, best = 0;
   float best_ms = place_probe_ms(ctx, ctx->d_recs, 1.0);
   ctx->place_ms[0] = best_ms;
-  for (; nc < PLACE_CANDIDATES; nc++) {
+  for (; nc < candidates; nc++) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < ctx->recs_cap + (8ull << 30)) break;
     void* p = nullptr;
@@ -3710,11 +3714,11 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
     ctx->sizing_valid = false;
     return rc;
   }
-  // (only where it was measured to pay: a chunk whose samples all fit the slots, so that
-  // every pass after the first is a pure bounce pass; at C3's 512 spp it changed nothing and
-  // its extra allocations can cost a first frame ~0.1 s on a box with VRAM to clear)
+  // (three candidates for a chunk whose samples all fit the slots, where every pass after
+  // the first is a pure bounce pass and the modes are widest; two otherwise: each extra
+  // allocation can cost a first frame ~60 ms on a box with VRAM to clear)
   const bool pure_bounce = (uint64_t)num_pixels * chunk <= slots;
-  if (fresh && pure_bounce && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) && (rc = pick_record_pages(ctx))) {
+  if (fresh && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) && (rc = pick_record_pages(ctx, pure_bounce ? 3 : 2))) {
     ctx->sizing_valid = false;
     return rc;
   }
