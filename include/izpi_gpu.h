@@ -310,7 +310,8 @@ int izpi_gpu_debug_realloc(izpi_ctx* ctx, uint32_t mask);
 /* Measurement hook: time (best of 2 launches, ms) a probe kernel over the current workspace
  * that mixes a streamed 16-B read-modify-write of the first `state_gb` GB of the wavefront
  * state with one random 24-B write into the unwinding records per piece, as a shading pass
- * does. Overwrites both (scratch between renders). Needs a workspace (one render first). */
+ * does (state_gb < 0: |state_gb| GB taken as 64-KB runs spread over the whole state).
+ * Overwrites both (scratch between renders). Needs a workspace (one render first). */
 int izpi_gpu_debug_place_probe(izpi_ctx* ctx, double state_gb, float* ms);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */

@@ -3051,7 +3051,7 @@ struct izpi_ctx {
   unsigned long long* d_counters = nullptr;
   unsigned long long* d_cpart = nullptr; size_t cpart_cap = 0;  // per-wave counter rows of a render (count_add)
   unsigned long long* d_finq = nullptr; size_t finq_cap = 0;
-  float place_ms[4] = {0, 0, 0, 0}; int place_pick = -1;  // pick_record_pages: the candidates' probe times, the one kept  // k_shade blocks' deferred unwinding jobs (fin_flush)
+  float place_ms[2] = {0, 0}; int place_pick[2] = {-1, -1};  // pick_pages (records, state): the kept candidate and its probe time  // k_shade blocks' deferred unwinding jobs (fin_flush)
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
@@ -3166,12 +3166,16 @@ int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n, bool* fresh) {
 // 24-B record written into the record array, as a shading pass mixes them. The contents
 // of both arrays are scratch between renders (k_start and the shading passes write before
 // they read).
-__global__ void __launch_bounds__(256) k_place_probe(uint4* s, uint64_t n16, double* r, uint64_t nrec, uint64_t seed) {
+// bstride != 0: the n16 pieces are taken as 64-KB runs spread over the whole state (run k
+// at k * bstride pieces) instead of one contiguous range.
+__global__ void __launch_bounds__(256) k_place_probe(uint4* s, uint64_t n16, double* r, uint64_t nrec, uint64_t seed,
+                                                     uint64_t bstride) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += stride) {
-    uint4 v = s[i];
+    const uint64_t a = bstride ? (i >> 12) * bstride + (i & 4095u) : i;
+    uint4 v = s[a];
     v.x += 1u;
-    s[i] = v;
+    s[a] = v;
     uint64_t h = seed ^ (i * 0x9E3779B97F4A7C15ull);
     h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
     double* q = r + (h % nrec) * 3;
@@ -3182,14 +3186,20 @@ __global__ void __launch_bounds__(256) k_place_probe(uint4* s, uint64_t n16, dou
 
 // One timing of k_place_probe over `gb` GB of the state and the record array `recs`:
 // the better of two launches, ms.
-float place_probe_ms(izpi_ctx* ctx, double* recs, double gb) {
-  const uint64_t n16 = std::min<uint64_t>(ctx->state_cap / 16, (uint64_t)(gb * 1e9) / 16);
+float place_probe_ms(izpi_ctx* ctx, char* state, double* recs, double gb, bool spread = false) {
+  const uint64_t total16 = ctx->state_cap / 16;
+  uint64_t n16 = std::min<uint64_t>(total16, (uint64_t)(gb * 1e9) / 16);
+  uint64_t bstride = 0;
+  if (spread && n16 >= 4096 && total16 > n16) {
+    n16 &= ~(uint64_t)4095;
+    bstride = (total16 / (n16 >> 12)) & ~(uint64_t)4095;  // >= 4096: the runs do not overlap
+  }
   hipStream_t st = ctx->stream;
   float best = 1e30f;
   for (int k = 0; k < 2; k++) {
     if (hipEventRecord(ctx->evb[0], st) != hipSuccess) return 0.0f;
-    hipLaunchKernelGGL(k_place_probe, dim3(ctx->num_cus * 8), dim3(256), 0, st, (uint4*)ctx->d_state, n16, recs,
-                       (uint64_t)(ctx->recs_cap / 24), 77ull + k);
+    hipLaunchKernelGGL(k_place_probe, dim3(ctx->num_cus * 8), dim3(256), 0, st, (uint4*)state, n16, recs,
+                       (uint64_t)(ctx->recs_cap / 24), 77ull + k, bstride);
     float t = 0;
     if (hipEventRecord(ctx->evb[1], st) != hipSuccess || hipEventSynchronize(ctx->evb[1]) != hipSuccess ||
         hipEventElapsedTime(&t, ctx->evb[0], ctx->evb[1]) != hipSuccess)
@@ -3199,43 +3209,60 @@ float place_probe_ms(izpi_ctx* ctx, double* recs, double gb) {
   return best;
 }
 
-// Pages for the record array (shading-time modes). k_shade's time depends on
-// where the driver put the record array against the state (C3 at 128 spp: 25.0 - 31.3 ms
-// of shading for the same frame over re-allocations of the records alone), and a short
-// probe of the same access mix tells the slow placements: the probe's slowest level
-// (~1.35x its fastest) came with 31.3 ms every time (`profiles/r5b/mode_place_recs.jsonl`).
-// At C3's 512 spp the same holds on boxes that show the slow mode: over six re-allocations
-// the probe read 3.37-3.41 ms with 113.6-113.8 ms of shading and 3.00-3.10 ms with
-// 104.1-105.7 (`profiles/r5b/mode_place_512.jsonl`). So a fresh record array of at least
-// 4 GB is probed on up to PLACE_CANDIDATES allocations, each new one made while the others
-// are held (other pages), and the fastest is kept. Costs ~10 ms per candidate plus the
-// allocations, on workspace allocations only.
+// Pages for the record array and the wavefront state (shading-time modes).
+// k_shade's time depends on where the driver put the record array and the state (C3 at
+// 128 spp: 25.0 - 31.3 ms of shading for the same frame over re-allocations of the records
+// alone), and a short probe of the same access mix tells the slow placements: the probe's
+// slowest level (~1.35x its fastest) came with 31.3 ms every time
+// (`profiles/r5b/mode_place_recs.jsonl`). At C3's 512 spp the same holds on boxes that
+// show the slow mode: over re-allocations of the records the probe read 3.37-3.41 ms with
+// 113.6-113.8 ms of shading and 3.00-3.10 ms with 104.1-105.7 (`mode_place_512.jsonl`);
+// over re-allocations of the state, with the probe's 1 GB spread over the whole state in
+// 64-KB runs, 3.35-3.39 ms with 109.3-112.9 ms and 3.16-3.20 ms with 103.9-104.2
+// (`mode_place_512_state2.jsonl`). So each fresh buffer of at least 4 GB is probed on up
+// to `candidates` allocations, each new one made while the others are held (other pages),
+// and the fastest is kept: the records first, then the state. Costs ~7 ms per candidate
+// plus the allocations, on workspace allocations only.
+// The state is not picked by default (IZPI_PICK_STATE): its 70-GB candidate cost a first
+// frame 4.6 s of allocation on a box with VRAM to clear, for 106.3 -> 105.6 ms of shading
+// over five process pairs on a box without a slow mode (`ab_pickstate_c3.jsonl`).
+#ifndef IZPI_PICK_STATE
+#define IZPI_PICK_STATE 0
+#endif
 constexpr int PLACE_CANDIDATES = 3;
-int pick_record_pages(izpi_ctx* ctx, int candidates) {
-  if (ctx->recs_cap < (4ull << 30) || !ctx->d_state || !ctx->d_recs) return IZPI_OK;
+int pick_pages(izpi_ctx* ctx, bool state_buf, int candidates) {
+  const size_t cap = state_buf ? ctx->state_cap : ctx->recs_cap;
+  if (cap < (4ull << 30) || !ctx->d_state || !ctx->d_recs) return IZPI_OK;
   candidates = std::min(candidates, PLACE_CANDIDATES);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  double* cand[PLACE_CANDIDATES] = {ctx->d_recs};
+  void* cand[PLACE_CANDIDATES] = {state_buf ? (void*)ctx->d_state : (void*)ctx->d_recs};
+  auto probe = [&](void* p) {
+    return place_probe_ms(ctx, state_buf ? (char*)p : (char*)ctx->d_state, state_buf ? ctx->d_recs : (double*)p, 1.0, true);
+  };
   int nc = 1, best = 0;
-  float best_ms = place_probe_ms(ctx, ctx->d_recs, 1.0);
-  ctx->place_ms[0] = best_ms;
+  float best_ms = probe(cand[0]);
   for (; nc < candidates; nc++) {
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < ctx->recs_cap + (8ull << 30)) break;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < cap + (8ull << 30)) break;
     void* p = nullptr;
-    if (hipMalloc(&p, ctx->recs_cap) != hipSuccess) {
+    const auto a0 = std::chrono::steady_clock::now();
+    if (hipMalloc(&p, cap) != hipSuccess) {
       (void)hipGetLastError();
       break;
     }
-    cand[nc] = (double*)p;
-    const float t = place_probe_ms(ctx, cand[nc], 1.0);
-    ctx->place_ms[nc] = t;
+    cand[nc] = p;
+    const float t = probe(p);
     if (t > 0.0f && t < best_ms) { best_ms = t; best = nc; }
+    // an allocation that waited for the driver to clear VRAM (seconds after a large
+    // process): no further candidates, the first frame has paid enough
+    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a0).count() > 50.0) { nc++; break; }
   }
   for (int k = 0; k < nc; k++)
     if (k != best) HIP_TRY(hipFree(cand[k]));
-  ctx->d_recs = cand[best];
-  ctx->place_pick = best;
+  if (state_buf) ctx->d_state = (char*)cand[best];
+  else ctx->d_recs = (double*)cand[best];
+  ctx->place_pick[state_buf ? 1 : 0] = best;
+  ctx->place_ms[state_buf ? 1 : 0] = best_ms;
   HIP_TRY(hipGetLastError());
   return IZPI_OK;
 }
@@ -3718,7 +3745,11 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // the first is a pure bounce pass and the modes are widest; two otherwise: each extra
   // allocation can cost a first frame ~60 ms on a box with VRAM to clear)
   const bool pure_bounce = (uint64_t)num_pixels * chunk <= slots;
-  if (fresh && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) && (rc = pick_record_pages(ctx, pure_bounce ? 3 : 2))) {
+  // (not when the workspace itself waited for the driver to clear VRAM: more allocations
+  // would wait too)
+  const bool alloc_fast = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count() < 50.0;
+  if (fresh && alloc_fast && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) &&
+      ((rc = pick_pages(ctx, false, pure_bounce ? 3 : 2)) || (IZPI_PICK_STATE && (rc = pick_pages(ctx, true, 2))))) {
     ctx->sizing_valid = false;
     return rc;
   }
@@ -4905,7 +4936,7 @@ int izpi_gpu_debug_place_probe(izpi_ctx* ctx, double state_gb, float* ms) {
   if (!ctx->d_state || !ctx->d_recs || ctx->recs_cap < 64) { ctx->err = "no workspace yet (render once first)"; return IZPI_ERR_INVALID; }
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  *ms = place_probe_ms(ctx, ctx->d_recs, state_gb);
+  *ms = place_probe_ms(ctx, (char*)ctx->d_state, ctx->d_recs, std::fabs(state_gb), state_gb < 0);  // (< 0: spread over the whole state)
   HIP_TRY(hipGetLastError());
   return IZPI_OK;
 }
