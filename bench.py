@@ -84,6 +84,10 @@ def parse(argv=None):
                    help="skip the reference-tree frame (timing and image comparison) of --bvh gpu")
     p.add_argument("--obj", default=None, help="C3 with this OBJ mesh (e.g. the Stanford dragon) instead of the "
                                                "synthetic one")
+    p.add_argument("--accumulation", default="forward", choices=["forward", "recursive"],
+                   help="forward (default): IZPI_ACC_FORWARD, checked at N=1 against frames of the bitwise "
+                        "recursion in the same run (pixel RMSE < 1e-6, same NaN / Inf pixels, else the recursion's "
+                        "figures are reported); recursive: IZPI_ACC_RECURSIVE, bit-identical to the oracle")
     return p.parse_args(argv)
 
 
@@ -144,7 +148,7 @@ def pmc_children(args, timeout=240):
     single GPU): per-kernel counter sums and dispatch counts."""
     out = {}
     base = [sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config, "--steps", "1",
-            "--warmup", "0", "--bvh", args.bvh]
+            "--warmup", "0", "--bvh", args.bvh, "--accumulation", args.accumulation]
     if args.spp:
         base += ["--spp", str(args.spp)]
     if args.scene:
@@ -355,32 +359,42 @@ def main():
         else:
             torch.cuda.synchronize()
 
-    def timed(bvh, steps, warmup, keep=False, reuse=None):
+    acc_main = N.ACC_FORWARD if args.accumulation == "forward" else N.ACC_RECURSIVE
+
+    def timed(bvh, steps, warmup, keep=False, reuse=None, acc=None, retree=True, host_canvas=False):
         """warmup untimed + `steps` timed frames; returns (elapsed, per-step stats sums of
         this process's device(s), canvas, info). keep: leave the (single-GPU) renderer open
         and return it as info["renderer"]; reuse: such a renderer, whose context and render
-        buffers take the scene again with the `bvh` tree (one workspace per process: the
-        driver clears every byte a process touched before handing it to the next one)."""
+        buffers take the scene again with the `bvh` tree when `retree` (one workspace per
+        process: the driver clears every byte a process touched before handing it to the next
+        one). acc: the accumulation mode (N.ACC_*, default the run's). host_canvas: each step
+        returns the canvas to host memory as izpi_gpu_render does for the Go shim."""
+        acc = acc_main if acc is None else acc
         ts = time.time()
         if reuse is not None:
             r = reuse
-            r.use_tree(scene, bvh, bvh_leaf_max=args.bvh_leaf_max)
+            r.accumulation = acc
+            if retree:
+                r.use_tree(scene, bvh, bvh_leaf_max=args.bvh_leaf_max)
             canvas_holder = {}
 
             def step():
+                if host_canvas:
+                    canvas_holder["c"] = r.render(post=post)
+                    return [r.stats]
                 canvas, st = r.render_distributed(rank, world, post=post)
                 canvas_holder["c"] = canvas
                 return [st]
         elif mode == "threads":
             r = MultiGPURenderer(scene, cfg.width, cfg.height, spp, list(range(n_gpus)), max_depth=cfg.max_depth,
-                                 sampler=cfg.sampler, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
+                                 sampler=cfg.sampler, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max, accumulation=acc)
 
             def step():
                 r.render(post=post, to_host=False)
                 return r.stats
         else:
             r = GPURenderer(scene, cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler,
-                            device=local, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max)
+                            device=local, bvh=bvh, bvh_leaf_max=args.bvh_leaf_max, accumulation=acc)
             if mode == "ranks":
                 cid = bytearray(N.COMM_ID_BYTES)
                 if rank == 0:
@@ -440,7 +454,8 @@ def main():
         if mode == "threads":  # one more frame, to the host, for the image summary
             img = r.render(post=post)
         elif rank == 0:
-            img = canvas_holder["c"].cpu().numpy() if canvas_holder.get("c") is not None else None
+            c = canvas_holder.get("c")
+            img = None if c is None else c if isinstance(c, np.ndarray) else c.cpu().numpy()
         if keep and mode == "single":
             info["renderer"] = r
         else:
@@ -452,19 +467,54 @@ def main():
         print(json.dumps({"pmc_child": True, "ms": elapsed * 1e3}), flush=True)
         return
 
-    want_ref = mode == "single" and args.bvh == "gpu" and not args.no_reference_check
-    elapsed, agg, img, info = timed(args.bvh, args.steps, args.warmup, keep=want_ref)
+    want_checks = mode == "single" and not args.no_reference_check
+    elapsed, agg, img, info = timed(args.bvh, args.steps, args.warmup, keep=want_checks)
     kept = info.pop("renderer", None)
     samples_per_step = cfg.width * cfg.height * spp
     value = samples_per_step * args.steps / elapsed / 1e6
-    ref_check = None
-    if want_ref:
+    ref_check = acc_check = host_check = None
+    rsteps = min(args.steps, 3)
+    if want_checks:
+        # izpi_gpu_render's form: the canvas back in host memory, as the Go shim's Render
+        # returns it (renderer.go:26-28); the timed frames above leave it in device memory
+        h_elapsed, h_agg, _, _ = timed(args.bvh, rsteps, 0, reuse=kept, retree=False, host_canvas=True)
+        host_check = {"value": round(samples_per_step * rsteps / h_elapsed / 1e6, 3),
+                      "ms_per_step": round(h_elapsed / rsteps * 1e3, 3), "steps": rsteps}
+    if want_checks and acc_main == N.ACC_FORWARD:
+        # The same frame through the recursion (IZPI_ACC_RECURSIVE, bit-identical to the CPU
+        # oracle), on the same tree and context: the forward form only counts if it is within
+        # north_star's tolerance of it (pixel RMSE < 1e-6) with NaN / Inf on the same pixels.
+        a_elapsed, a_agg, a_img, a_info = timed(args.bvh, rsteps, 1, reuse=kept, acc=N.ACC_RECURSIVE, retree=False)
+        fin = np.isfinite(img) & np.isfinite(a_img)
+        rmse = float(np.sqrt(np.mean((img[fin] - a_img[fin]) ** 2))) if fin.any() else 0.0
+        rel = np.abs(img[fin] - a_img[fin]) / np.maximum(np.abs(a_img[fin]), 1e-300)
+        same_special = bool(np.array_equal(np.isnan(img), np.isnan(a_img)) and
+                            np.array_equal(np.isinf(img) & (img > 0), np.isinf(a_img) & (a_img > 0)) and
+                            np.array_equal(np.isinf(img) & (img < 0), np.isinf(a_img) & (a_img < 0)))
+        a_value = samples_per_step * rsteps / a_elapsed / 1e6
+        counters_equal = all(a_agg[k] / rsteps == agg[k] / args.steps for k in
+                             ("rays", "node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests"))
+        acc_check = {"accumulation": "recursive", "value": round(a_value, 3),
+                     "ms_per_step": round(a_elapsed / rsteps * 1e3, 3), "steps": rsteps,
+                     "image_rmse": rmse, "image_max_rel_err": float(rel.max()) if rel.size else 0.0,
+                     "image_bitwise_equal": img.tobytes() == a_img.tobytes(),
+                     "nan_inf_positions_equal": same_special, "counters_equal": bool(counters_equal),
+                     "trace_ms_per_step": a_agg["kernel_ms"] / rsteps, "shade_ms_per_step": a_agg["shade_ms"] / rsteps,
+                     "first_frame_ms": a_info["first_frame_ms"], "hbm_workspace_gb": round(a_info["workspace_gb"], 2)}
+        if not (rmse < 1e-6 and same_special and counters_equal):
+            print("WARNING: forward accumulation differs from the recursion beyond north_star's tolerance (rmse %g); "
+                  "reporting the recursion" % rmse, file=sys.stderr)
+            elapsed, agg, img = a_elapsed * args.steps / rsteps, a_agg, a_img
+            for k in agg:
+                agg[k] *= args.steps / rsteps
+            value = a_value
+            args.accumulation = "recursive"
+            acc_main = N.ACC_RECURSIVE
+    if want_checks and args.bvh == "gpu":
         # The same frame on hitable.NewBVH4's own tree (rebuilt bit for bit on the host):
         # the GPU-built tree only counts if its image is the reference tree's image. Same
-        # context and render buffers as the timed frames.
-        rsteps = min(args.steps, 3)
+        # context, render buffers and accumulation as the timed frames.
         r_elapsed, r_agg, r_img, r_info = timed("reference", rsteps, 1, reuse=kept)
-        kept.close()
         equal = img.tobytes() == r_img.tobytes()
         rmse = float(np.sqrt(np.mean((img - r_img) ** 2)))
         ref_value = samples_per_step * rsteps / r_elapsed / 1e6
@@ -481,6 +531,8 @@ def main():
                 agg[k] *= args.steps / rsteps
             value = ref_value
             args.bvh = "reference"
+    if kept is not None:
+        kept.close()
 
     # dominant kernel: k_trace2 (the traversals k_tail runs at the end of the frame are counted apart)
     steps = args.steps
@@ -557,6 +609,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        # a fresh renderer's first frame, workspace allocation included: what izpi's leader
+        # sees, which renders one frame per process (leader.go:155-158, renderer.go:170,213)
+        "first_frame_msamples": round(samples_per_step / (info["first_frame_ms"] * 1e-3) / 1e6, 3)
+        if info.get("first_frame_ms") else None,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -564,7 +620,8 @@ def main():
         "data": "synthetic (deterministic Cornell box + 817k-triangle displaced cube-sphere dragon)",
         "config": {"workload": cfg.name, "width": cfg.width, "height": cfg.height, "spp": spp,
                    "max_depth": cfg.max_depth, "triangles": info["triangles"],
-                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "bvh_leaf_max": info["leaf_max"], "parallelism": "tiles%d" % n_gpus, "mode": mode,
+                   "bvh4_nodes": info["nodes"], "bvh": args.bvh, "bvh_leaf_max": info["leaf_max"],
+                   "accumulation": args.accumulation, "parallelism": "tiles%d" % n_gpus, "mode": mode,
                    "samples_per_step": samples_per_step},
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -593,6 +650,8 @@ def main():
             "scene_gen_s": round(scene_s, 2),
             "bvh_build_ms": info["build_ms"],
             "reference_tree": ref_check,
+            "accumulation_check": acc_check,
+            "host_canvas": host_check,
             "image_mean_rgb": [float(x) for x in img[1:, :, :3].mean(axis=(0, 1))] if img is not None else None,
         },
     }

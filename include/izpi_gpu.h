@@ -108,8 +108,7 @@ enum {
   IZPI_TUNE_NO_LDS_BVH = 64,      /* small scenes: traverse from global memory, not the per-block LDS copy */
   IZPI_TUNE_NO_RAY_LDS = 128,     /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
   IZPI_TUNE_NO_PRIM_LDS = 256,    /* small scenes: shading reads the primitives' records from global memory, not the per-block LDS copy */
-  IZPI_TUNE_NO_PLACE_PICK = 512   /* keep the record array's first allocation: no probe of alternative pages (done when
-                                     the records take >= 4 GB: 3 candidates if a chunk's samples all fit the slots, else 2) */
+  IZPI_TUNE_NO_PLACE_PICK = 512   /* ignored since ABI 3 (the record arrays' page pick of ABI 2 is gone) */
 };
 
 typedef struct izpi_render_req {
@@ -126,12 +125,27 @@ typedef struct izpi_render_req {
   double background[3];       /* Colour background (leader.go:140: black) */
   uint64_t seed;              /* master seed of the per-sample LCG streams */
   uint32_t post;              /* IZPI_POST_*: post-processing of a whole-frame IZPI_OUT_CANVAS render */
-  uint32_t abi_version;       /* IZPI_ABI_VERSION (2); 0 = a request laid out by ABI 1 (this field was padding):
+  uint32_t abi_version;       /* IZPI_ABI_VERSION (3); 0 = a request laid out by ABI 1 (this field was padding):
                                  its tuning, when set, is read as ABI 1's izpi_render_tuning, which ended at
-                                 tail_paths; the later fields keep their defaults */
+                                 tail_paths; the later fields keep their defaults. A request of ABI 1 or 2
+                                 ends at `tuning`: it renders IZPI_ACC_RECURSIVE */
   double exposure;            /* XYZToRGB exposure (Scene.Exposure = camera exposure) */
   const izpi_render_tuning* tuning; /* NULL = defaults */
+  uint32_t accumulation;      /* IZPI_ACC_* (ABI 3) */
+  uint32_t pad_req;
 } izpi_render_req;
+
+/* How a path's radiance is summed (izpi_render_req.accumulation). Both trace the same
+ * rays with the same random draws, so every counter is the same.
+ *  IZPI_ACC_RECURSIVE: the recursion of Colour.Sample / SampleSpectral (colour.go:44-57,
+ *    sampler/spectral.go:60-72) unwound from the deepest bounce, in its operation order:
+ *    bit-identical to the CPU restatement. The default.
+ *  IZPI_ACC_FORWARD: the path's throughput is carried forward, T = (T * att) * (s / p) per
+ *    non-specular bounce and T *= att per specular one, and the sample is T * (terminal
+ *    radiance). Only the rounding differs (a few ulp per bounce; pixel RMSE < 1e-6, the
+ *    north star's contract); NaN and Inf land where the recursion puts them (DESIGN.md
+ *    section 3.2). No per-bounce records: a smaller, faster workspace. */
+enum { IZPI_ACC_RECURSIVE = 0, IZPI_ACC_FORWARD = 1 };
 
 /* Post-processing applied by Render for the Spectral sampler (renderer.go:215-219):
  * spectral.FireflyRejection (firefly_rejection.go:12-113) then spectral.XYZToRGB
@@ -291,28 +305,6 @@ int izpi_gpu_render_rank(izpi_ctx* ctx, const izpi_render_req* req, double* out_
  * form sums the contexts of `m` (their shares of one frame). */
 int izpi_gpu_progress(izpi_ctx* ctx, uint64_t* samples_done, uint64_t* samples_total);
 int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* samples_total);
-
-/* Test hook (fault injection): where = 1 makes izpi_gpu_render_rank fail this rank's local
- * checks, 2 makes every render on this context fail as a device fault would, 3 makes this
- * rank's stream stall before the gather as a rank waiting on a dead peer does (released
- * once the call has given up on it), 4 makes izpi_gpu_render_rank's collective waits see a
- * failed stream (a sticky device error): the rank aborts its communicator and returns
- * IZPI_ERR_PEER; 0 = off. */
-int izpi_gpu_debug_fault(izpi_ctx* ctx, int where);
-
-/* Measurement hook: re-allocate the render workspace buffers selected by `mask` (bit 0
- * per-sample results, 1 unwinding records, 2 overflow record blocks, 3 their free rings,
- * 4 running sums, 5 wavefront state, 6 traversal-stack spill) on other pages: each new
- * buffer is allocated while the old one is still held, then the old one is freed. The
- * contents are not kept (every render rewrites them). */
-int izpi_gpu_debug_realloc(izpi_ctx* ctx, uint32_t mask);
-
-/* Measurement hook: time (best of 2 launches, ms) a probe kernel over the current workspace
- * that mixes a streamed 16-B read-modify-write of the first `state_gb` GB of the wavefront
- * state with one random 24-B write into the unwinding records per piece, as a shading pass
- * does (state_gb < 0: |state_gb| GB taken as 64-KB runs spread over the whole state).
- * Overwrites both (scratch between renders). Needs a workspace (one render first). */
-int izpi_gpu_debug_place_probe(izpi_ctx* ctx, double state_gb, float* ms);
 
 /* Bytes of device output izpi_gpu_render_device writes for `req`. */
 uint64_t izpi_gpu_output_bytes(const izpi_render_req* req);

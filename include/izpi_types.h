@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define IZPI_ABI_VERSION 2u
+#define IZPI_ABI_VERSION 3u
 
 /* ---- status codes (0 = OK) ------------------------------------------------ */
 enum {

@@ -17,7 +17,8 @@ c_float_p = C.POINTER(C.c_float)
 # ---- include/izpi_types.h
 COMM_ID_BYTES = 128
 IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE, IZPI_ERR_PEER = range(7)
-IZPI_ABI_VERSION = 2
+IZPI_ABI_VERSION = 3
+ACC_RECURSIVE, ACC_FORWARD = 0, 1
 PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
 TEX_CONSTANT, TEX_IMAGE, TEX_SPECTRAL_GAUSSIAN, TEX_SPECTRAL_TABULATED, TEX_SPECTRAL_IMAGE = 1, 3, 5, 7, 9
 MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC, MAT_LAMBERT, MAT_METAL, MAT_PBR = 1, 2, 3, 4, 5, 6
@@ -110,7 +111,7 @@ class RenderReq(C.Structure):
                 ("num_bg_spd", C.c_uint32), ("tiles", c_uint32_p), ("bg_spd_wavelengths", c_double_p),
                 ("bg_spd_values", c_double_p), ("background", C.c_double * 3), ("seed", C.c_uint64),
                 ("post", C.c_uint32), ("abi_version", C.c_uint32), ("exposure", C.c_double),
-                ("tuning", C.POINTER(RenderTuning))]
+                ("tuning", C.POINTER(RenderTuning)), ("accumulation", C.c_uint32), ("pad_req", C.c_uint32)]
 
 
 class RenderStats(C.Structure):
@@ -201,7 +202,7 @@ EXPORTS = [
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
     "izpi_gpu_build_bvh4", "izpi_gpu_multi_open", "izpi_gpu_multi_close", "izpi_gpu_multi_last_error",
     "izpi_gpu_multi_size", "izpi_gpu_multi_context", "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render",
-    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_gpu_debug_realloc", "izpi_gpu_debug_place_probe", "izpi_gpu_progress", "izpi_gpu_multi_progress", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
+    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_gpu_debug_realloc", "izpi_gpu_progress", "izpi_gpu_multi_progress", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_share_block", "izpi_host_assemble_shares", "izpi_host_bvh_leaf_max", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_serialize", "izpi_scene_info", "izpi_scene_image_file",
@@ -260,7 +261,6 @@ def lib():
     L.izpi_gpu_render_rank.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
     L.izpi_gpu_debug_fault.argtypes = [C.c_void_p, C.c_int]
     L.izpi_gpu_debug_realloc.argtypes = [C.c_void_p, C.c_uint32]
-    L.izpi_gpu_debug_place_probe.argtypes = [C.c_void_p, C.c_double, C.POINTER(C.c_float)]
     L.izpi_gpu_progress.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.izpi_gpu_multi_progress.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]

@@ -34,6 +34,7 @@
 #include <thread>
 
 #include "../../include/izpi_host.h"
+#include "../../include/izpi_gpu_debug.h"
 #include "izpi_dev.h"
 #include "cie_tables.h"
 
@@ -554,6 +555,7 @@ IZPI_DEV int32_t hit_prim(double2 h) { return (int32_t)__double2loint(h.y); }
 struct PathSt {               // register form
   double lambda, lpdf;        // wavelength and its pdf (spectral)
   double pend[3];             // dielectric hit point while its path-length ray is traced
+  double thr[3];              // IZPI_ACC_FORWARD: the path's throughput (Spectral: thr[0])
   uint32_t rng, depth, unit, rslot, blk;
   uint32_t zf;                // ZF_*: what unwinding its records does to a zero radiance (finish)
 };
@@ -585,6 +587,8 @@ struct WaveBuf {
   double2* huv;       // (u, v) of the hit, entry i at huv[i * hs]; null when nothing reads it (WaveParams::hit_uv == 0)
   uint32_t hs;        // 1: hit alone (16-B stride); 2: hit and (u, v) interleaved (huv = hit + 1), one 32-B record per entry
   const double2* tminmax;  // izpi_gpu_trace only: per-entry (tMin, tMax) instead of the kind's
+  double* thr;        // IZPI_ACC_FORWARD: the throughput, component c of entry i at thr[c * tplane + i]; else null
+  uint32_t tplane;
 };
 struct WaveParams {
   WaveBuf in, out;
@@ -1836,6 +1840,25 @@ IZPI_DEV bool finish_reads(const PathSt& P, V3 L) {
   return P.depth > 0;
 }
 
+// IZPI_ACC_FORWARD: the finished path's sample is its throughput times the terminal
+// radiance L (Colour: DeNAN per sample, rgb.go:36; Spectral: the XYZ weights of
+// render/spectral.go:92-96), with no records to read.
+template <int SAMPLER>
+IZPI_DEV void finish_fwd(const ShadeParams& sp, const PathSt& P, V3 L) {
+  double* out = sample_out(sp, P.unit);
+  if (SAMPLER == IZPI_SAMPLER_COLOUR) {
+    const V3 c = denan(mk(P.thr[0] * L.x, P.thr[1] * L.y, P.thr[2] * L.z));
+    sst(out, c.x); sst(out + 1, c.y); sst(out + 2, c.z);
+  } else {
+    const double r = P.thr[0] * L.x;
+    double cx, cy, cz;
+    if (sp.staged) cie_values<true>(P.lambda, cx, cy, cz);
+    else cie_values<false>(P.lambda, cx, cy, cz);
+    const V3 o = sdiv(mk(r * cx, r * cy, r * cz), P.lpdf);
+    sst(out, o.x); sst(out + 1, o.y); sst(out + 2, o.z);
+  }
+}
+
 // The background SPD at lambda (sampler/spectral.go:48-51,79), staged or not
 IZPI_DEV double bg_value(const ShadeParams& sp, double lambda) {
   if (sp.staged) return spd_value<true>(bg_lds(), bgv_lds(), sp.num_bg_spd, lambda, sp.bg_sorted != 0);
@@ -1869,6 +1892,7 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
   P.blk = 0;
   P.lambda = 0;
   P.lpdf = 1;
+  P.thr[0] = 1.0; P.thr[1] = 1.0; P.thr[2] = 1.0;
   if (SAMPLER == IZPI_SAMPLER_SPECTRAL) {
     const double r = rng.next();
     if (sp.staged) sample_wavelength<true>(r, P.lambda, P.lpdf);
@@ -1911,8 +1935,12 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
 // A path's state into entry `pos` of buffer `b` (coalesced: the writing wave's entries
 // are consecutive). The cold record carries the wavelength (spectral) and, for a
 // path-length ray, the dielectric hit point.
-template <int SAMPLER>
+template <int SAMPLER, bool FWD>
 IZPI_DEV void store_entry(const WaveBuf& b, uint32_t pos, const PathSt& P, const RayRec& R) {
+  if constexpr (FWD) {  // one plane per component: every store a coalesced 8 B per lane
+    sst(b.thr + pos, P.thr[0]);
+    if (SAMPLER == IZPI_SAMPLER_COLOUR) { sst(b.thr + b.tplane + pos, P.thr[1]); sst(b.thr + 2 * (size_t)b.tplane + pos, P.thr[2]); }
+  }
   double2* r = reinterpret_cast<double2*>(b.ray + pos);
   sst(r, make_double2(R.o[0], R.o[1]));
   sst(r + 1, make_double2(R.o[2], R.d[0]));
@@ -1941,6 +1969,7 @@ IZPI_DEV void copy_entry(const WaveBuf& in, uint32_t i, const WaveBuf& out, uint
   if (in.cold) out.cold[pos] = in.cold[i];
   out.hit[(size_t)pos * out.hs] = in.hit[(size_t)i * in.hs];
   if (in.huv) out.huv[(size_t)pos * out.hs] = in.huv[(size_t)i * in.hs];
+  // (no throughput: only a render with overflow record blocks parks, and IZPI_ACC_FORWARD has none)
 }
 // The path state of entry i (the ray and hit are read by shade_item).
 // What a shading pass reads of entry i besides its path state: the traced ray, the first
@@ -1955,8 +1984,12 @@ IZPI_DEV void load_entry(const WaveBuf& b, uint32_t i, EntryIn& E) {
   E.hit = sld(b.hit + (size_t)i * b.hs);
   E.time = b.time ? sld(b.time + i) : 0.0;
 }
-template <int SAMPLER>
+template <int SAMPLER, bool FWD>
 IZPI_DEV void load_path(const WaveBuf& b, uint32_t i, PathSt& P) {
+  if constexpr (FWD) {
+    P.thr[0] = sld(b.thr + i);
+    if (SAMPLER == IZPI_SAMPLER_COLOUR) { P.thr[1] = sld(b.thr + b.tplane + i); P.thr[2] = sld(b.thr + 2 * (size_t)b.tplane + i); }
+  }
   const PathHot ph = sld(b.path + i);
   P.rng = ph.rng; P.depth = ph.depth & 0xFFFFu; P.zf = ph.depth >> 16; P.unit = ph.unit; P.rslot = ph.rslot;
   P.blk = b.blk ? sld(b.blk + i) : 0u;
@@ -1981,7 +2014,7 @@ IZPI_DEV uint32_t grab_unit(const ShadeParams& sp, bool want) {
 // starts the unit head at min(slots, units), so no atomic is needed: one counter word
 // serialises ~88 atomics/us), then further units from the head while its path needs no
 // tracing; the path goes to entry j of `out`.
-template <int SAMPLER>
+template <int SAMPLER, bool FWD>
 __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadeParams sp_in, const WaveParams wp) {
   ShadeParams sp = sp_in;
   sp.staged = 0;  // k_start stages no tables: its path starts read them from global memory
@@ -2018,7 +2051,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
   // the first shading pass drops.
   const uint32_t fill = min(sp.slots, sp.total_units);
   if (j < fill) {
-    if (push) store_entry<SAMPLER>(wp.out, j, P, R);
+    if (push) store_entry<SAMPLER, FWD>(wp.out, j, P, R);
     else dead_entry(wp.out, j);
   }
   if (j == 0) *wp.out_count = fill;
@@ -2134,7 +2167,7 @@ IZPI_DEV void block_reserve2(const ShadeParams& sp, uint32_t* out_count, bool pu
 // unit's path in the finished path's record slot and store it; when its sample completes
 // without a ray, take further units one at a time (rare), and leave a dead entry when
 // none traces.
-template <int SAMPLER>
+template <int SAMPLER, bool FWD>
 IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBuf& out, uint32_t unit, uint32_t pos,
                          PathSt& P) {
   RayRec R;
@@ -2144,7 +2177,7 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
 #endif
   for (;;) {
     if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
-      store_entry<SAMPLER>(out, pos, P, R);
+      store_entry<SAMPLER, FWD>(out, pos, P, R);
       return;
     }
     unit = atomicAdd(sp.head, 1u);
@@ -2177,7 +2210,7 @@ IZPI_DEV double path_length(V3 hp, V3 exit_p) {
 // (Spectral: R.o[0]) for the caller's queue (fin_queue), and the caller frees its block
 // after the unwinding. (Spectral queues every finished path: the test cost the Spectral
 // instances up to 24 more spilled VGPRs, C5 shade 320 -> 352 ms.)
-template <int SAMPLER, int MATSET, bool DEFER = false>
+template <int SAMPLER, int MATSET, bool DEFER, bool FWD>
 IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBuf& in, uint32_t i, uint32_t kind,
                          const EntryIn& E, PathSt& P, RayRec& R, bool& push, bool& done, uint32_t& fblk, uint32_t& c_lt,
                          uint32_t& c_ls, bool& queued) {
@@ -2362,7 +2395,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
   if (!push) {
     if (terminal) {
       SCLK_T(sc1);
-      if constexpr (DEFER && !COLOUR) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; }
+      if constexpr (FWD) finish_fwd<SAMPLER>(sp, P, L);
+      else if constexpr (DEFER && !COLOUR) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; }
       else if (DEFER && finish_reads<SAMPLER, MATSET>(P, L)) { R.o[0] = L.x; R.o[1] = L.y; R.o[2] = L.z; queued = true; }
       else finish<SAMPLER, MATSET>(sp, P, L);
       SCLK_ADD(SCLK_FIN, sc1);
@@ -2383,16 +2417,27 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         double sc_cos = dot(hit_n, ud);  // ScatteringPDF with the hit normal
         if (sc_cos < 0) sc_cos = 0;
         const double spdf = zero_spdf ? 0.0 : sc_cos / 3.141592653589793;  // Isotropic.ScatteringPDF is 0
-        rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, spdf, rec_mat);
+        if constexpr (FWD) {  // T * att now (frees T and att during the light-pdf loop), * (s / p) after it
+          P.thr[0] = P.thr[0] * att.x;
+          if (COLOUR) { P.thr[1] = P.thr[1] * att.y; P.thr[2] = P.thr[2] * att.z; }
+        } else {
+          rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, false, att, spdf, rec_mat);
+        }
         SCLK_T(sc3);
         const double pdf_val = 0.5 * lights_pdf(sc, st, next_o, dir, c_lt, c_ls) + 0.5 * cos_pdf;
         SCLK_ADD(SCLK_LPDF, sc3);
-#ifdef IZPI_EXP_NOREC
-        if (P.depth >= IZPI_EXP_NOREC)
-#endif
-        sst(rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth) + RecLayout<SAMPLER, MATSET>::P, pdf_val);
-        if constexpr (ms_spec(MATSET) || SAMPLER == IZPI_SAMPLER_SPECTRAL) rec_zero_track<SAMPLER>(P.zf, false, att, spdf, pdf_val);
+        if constexpr (FWD) {
+          const double w = spdf / pdf_val;
+          P.thr[0] = P.thr[0] * w;
+          if (COLOUR) { P.thr[1] = P.thr[1] * w; P.thr[2] = P.thr[2] * w; }
+        } else {
+          sst(rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth) + RecLayout<SAMPLER, MATSET>::P, pdf_val);
+          if constexpr (ms_spec(MATSET) || SAMPLER == IZPI_SAMPLER_SPECTRAL) rec_zero_track<SAMPLER>(P.zf, false, att, spdf, pdf_val);
+        }
         next_d = dir;
+      } else if constexpr (FWD) {
+        P.thr[0] = P.thr[0] * att.x;
+        if (COLOUR) { P.thr[1] = P.thr[1] * att.y; P.thr[2] = P.thr[2] * att.z; }
       } else {
         rec_store<SAMPLER, MATSET>(sp, P.rslot, P.blk, P.depth, true, att, 0, rec_mat);
         rec_zero_track<SAMPLER>(P.zf, true, att, 0.0, 0.0);
@@ -2402,7 +2447,8 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
       P.rng = rng.s;
       if (P.depth >= sp.max_depth) {
         const V3 Lt = terminal_max_depth(sp, P, COLOUR);
-        if constexpr (DEFER && !COLOUR) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; }
+        if constexpr (FWD) finish_fwd<SAMPLER>(sp, P, Lt);
+        else if constexpr (DEFER && !COLOUR) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; }
         else if (DEFER && finish_reads<SAMPLER, MATSET>(P, Lt)) { R.o[0] = Lt.x; R.o[1] = Lt.y; R.o[2] = Lt.z; queued = true; }
         else finish<SAMPLER, MATSET>(sp, P, Lt);
         done = true;
@@ -2521,7 +2567,7 @@ IZPI_DEV void fin_flush(const ShadeParams& sp, const unsigned long long* q, uint
 #ifndef IZPI_SHADE_WPE_OTHER
 #define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
 #endif
-template <int SAMPLER, int MATSET>
+template <int SAMPLER, int MATSET, bool FWD>
 __global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
                                                                                               : IZPI_SHADE_WPE_OTHER)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
@@ -2533,7 +2579,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * SHADE_THREADS;
-  constexpr bool DEFER = IZPI_FIN_DEFER == 2 || (IZPI_FIN_DEFER == 1 && (SAMPLER == IZPI_SAMPLER_SPECTRAL || ms_spec(MATSET)));
+  constexpr bool DEFER = !FWD && (IZPI_FIN_DEFER == 2 || (IZPI_FIN_DEFER == 1 && (SAMPLER == IZPI_SAMPLER_SPECTRAL || ms_spec(MATSET))));
   constexpr bool COLOUR_DEFER = DEFER && SAMPLER == IZPI_SAMPLER_COLOUR;  // a subset of the finished paths is queued
   unsigned long long* fq = sp.finq + (size_t)blockIdx.x * FINQ_WORDS * FINQ_CAP;
   uint32_t fq_n = 0;  // jobs in this block's queue (the same in every thread)
@@ -2562,7 +2608,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       // path and hit are read too, and ignored): waiting for the kind word first, then the
       // path, then the ray put three memory round trips in front of every item
       kind = sld(wp.in.kind + i) & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
-      load_path<SAMPLER>(wp.in, i, P);
+      load_path<SAMPLER, FWD>(wp.in, i, P);
       load_entry(wp.in, i, E);
     }
     const bool live = valid && !(kind & RAY_DEAD);
@@ -2574,7 +2620,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       c_park += parked ? 1u : 0u;
     }
     bool queued = false;    // (DEFER) its unwinding waits in the block's queue
-    if (live && !parked) shade_item<SAMPLER, MATSET, DEFER>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls, queued);
+    if (live && !parked) shade_item<SAMPLER, MATSET, DEFER, FWD>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls, queued);
     if (SAMPLER == IZPI_SAMPLER_SPECTRAL) queued = DEFER && done;  // (every finished path)
     // a queued path's overflow block is freed after its unwinding (fin_flush)
     if ((COLOUR_DEFER ? !queued : !DEFER) && sp.rec_pool && fblk) pool_free_one(sp, fblk);
@@ -2589,14 +2635,14 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     block_reserve2<COLOUR_DEFER>(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, queued, frank, ftotal);
     if (queued) fin_queue<SAMPLER>(fq, fq_n + frank, P, R);  // (before refill_one reuses P)
     fq_n += ftotal;
-    if (push) store_entry<SAMPLER>(wp.out, pos, P, R);
+    if (push) store_entry<SAMPLER, FWD>(wp.out, pos, P, R);
     if (parked) copy_entry(wp.in, i, wp.out, pos);
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
     k_push += t1 - t0;
     t0 = t1;
 #endif
-    if (unit != 0xFFFFFFFFu) refill_one<SAMPLER>(sc, sp, wp.out, unit, pos, P);
+    if (unit != 0xFFFFFFFFu) refill_one<SAMPLER, FWD>(sc, sp, wp.out, unit, pos, P);
     else if (done && pos != 0xFFFFFFFFu) dead_entry(wp.out, pos);  // entry reserved, the units ran out
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
@@ -2636,7 +2682,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 // k_tail instead runs each remaining path to its end in one lane: trace, shade, trace...
 // (no refill: the unit head is exhausted), so the passes of different paths overlap.
 // Same per-ray code paths, results and counters as k_trace + k_shade.
-template <int SAMPLER, int MATSET, int STACK>
+template <int SAMPLER, int MATSET, int STACK, bool FWD>
 __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadeParams sp, const WaveParams wp, int32_t* spill) {
   shade_stage(sc, sp);
   __shared__ int32_t lds_stack[std::min(STACK, TAIL_LDS_STACK) * 256];
@@ -2654,7 +2700,7 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
       traced = false;
       PathSt P;
       RayRec R;
-      load_path<SAMPLER>(wp.in, i, P);
+      load_path<SAMPLER, FWD>(wp.in, i, P);
       const uint32_t kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;
       if (sp.rec_pool && P.depth >= sp.rec_dense && P.blk == 0) {
         // The host launches k_tail with at most pool blocks paths, all of the free
@@ -2667,10 +2713,10 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
       EntryIn E;
       load_entry(wp.in, i, E);
       bool queued = false;  // (k_tail unwinds in place)
-      shade_item<SAMPLER, MATSET>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls, queued);
+      shade_item<SAMPLER, MATSET, false, FWD>(sc, sp, wp.in, i, kind, E, P, R, push, done, fblk, c_lt, c_ls, queued);
       if (fblk) pool_free_one(sp, fblk);
       if (!push) break;
-      store_entry<SAMPLER>(wp.in, i, P, R);
+      store_entry<SAMPLER, FWD>(wp.in, i, P, R);
     }
   }
   const uint32_t lane = threadIdx.x & 63;
@@ -3050,8 +3096,7 @@ struct izpi_ctx {
   uint32_t* d_misc = nullptr;              // words k * MISC_STRIDE (misc()): 0 unit head, 1 error, 2 trace cursor, 3..4 queue counts, 6..7 park flags
   unsigned long long* d_counters = nullptr;
   unsigned long long* d_cpart = nullptr; size_t cpart_cap = 0;  // per-wave counter rows of a render (count_add)
-  unsigned long long* d_finq = nullptr; size_t finq_cap = 0;
-  float place_ms[2] = {0, 0}; int place_pick[2] = {-1, -1};  // pick_pages (records, state): the kept candidate and its probe time  // k_shade blocks' deferred unwinding jobs (fin_flush)
+  unsigned long long* d_finq = nullptr; size_t finq_cap = 0;  // k_shade blocks' deferred unwinding jobs (fin_flush)
   char* d_state = nullptr; size_t state_cap = 0;      // the two WaveBufs (carve_state)
   int32_t* d_spill = nullptr; size_t spill_cap = 0;  // traversal-stack spill area of k_trace2
   double* d_post = nullptr; size_t post_cap = 0;      // spectral post-processing output
@@ -3138,6 +3183,13 @@ struct RenderBuf {
 // Make every buffer of `b` at least its `bytes`: if any must grow, free them all first,
 // then allocate each at exactly its size.
 int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n, bool* fresh) {
+  for (size_t i = 0; i < n; i++)  // a buffer this render does not use (the records of IZPI_ACC_FORWARD)
+    if (b[i].bytes == 0 && *b[i].p) {
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+      HIP_TRY(hipFree(*b[i].p));
+      *b[i].p = nullptr;
+      *b[i].cap = 0;
+    }
   bool must = false;
   for (size_t i = 0; i < n; i++) must = must || *b[i].cap < b[i].bytes;
   *fresh = must;
@@ -3161,115 +3213,9 @@ int grow_render_buffers(izpi_ctx* ctx, RenderBuf* b, size_t n, bool* fresh) {
   return IZPI_OK;
 }
 
-// Placement probe over the current workspace (shading-time modes): a streamed
-// 16-B read-modify-write of the first `n16` pieces of the state with, per piece, one random
-// 24-B record written into the record array, as a shading pass mixes them. The contents
-// of both arrays are scratch between renders (k_start and the shading passes write before
-// they read).
-// bstride != 0: the n16 pieces are taken as 64-KB runs spread over the whole state (run k
-// at k * bstride pieces) instead of one contiguous range.
-__global__ void __launch_bounds__(256) k_place_probe(uint4* s, uint64_t n16, double* r, uint64_t nrec, uint64_t seed,
-                                                     uint64_t bstride) {
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += stride) {
-    const uint64_t a = bstride ? (i >> 12) * bstride + (i & 4095u) : i;
-    uint4 v = s[a];
-    v.x += 1u;
-    s[a] = v;
-    uint64_t h = seed ^ (i * 0x9E3779B97F4A7C15ull);
-    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
-    double* q = r + (h % nrec) * 3;
-    q[0] = (double)v.y; q[1] = 0.0; q[2] = 1.0;
-  }
-}
-
-
-// One timing of k_place_probe over `gb` GB of the state and the record array `recs`:
-// the better of two launches, ms.
-float place_probe_ms(izpi_ctx* ctx, char* state, double* recs, double gb, bool spread = false) {
-  const uint64_t total16 = ctx->state_cap / 16;
-  uint64_t n16 = std::min<uint64_t>(total16, (uint64_t)(gb * 1e9) / 16);
-  uint64_t bstride = 0;
-  if (spread && n16 >= 4096 && total16 > n16) {
-    n16 &= ~(uint64_t)4095;
-    bstride = (total16 / (n16 >> 12)) & ~(uint64_t)4095;  // >= 4096: the runs do not overlap
-  }
-  hipStream_t st = ctx->stream;
-  float best = 1e30f;
-  for (int k = 0; k < 2; k++) {
-    if (hipEventRecord(ctx->evb[0], st) != hipSuccess) return 0.0f;
-    hipLaunchKernelGGL(k_place_probe, dim3(ctx->num_cus * 8), dim3(256), 0, st, (uint4*)state, n16, recs,
-                       (uint64_t)(ctx->recs_cap / 24), 77ull + k, bstride);
-    float t = 0;
-    if (hipEventRecord(ctx->evb[1], st) != hipSuccess || hipEventSynchronize(ctx->evb[1]) != hipSuccess ||
-        hipEventElapsedTime(&t, ctx->evb[0], ctx->evb[1]) != hipSuccess)
-      return 0.0f;
-    best = std::min(best, t);
-  }
-  return best;
-}
-
-// Pages for the record array and the wavefront state (shading-time modes).
-// k_shade's time depends on where the driver put the record array and the state (C3 at
-// 128 spp: 25.0 - 31.3 ms of shading for the same frame over re-allocations of the records
-// alone), and a short probe of the same access mix tells the slow placements: the probe's
-// slowest level (~1.35x its fastest) came with 31.3 ms every time
-// (`profiles/r5b/mode_place_recs.jsonl`). At C3's 512 spp the same holds on boxes that
-// show the slow mode: over re-allocations of the records the probe read 3.37-3.41 ms with
-// 113.6-113.8 ms of shading and 3.00-3.10 ms with 104.1-105.7 (`mode_place_512.jsonl`);
-// over re-allocations of the state, with the probe's 1 GB spread over the whole state in
-// 64-KB runs, 3.35-3.39 ms with 109.3-112.9 ms and 3.16-3.20 ms with 103.9-104.2
-// (`mode_place_512_state2.jsonl`). So each fresh buffer of at least 4 GB is probed on up
-// to `candidates` allocations, each new one made while the others are held (other pages),
-// and the fastest is kept: the records first, then the state. Costs ~7 ms per candidate
-// plus the allocations, on workspace allocations only.
-// The state is not picked by default (IZPI_PICK_STATE): its 70-GB candidate cost a first
-// frame 4.6 s of allocation on a box with VRAM to clear, for 106.3 -> 105.6 ms of shading
-// over five process pairs on a box without a slow mode (`ab_pickstate_c3.jsonl`).
-#ifndef IZPI_PICK_STATE
-#define IZPI_PICK_STATE 0
-#endif
-constexpr int PLACE_CANDIDATES = 3;
-int pick_pages(izpi_ctx* ctx, bool state_buf, int candidates) {
-  const size_t cap = state_buf ? ctx->state_cap : ctx->recs_cap;
-  if (cap < (4ull << 30) || !ctx->d_state || !ctx->d_recs) return IZPI_OK;
-  candidates = std::min(candidates, PLACE_CANDIDATES);
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  void* cand[PLACE_CANDIDATES] = {state_buf ? (void*)ctx->d_state : (void*)ctx->d_recs};
-  auto probe = [&](void* p) {
-    return place_probe_ms(ctx, state_buf ? (char*)p : (char*)ctx->d_state, state_buf ? ctx->d_recs : (double*)p, 1.0, true);
-  };
-  int nc = 1, best = 0;
-  float best_ms = probe(cand[0]);
-  for (; nc < candidates; nc++) {
-    size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < cap + (8ull << 30)) break;
-    void* p = nullptr;
-    const auto a0 = std::chrono::steady_clock::now();
-    if (hipMalloc(&p, cap) != hipSuccess) {
-      (void)hipGetLastError();
-      break;
-    }
-    cand[nc] = p;
-    const float t = probe(p);
-    if (t > 0.0f && t < best_ms) { best_ms = t; best = nc; }
-    // an allocation that waited for the driver to clear VRAM (seconds after a large
-    // process): no further candidates, the first frame has paid enough
-    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a0).count() > 50.0) { nc++; break; }
-  }
-  for (int k = 0; k < nc; k++)
-    if (k != best) HIP_TRY(hipFree(cand[k]));
-  if (state_buf) ctx->d_state = (char*)cand[best];
-  else ctx->d_recs = (double*)cand[best];
-  ctx->place_pick[state_buf ? 1 : 0] = best;
-  ctx->place_ms[state_buf ? 1 : 0] = best_ms;
-  HIP_TRY(hipGetLastError());
-  return IZPI_OK;
-}
-
 // The two sides of the wavefront state, `slots` entries each, in one allocation:
 // returns the bytes (base == nullptr) or fills b[0], b[1].
-size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, bool uv, WaveBuf* b) {
+size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, bool uv, uint32_t thr_planes, WaveBuf* b) {
   size_t off = 0;
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
@@ -3293,6 +3239,8 @@ size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, b
     w.hit = (double2*)take((size_t)slots * w.hs * sizeof(double2));
     w.huv = uv && w.hit ? w.hit + 1 : nullptr;
     w.tminmax = nullptr;
+    w.thr = thr_planes ? (double*)take((size_t)slots * thr_planes * sizeof(double)) : nullptr;
+    w.tplane = slots;
     if (b) b[k] = w;
   }
   return off;
@@ -3427,7 +3375,7 @@ uint32_t validate_tiles(const izpi_render_req* req, const uint32_t* tiles, uint3
 // k_shade alternate until no slot has a ray left (the last few paths run to their end
 // in k_tail); k_accumulate folds the chunk's per-sample radiance into the pixels in
 // sample order.
-template <int SAMPLER, int MATSET>
+template <int SAMPLER, int MATSET, bool FWD>
 int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, const Tracer& tr, ShadeParams& sp,
                WaveParams& wp, AccumParams& ap, uint32_t num_pixels, uint32_t chunk, uint32_t pool_blocks,
                float* trace_ms, float* shade_ms, float* tail_ms, uint32_t* launches) {
@@ -3435,13 +3383,13 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
   const izpi_render_tuning& tu = tuning_of(req);
   int shade_res = 0;
   const size_t dyn = sc.lds_bytes;  // the staged tables' LDS arena (render_body)
-  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET>, &shade_res, (int)SHADE_THREADS, dyn);
+  int rc = resident_blocks(ctx, k_shade<SAMPLER, MATSET, FWD>, &shade_res, (int)SHADE_THREADS, dyn);
   if (rc) return rc;
   // tail kernel: used once every unit has started and at most `tail_max` paths remain
   const bool tail_deep = ctx->stack_needed > 32;
   int tail_res = 0;
-  if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64>, &tail_res, 256, dyn)
-                      : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32>, &tail_res, 256, dyn))) return rc;
+  if ((rc = tail_deep ? resident_blocks(ctx, k_tail<SAMPLER, MATSET, 64, FWD>, &tail_res, 256, dyn)
+                      : resident_blocks(ctx, k_tail<SAMPLER, MATSET, 32, FWD>, &tail_res, 256, dyn))) return rc;
   if ((uint32_t)std::max({tr.blocks * 4, shade_res * (int)SHADE_WAVES, tail_res * 4}) > ctx->num_cus * CPART_BLOCKS_PER_CU * 4 ||
       (uint32_t)shade_res > ctx->num_cus * CPART_BLOCKS_PER_CU) {
     ctx->err = "grid larger than the counter rows or the unwinding queues";
@@ -3470,7 +3418,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     HIP_TRY(hipMemsetAsync(misc(ctx, 2), 0, 3 * MISC_STRIDE * sizeof(uint32_t), st));  // dequeue cursor, queue counts
     HIP_TRY(hipMemsetAsync(misc(ctx, 6), 0, 2 * MISC_STRIDE * sizeof(uint32_t), st));  // park flags of the two sides
     wp.out = q[0]; wp.out_count = qn[0];
-    hipLaunchKernelGGL(k_start<SAMPLER>, dim3((fill + 255) / 256), dim3(256), 0, st, sc, sp, wp);
+    hipLaunchKernelGGL((k_start<SAMPLER, FWD>), dim3((fill + 255) / 256), dim3(256), 0, st, sc, sp, wp);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -3495,7 +3443,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         launch_trace(ctx, sc, tr, wp, st, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
-        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET>), dim3(shade_res), dim3(SHADE_THREADS), dyn, st, sc, sp, wp);
+        hipLaunchKernelGGL((k_shade<SAMPLER, MATSET, FWD>), dim3(shade_res), dim3(SHADE_THREADS), dyn, st, sc, sp, wp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
@@ -3526,8 +3474,8 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         if (sp.rec_pool) hipLaunchKernelGGL(k_pool_publish, dim3(1), dim3(256), 0, st, sp.pool_ctr);
         // (the deep instance spills stack entries past 32 into k_trace2's spill area, which
         // holds 64 entries for each of k_trace2's threads, more than k_tail has)
-        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64>), dim3(tail_res), dim3(256), dyn, st, sc, sp, wp, ctx->d_spill);
-        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32>), dim3(tail_res), dim3(256), dyn, st, sc, sp, wp, ctx->d_spill);
+        if (tail_deep) hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 64, FWD>), dim3(tail_res), dim3(256), dyn, st, sc, sp, wp, ctx->d_spill);
+        else hipLaunchKernelGGL((k_tail<SAMPLER, MATSET, 32, FWD>), dim3(tail_res), dim3(256), dyn, st, sc, sp, wp, ctx->d_spill);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev3, st));
         HIP_TRY(hipEventSynchronize(ctx->ev3));
@@ -3603,6 +3551,10 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
   if (req->abi_version > IZPI_ABI_VERSION) { ctx->err = "render request from a newer ABI"; return IZPI_ERR_INVALID; }
   if (req->sampler != IZPI_SAMPLER_COLOUR && req->sampler != IZPI_SAMPLER_SPECTRAL) { ctx->err = "unsupported sampler"; return IZPI_ERR_UNSUPPORTED; }
+  // (a request of ABI 1 or 2 ends at `tuning`: accumulation is not read)
+  const uint32_t acc = req->abi_version >= 3 ? req->accumulation : (uint32_t)IZPI_ACC_RECURSIVE;
+  if (acc != IZPI_ACC_RECURSIVE && acc != IZPI_ACC_FORWARD) { ctx->err = "unknown accumulation mode"; return IZPI_ERR_INVALID; }
+  const bool fwd = acc == IZPI_ACC_FORWARD;
   if (req->post != IZPI_POST_NONE &&
       ((req->post & ~(uint32_t)(IZPI_POST_SPECTRAL | IZPI_POST_GAMMA_CLAMP)) || req->out_layout != IZPI_OUT_CANVAS ||
        req->num_tiles != 0)) {
@@ -3637,7 +3589,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // holds and would release (a later frame reuses them, so every frame of a renderer sizes
   // alike), shared evenly by the contexts of one process on this device.
   const uint64_t size_key[8] = {num_pixels, req->spp, req->sampler, req->max_depth, ctx->pool_grow,
-                                ((uint64_t)tu.slots << 32) | tu.chunk_units, ((uint64_t)tu.rec_dense << 32) | tu.pool_div, 0};
+                                ((uint64_t)tu.slots << 32) | tu.chunk_units, ((uint64_t)tu.rec_dense << 32) | tu.pool_div, acc};
   const bool reuse = ctx->sizing_valid && memcmp(size_key, ctx->sizing.key, sizeof(size_key)) == 0;
   size_t free_b = 0, total_b = 0;
   if (!reuse && hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
@@ -3662,7 +3614,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // Unwinding records: the first rec_dense levels per slot, deeper levels in overflow
   // blocks (ShadeParams::rec_pool). Colour records are 40 B (24 B compact), spectral 24 B.
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
-  const bool compact = !spectral && ctx->basic_materials && ctx->const_albedo;
+  const bool compact = !fwd && !spectral && ctx->basic_materials && ctx->const_albedo;
   const uint32_t D = spectral  ? RecLayout<IZPI_SAMPLER_SPECTRAL, MATSET_FULL>::D
                      : compact ? RecLayout<IZPI_SAMPLER_COLOUR, MATSET_CONST>::D
                                : RecLayout<IZPI_SAMPLER_COLOUR, MATSET_FULL>::D;
@@ -3674,7 +3626,11 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   uint32_t rec_dense = spectral ? 32u : 8u;
   if (tu.rec_dense) rec_dense = tu.rec_dense;
   rec_dense = std::min(rec_dense, max_depth);
+  if (fwd) rec_dense = max_depth;  // (no records at all: see need[] and the pool below)
   const uint32_t rec_pool = max_depth - rec_dense;
+  // IZPI_ACC_FORWARD: the throughput per entry instead of the records (3 planes Colour, 1 Spectral)
+  const uint32_t thr_planes = fwd ? (spectral ? 1u : 3u) : 0u;
+  const uint64_t rec_bytes_slot = fwd ? 0 : (uint64_t)rec_dense * D * sizeof(double);
   // PathCold (wavelength, dielectric point) is read only by the spectral sampler and glass
   const bool need_cold = spectral || !ctx->sc.no_pathlen;
   // a hit's (u, v) array: read by (u, v)-reading textures and, for spheres, the root (A16)
@@ -3688,8 +3644,9 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   uint64_t slot_cap = 256ull << 20;
   if (tu.slots) slot_cap = std::max<uint64_t>(1024, tu.slots);
   const uint64_t per_slot = 2 * (sizeof(RayOD) + sizeof(uint32_t) + (ctx->sc.tri_only ? 0 : sizeof(double)) + sizeof(PathHot) +
-                                 sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(double2) * (need_uv ? 2 : 1)) +
-                            (uint64_t)rec_dense * D * sizeof(double);
+                                 sizeof(uint32_t) + (need_cold ? sizeof(PathCold) : 0) + sizeof(double2) * (need_uv ? 2 : 1) +
+                                 thr_planes * sizeof(double)) +
+                            rec_bytes_slot;
   // Overflow blocks per slot. Lambert/light scenes: 1 per 16 slots (C3: ~3% of the paths
   // in flight are deeper than 8). Scenes with glass or the spectral sampler run deep
   // chains through glass: 1 per 4 slots (C5 at 1 per 16 parked 29% of its
@@ -3729,27 +3686,15 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const auto t_alloc0 = std::chrono::steady_clock::now();
   RenderBuf need[] = {
       {(void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * SMP_D * sizeof(double)},
-      {(void**)&ctx->d_recs, &ctx->recs_cap, (size_t)rec_dense * D * slots * sizeof(double)},
+      {(void**)&ctx->d_recs, &ctx->recs_cap, (size_t)rec_bytes_slot * slots},
       {(void**)&ctx->d_pool, &ctx->pool_cap, rec_pool ? (size_t)pool_blocks * rec_pool * D * sizeof(double) : 0},
       {(void**)&ctx->d_ring, &ctx->ring_cap, rec_pool ? (size_t)pool_blocks * sizeof(uint32_t) : 0},
       {(void**)&ctx->d_running, &ctx->running_cap, (size_t)num_pixels * 3 * sizeof(double)},
-      {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, need_uv, nullptr)},
+      {(void**)&ctx->d_state, &ctx->state_cap, carve_state(nullptr, slots, need_time, rec_pool != 0, need_cold, need_uv, thr_planes, nullptr)},
       {(void**)&ctx->d_spill, &ctx->spill_cap, tr.spill_bytes},
   };
   bool fresh = false;
   if ((rc = grow_render_buffers(ctx, need, sizeof(need) / sizeof(need[0]), &fresh))) {
-    ctx->sizing_valid = false;
-    return rc;
-  }
-  // (three candidates for a chunk whose samples all fit the slots, where every pass after
-  // the first is a pure bounce pass and the modes are widest; two otherwise: each extra
-  // allocation can cost a first frame ~60 ms on a box with VRAM to clear)
-  const bool pure_bounce = (uint64_t)num_pixels * chunk <= slots;
-  // (not when the workspace itself waited for the driver to clear VRAM: more allocations
-  // would wait too)
-  const bool alloc_fast = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count() < 50.0;
-  if (fresh && alloc_fast && !(tuning_of(req).flags & IZPI_TUNE_NO_PLACE_PICK) &&
-      ((rc = pick_pages(ctx, false, pure_bounce ? 3 : 2)) || (IZPI_PICK_STATE && (rc = pick_pages(ctx, true, 2))))) {
     ctx->sizing_valid = false;
     return rc;
   }
@@ -3761,10 +3706,10 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const uint32_t cpart_rows = ctx->num_cus * CPART_BLOCKS_PER_CU * 4u;
   if ((rc = grow(ctx, (void**)&ctx->d_cpart, &ctx->cpart_cap, (size_t)cpart_rows * CNT_N * sizeof(unsigned long long)))) return rc;
   // deferred unwinding jobs: one queue per k_shade block (run_chunks checks its grid against it)
-  if ((rc = grow(ctx, (void**)&ctx->d_finq, &ctx->finq_cap, (size_t)ctx->num_cus * CPART_BLOCKS_PER_CU * FINQ_WORDS * FINQ_CAP * sizeof(unsigned long long)))) return rc;
+  if (!fwd && (rc = grow(ctx, (void**)&ctx->d_finq, &ctx->finq_cap, (size_t)ctx->num_cus * CPART_BLOCKS_PER_CU * FINQ_WORDS * FINQ_CAP * sizeof(unsigned long long)))) return rc;
   const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count();
   WaveBuf bufs[2];
-  carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, need_uv, bufs);
+  carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, need_uv, thr_planes, bufs);
   hipStream_t st = ctx->stream;
   HIP_TRY(hipMemcpyAsync(ctx->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   if (nbg) {
@@ -3787,7 +3732,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.rec_dense = rec_dense; sp.rec_pool = rec_pool;
   sp.pool_shift = 0;
   while (pool_blocks && (POOL_SHARDS << sp.pool_shift) < pool_blocks) sp.pool_shift++;
-  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = misc(ctx, 0);
+  sp.seed = req->seed; sp.out = ctx->d_samples; sp.recs = fwd ? nullptr : ctx->d_recs; sp.mat_const = sc.mat_const; sp.head = misc(ctx, 0);
   sp.num_mc = ctx->num_materials; sp.num_tex = ctx->num_textures; sp.num_spd = ctx->num_spd;
   sp.staged = ctx->num_materials <= MC_LDS && ctx->num_materials <= MAT_LDS && sc.num_lights <= LT_LDS &&
               ctx->num_textures <= TEX_LDS && ctx->num_spd <= SPD_LDS && nbg <= BG_LDS;
@@ -3818,7 +3763,8 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   float trace_ms = 0, shade_ms = 0, tail_ms = 0;
   uint32_t launches = 0;
   HIP_TRY(hipEventRecord(ctx->ev0, st));
-#define IZPI_RUN(S, M) run_chunks<S, M>(ctx, req, sc, tr, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches)
+#define IZPI_RUN(S, M) (fwd ? run_chunks<S, M == MATSET_CONST ? MATSET_BASIC : M, true>(ctx, req, sc, tr, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches) \
+                          : run_chunks<S, M, false>(ctx, req, sc, tr, sp, wp, ap, num_pixels, chunk, pool_blocks, &trace_ms, &shade_ms, &tail_ms, &launches))
   // the smallest compiled material set holding the scene's material kinds
   const uint32_t ms = ctx->matset;
   const int set = ms == 0 ? MATSET_BASIC : (ms & ~(uint32_t)MATSET_SURF) == 0 ? MATSET_SURF : MATSET_FULL;
@@ -3855,7 +3801,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   s.parks = cnt[CNT_PARK];
   s.workspace_bytes = workspace_bytes(ctx);
   s.scene_bytes = ctx->scene_bytes;
-  s.slots = slots; s.rec_dense = rec_dense; s.pool_blocks = pool_blocks; s.chunk_spp = chunk;
+  s.slots = slots; s.rec_dense = fwd ? 0 : rec_dense; s.pool_blocks = pool_blocks; s.chunk_spp = chunk;
   s.alloc_ms = alloc_ms;
   if (rec_pool && s.parks * 64 > s.rays && pool_blocks < slots) ctx->pool_grow++;
 #ifdef IZPI_SHADE_CLOCKS
@@ -4927,17 +4873,6 @@ int izpi_gpu_multi_progress(izpi_multi* m, uint64_t* samples_done, uint64_t* sam
     izpi_gpu_progress(c, &d, &t);
     *samples_done += d; *samples_total += t;
   }
-  return IZPI_OK;
-}
-
-int izpi_gpu_debug_place_probe(izpi_ctx* ctx, double state_gb, float* ms) {
-  if (!ctx || !ms) return IZPI_ERR_INVALID;
-  *ms = 0.0f;
-  if (!ctx->d_state || !ctx->d_recs || ctx->recs_cap < 64) { ctx->err = "no workspace yet (render once first)"; return IZPI_ERR_INVALID; }
-  HIP_TRY(hipSetDevice(ctx->device));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  *ms = place_probe_ms(ctx, (char*)ctx->d_state, ctx->d_recs, std::fabs(state_gb), state_gb < 0);  // (< 0: spread over the whole state)
-  HIP_TRY(hipGetLastError());
   return IZPI_OK;
 }
 

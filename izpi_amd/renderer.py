@@ -62,11 +62,13 @@ def build_bvh4(ctx, boxes, leaf_max=4, method=None):
 
 
 def make_request(width, height, spp, max_depth, sampler, background, seed, exposure, bg_spd=None, tiles=None,
-                 layout=N.OUT_CANVAS, post=N.POST_NONE, tuning=None):
+                 layout=N.OUT_CANVAS, post=N.POST_NONE, tuning=None, accumulation=N.ACC_RECURSIVE):
     """izpi_render_req for Render (the arrays it points to are kept alive on `req._keep`).
-    tuning: an N.RenderTuning (launch settings; None = the library's defaults)."""
+    tuning: an N.RenderTuning (launch settings; None = the library's defaults).
+    accumulation: N.ACC_RECURSIVE (bitwise against the oracle's recursion) or N.ACC_FORWARD."""
     req = N.RenderReq()
     req.abi_version = N.IZPI_ABI_VERSION
+    req.accumulation = accumulation
     req.post = post
     req.exposure = exposure
     req.width, req.height = width, height
@@ -107,12 +109,14 @@ def common_tiles(width, height):
 class GPURenderer:
     def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
                  spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference",
-                 bvh_leaf_max=None, tuning=None):
+                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE):
         """bvh="reference": hitable.NewBVH4's tree, rebuilt bit for bit on the host (the
         parity default); bvh="gpu": the GPU linear BVH4 builder (izpi_gpu_build_bvh4),
         same node format, different topology. tuning: an
-        N.RenderTuning for every request (None = library defaults)."""
+        N.RenderTuning for every request (None = library defaults). accumulation: how a
+        path's radiance is summed (N.ACC_*; the attribute may be changed between frames)."""
         self.tuning = tuning
+        self.accumulation = int(accumulation)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
@@ -168,7 +172,7 @@ class GPURenderer:
     def request(self, tiles=None, layout=N.OUT_CANVAS, spp=None, post=N.POST_NONE):
         return make_request(self.width, self.height, self.spp if spp is None else int(spp), self.max_depth,
                             self.sampler, self.background, self.seed, self.exposure, (self._bg_wl, self._bg_val),
-                            tiles, layout, post, self.tuning)
+                            tiles, layout, post, self.tuning, self.accumulation)
 
     # --------------------------------------------------------------- render
     @property
@@ -283,8 +287,9 @@ class MultiGPURenderer:
 
     def __init__(self, scene, width, height, spp, devices, max_depth=50, sampler=N.SAMPLER_COLOUR,
                  background=(0.0, 0.0, 0.0), spectral_background=None, seed=12345, bvh_seed=12345, bvh="gpu",
-                 bvh_leaf_max=None, tuning=None):
+                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE):
         self.tuning = tuning
+        self.accumulation = int(accumulation)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
@@ -328,7 +333,8 @@ class MultiGPURenderer:
         to_host=False (the canvas stays on device 0: the timing form). self.stats is the
         list of per-device stats."""
         req = make_request(self.width, self.height, self.spp, self.max_depth, self.sampler, self.background,
-                           self.seed, self.exposure, self._bg, None, N.OUT_CANVAS, post, self.tuning)
+                           self.seed, self.exposure, self._bg, None, N.OUT_CANVAS, post, self.tuning,
+                           self.accumulation)
         G = len(self.devices)
         st = (N.RenderStats * G)()
         if to_host and canvas is None:

@@ -1283,6 +1283,37 @@ struct ColourSampler {  // sampler/colour.go
     }
     return background;
   }
+  // The same estimator with the throughput carried forward (IZPI_ACC_FORWARD; a restatement
+  // of the GPU's forward mode, not of izpi): identical rays, draws and counters; the radiance
+  // is T * (terminal radiance) with T = (T * att) * (s / p) per non-specular bounce and T *= att
+  // per specular one. Every scattering material emits 0 (non_emitter.go:12-14,
+  // dielectric.go:219-221), so colour.go:57's `emitted +` adds nothing before the end.
+  Vec3 SampleForward(Ray r, const World& W, LCG& rnd) const {
+    Vec3 T = V(1.0, 1.0, 1.0);
+    for (int depth = 0;; depth++) {
+      if (depth >= maxDepth) return Mul(T, V(0, 0, 1.0));
+      g_cnt.rays++;
+      HitRecord rec; const Material* mat;
+      if (!W.world.Hit(r, 0.001, GO_MAXFLOAT64, rec, mat)) return Mul(T, background);
+      ScatterRecord srec;
+      bool ok = mat->Scatter(r, rec, rnd, srec);
+      Vec3 emitted = mat->Emitted(r, rec, rec.u, rec.v, rec.p);
+      if (!ok) return Mul(T, emitted);
+      if (srec.isSpecular) {
+        T = Mul(T, srec.albedo);
+        r = srec.specularRay;
+        continue;
+      }
+      Vec3 dir;
+      if (rnd.Float64() < 0.5) dir = W.lights.Random(rec.p, rnd);
+      else dir = srec.pdf.Generate(rnd);
+      Ray scattered = NewRay(rec.p, dir, r.time);
+      double pdfVal = 0.5 * W.lights.PDFValue(rec.p, scattered.d) + 0.5 * srec.pdf.Value(scattered.d);
+      const double w = mat->ScatteringPDF(r, rec, scattered) / pdfVal;
+      T = ScalarMul(Mul(T, srec.albedo), w);
+      r = scattered;
+    }
+  }
 };
 
 struct SpectralSampler {  // sampler/spectral.go
@@ -1310,6 +1341,33 @@ struct SpectralSampler {  // sampler/spectral.go
       return emitted;
     }
     return background.Value(r.lambda);
+  }
+  // Forward form of SampleSpectral (see ColourSampler::SampleForward).
+  double SampleSpectralForward(Ray r, const World& W, LCG& rnd) const {
+    double T = 1.0;
+    for (int depth = 0;; depth++) {
+      if (depth >= maxDepth) return T * background.Value(r.lambda);
+      g_cnt.rays++;
+      HitRecord rec; const Material* mat;
+      if (!W.world.Hit(r, 0.001, GO_MAXFLOAT64, rec, mat)) return T * background.Value(r.lambda);
+      SpectralScatterRecord srec;
+      bool ok = mat->SpectralScatter(r, rec, rnd, srec);
+      double emitted = mat->EmittedSpectral(r, rec, rec.u, rec.v, r.lambda, rec.p);
+      if (!ok) return T * emitted;
+      if (srec.isSpecular) {
+        T = T * srec.albedo;
+        r = srec.specularRay;
+        continue;
+      }
+      Vec3 dir;
+      if (rnd.Float64() < 0.5) dir = W.lights.Random(rec.p, rnd);
+      else dir = srec.pdf.Generate(rnd);
+      Ray scattered = NewRayL(rec.p, dir, r.time, r.lambda);
+      double pdfVal = 0.5 * W.lights.PDFValue(rec.p, scattered.d) + 0.5 * srec.pdf.Value(scattered.d);
+      const double w = mat->ScatteringPDF(r, rec, scattered) / pdfVal;
+      T = (T * srec.albedo) * w;
+      r = scattered;
+    }
   }
 };
 
@@ -1859,6 +1917,7 @@ int oracle_render(oracle_scene* s, const izpi_render_req* req, double* canvas, o
     ss.background.val.assign(ORACLE_CIE_N, 0.0);  // colours.SpectralBlack
   }
   const bool spectral = req->sampler == IZPI_SAMPLER_SPECTRAL;
+  const bool forward = req->abi_version >= 3 && req->accumulation == IZPI_ACC_FORWARD;
   std::atomic<size_t> next(0);
   std::vector<Counters> per((size_t)(nthreads > 0 ? nthreads : 1));
   auto worker = [&](int tid) {
@@ -1881,7 +1940,7 @@ int oracle_render(oracle_scene* s, const izpi_render_req* req, double* canvas, o
               double u = ((double)x + rnd.Float64()) / (double)nx;
               double v = ((double)y + rnd.Float64()) / (double)ny;
               Ray r = W.camera.GetRay(u, v, cam, 0);
-              col = Add(col, DeNAN(cs.Sample(r, W, 0, rnd)));
+              col = Add(col, DeNAN(forward ? cs.SampleForward(r, W, rnd) : cs.Sample(r, W, 0, rnd)));
             }
             col = ScalarDiv(col, (double)req->spp);
             out[0] = col.X; out[1] = col.Y; out[2] = col.Z;
@@ -1898,7 +1957,7 @@ int oracle_render(oracle_scene* s, const izpi_render_req* req, double* canvas, o
               double u = ((double)x + rnd.Float64()) / (double)nx;
               double v = ((double)y + rnd.Float64()) / (double)ny;
               Ray r = W.camera.GetRay(u, v, cam, lambda);
-              double radiance = ss.SampleSpectral(r, W, 0, rnd);
+              double radiance = forward ? ss.SampleSpectralForward(r, W, rnd) : ss.SampleSpectral(r, W, 0, rnd);
               double cx, cy, cz;
               GetCIEValues(lambda, &cx, &cy, &cz);
               sumX += (radiance * cx) / pdf;

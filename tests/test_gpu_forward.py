@@ -1,0 +1,163 @@
+"""GPU parity of IZPI_ACC_FORWARD (the forward-throughput accumulation, include/izpi_gpu.h).
+
+Two checks per case:
+* the kernels' forward mode == the oracle's restatement of it (ColourSampler::SampleForward,
+  SpectralSampler::SampleSpectralForward) bit for bit, counters equal;
+* the kernels' forward mode against the oracle's recursion (colour.go:33-65,
+  sampler/spectral.go:47-80): pixel RMSE < 1e-6 (north_star), NaN / Inf at the same pixels,
+  counters equal (tests/test_forward_accumulation.py gives the argument).
+At BASELINE.json's sizes: every config's full frame (C3 at 2 spp, the others at 1 spp) and
+the frames' centre tiles at their full spp.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from izpi_amd import _native as N
+from izpi_amd import configs
+from izpi_amd.renderer import GPURenderer, MultiGPURenderer, common_tiles
+from oracle import oracle as O
+from tests.test_forward_accumulation import CASES, assert_within_tolerance, scene_case
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_both(scene, W, H, spp, sampler, tiles=None, o=None, threads=16):
+    """The oracle's (recursive, forward) canvases and stats."""
+    own = o is None
+    if own:
+        o = O.OracleScene(scene, aspect_override=W / H)
+    out = []
+    for acc in (N.ACC_RECURSIVE, N.ACC_FORWARD):
+        req = N.RenderReq(width=W, height=H, spp=spp, max_depth=50, sampler=sampler, seed=12345,
+                          abi_version=N.IZPI_ABI_VERSION, accumulation=acc)
+        keep = None
+        if tiles is not None:
+            keep = np.ascontiguousarray(tiles, np.uint32)
+            req.num_tiles = len(keep)
+            req.tiles = keep.ctypes.data_as(C.POINTER(C.c_uint32))
+        canvas, st = o.render(req, threads=threads)
+        out.append((canvas.reshape(H, W, 4), st))
+    if own:
+        o.close()
+    return out
+
+
+def check_forward(img, stats, ora):
+    (rec, rs), (fwd, fs) = ora
+    assert stats["rec_dense"] == 0 and stats["pool_blocks"] == 0, stats  # no unwinding records
+    assert_parity(img, fwd, stats, fs)            # == the oracle's forward form, bit for bit
+    return assert_within_tolerance(img, rec, stats, rs)  # == the recursion within north_star's bound
+
+
+@pytest.mark.parametrize("which", CASES)
+def test_forward_small_scenes(gpu, which):
+    scene, W, H, spp, sampler = scene_case(which)
+    r = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=N.ACC_FORWARD)
+    img = r.render()
+    check_forward(img, r.stats, oracle_both(scene, W, H, spp, sampler))
+    # the same renderer, back to the recursion: bit-identical to the oracle's
+    r.accumulation = N.ACC_RECURSIVE
+    img2 = r.render()
+    assert r.stats["pool_blocks"] >= 0
+    (rec, rs), _ = oracle_both(scene, W, H, spp, sampler)
+    assert_parity(img2, rec, r.stats, rs)
+    r.close()
+
+
+@pytest.mark.parametrize("tune", [{"flags": N.TUNE_NO_TAIL}, {"slots": 3000}, {"chunk_units": 3000}])
+def test_forward_launch_variants(gpu, tune):
+    """k_tail or none, few slots (many refills), several chunks of per-sample results."""
+    for which in ("glass_spectral", "pbr"):
+        scene, W, H, spp, sampler = scene_case(which)
+        r = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=N.ACC_FORWARD, tuning=N.tuning(**tune))
+        img = r.render()
+        check_forward(img, r.stats, oracle_both(scene, W, H, spp, sampler))
+        r.close()
+
+
+def test_forward_full_size_c3_frame(gpu):
+    """BASELINE.json's C3 frame (1024x1024, 817k-triangle dragon) at 2 spp, forward mode."""
+    cfg = configs.configs()["C3"]
+    scene = cfg.build()
+    r = GPURenderer(scene, cfg.width, cfg.height, 2, accumulation=N.ACC_FORWARD)
+    img = r.render()
+    check_forward(img, r.stats, oracle_both(scene, cfg.width, cfg.height, 2, N.SAMPLER_COLOUR))
+    r.close()
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C4", "C5"])
+def test_forward_full_size_frames(gpu, name):
+    """C1 at its full 16 spp; C2, C4 and C5 as full frames at 1 spp (C5 with the Spectral
+    post-processing on both sides)."""
+    cfg = configs.configs()[name]
+    scene = cfg.build()
+    spp = cfg.spp if name == "C1" else 1
+    r = GPURenderer(scene, cfg.width, cfg.height, spp, sampler=cfg.sampler, accumulation=N.ACC_FORWARD)
+    if cfg.sampler == N.SAMPLER_SPECTRAL:
+        img = r.render_spectral_rgb()
+        o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
+        ora = oracle_both(scene, cfg.width, cfg.height, spp, cfg.sampler, o=o)
+        ora = [(O.xyz_to_rgb(O.firefly(c.reshape(-1), cfg.width, cfg.height), cfg.width, cfg.height,
+                             r.exposure).reshape(cfg.height, cfg.width, 4), st) for c, st in ora]
+        o.close()
+    else:
+        img = r.render()
+        ora = oracle_both(scene, cfg.width, cfg.height, spp, cfg.sampler)
+    check_forward(img, r.stats, ora)
+    r.close()
+
+
+@pytest.mark.parametrize("name,ntiles,tune", [
+    ("C3", 4, None),
+    ("C2", 4, None),
+    ("C4", 2, None),
+    ("C5", 1, {"chunk_units": 1 << 20}),  # 5 chunks of per-sample results, as C5's full frame
+])
+@pytest.mark.timeout(600)
+def test_forward_full_spp_centre_tiles(gpu, name, ntiles, tune):
+    """Each config's first tiles in spiral order (the centre) at its FULL spp."""
+    cfg = configs.configs()[name]
+    scene = cfg.build()
+    tiles = common_tiles(cfg.width, cfg.height)[:ntiles]
+    r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp, sampler=cfg.sampler, accumulation=N.ACC_FORWARD,
+                    tuning=N.tuning(**tune) if tune else None)
+    img = r.render(tiles=tiles)
+    rmse = check_forward(img, r.stats, oracle_both(scene, cfg.width, cfg.height, cfg.spp, cfg.sampler, tiles=tiles))
+    print("%s forward vs recursion: rmse %.3g" % (name, rmse))
+    r.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_forward_multi_gpu(gpu, devices):
+    """The multi-context fan-out in forward mode: the canvas equals one context's."""
+    scene, W, H, spp, sampler = scene_case("glass_spectral")
+    m = MultiGPURenderer(scene, W, H, spp, devices, sampler=sampler, bvh="reference", accumulation=N.ACC_FORWARD)
+    img = m.render()
+    m.close()
+    r = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=N.ACC_FORWARD)
+    one = r.render()
+    r.close()
+    assert img.tobytes() == one.tobytes()
+
+
+def test_forward_request_checks(gpu):
+    """An unknown accumulation mode is refused; an ABI-2 request (abi_version 2: the field
+    lies past its end) renders the recursion whatever the bytes there hold."""
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 24, 24, 2)
+    req = r.request()
+    req.accumulation = 7
+    st = N.RenderStats()
+    canvas = np.zeros((24, 24, 4))
+    rc = N.lib().izpi_gpu_render(r.ctx, C.byref(req), canvas.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st))
+    assert rc == N.IZPI_ERR_INVALID
+    req.abi_version = 2
+    req.accumulation = N.ACC_FORWARD
+    assert N.lib().izpi_gpu_render(r.ctx, C.byref(req), canvas.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)) == 0
+    assert st.rec_dense > 0  # the recursion's records
+    (rec, _), _ = oracle_both(scene, 24, 24, 2, N.SAMPLER_COLOUR)
+    assert canvas.tobytes() == rec.tobytes()
+    r.close()
