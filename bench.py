@@ -458,7 +458,7 @@ def main():
             img = None if c is None else c if isinstance(c, np.ndarray) else c.cpu().numpy()
         if keep and mode == "single":
             info["renderer"] = r
-        else:
+        elif reuse is None:  # (a reused renderer stays open: its owner closes it)
             r.close()
         return elapsed, agg, img, info
 
