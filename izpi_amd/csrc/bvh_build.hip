@@ -59,9 +59,7 @@ namespace {
     }                                                                       \
   } while (0)
 
-#ifndef IZPI_PLOC_RADIUS
-#define IZPI_PLOC_RADIUS 8  // PLOC search window (+-positions); 8 and 16 measured equal on C3's mesh
-#endif
+constexpr int PLOC_RADIUS = 8;  // PLOC search window (+-positions); 8 and 16 measured equal on C3's mesh
 
 constexpr float kMaxF32 = 3.40282346638528859811704183484516925440e+38f;
 
@@ -302,19 +300,13 @@ __global__ void k_ploc_offsets(uint32_t total, const int32_t* pl, const int32_t*
 // of collectChildren's greedy expansion. dec bits: 0 = the single slot is a leaf, 1-2 =
 // the wide node's split (k slots on the left), 3-4 / 5-6 / 7-8 = the split for i = 2 / 3 / 4
 // (0: use i - 1 slots).
-#ifndef IZPI_SAH_CN
-#define IZPI_SAH_CN 1.0   // visit of a wide node (one node step)
-#endif
-#ifndef IZPI_SAH_CL
-#define IZPI_SAH_CL 0.5   // visit of a leaf node (often skipped by the traversal's leaf shortcut)
-#endif
-#ifndef IZPI_SAH_CT
-#define IZPI_SAH_CT 1.0   // one primitive test
-#endif
+constexpr double SAH_CN = 1.0;  // visit of a wide node (one node step)
+constexpr double SAH_CL = 0.5;  // visit of a leaf node (often skipped by the traversal's leaf shortcut)
+constexpr double SAH_CT = 1.0;  // one primitive test
 __global__ void k_sah_leaves(uint32_t n, const Box6* pbox, double4* dcost, uint16_t* dec) {
   const uint32_t id = blockIdx.x * 256 + threadIdx.x;
   if (id >= n) return;
-  const double c = half_area(pbox[id]) * (IZPI_SAH_CL + IZPI_SAH_CT);
+  const double c = half_area(pbox[id]) * (SAH_CL + SAH_CT);
   dcost[id] = make_double4(c, c, c, c);
   dec[id] = 1;
 }
@@ -332,10 +324,10 @@ __global__ void k_sah_level(uint32_t b0, uint32_t cnt, const int32_t* pl, const 
   for (uint32_t j = 2; j <= 3; j++)
     if (L[j] + R[4 - j] < best4) { best4 = L[j] + R[4 - j]; k4 = j; }
   double d[5];
-  d[1] = area * IZPI_SAH_CN + best4;
+  d[1] = area * SAH_CN + best4;
   uint32_t bits = k4 << 1;
   if (psize[id] <= leaf_max) {
-    const double lc = area * (IZPI_SAH_CL + IZPI_SAH_CT * (double)psize[id]);
+    const double lc = area * (SAH_CL + SAH_CT * (double)psize[id]);
     if (lc <= d[1]) { d[1] = lc; bits |= 1u; }
   }
   for (uint32_t i = 2; i <= 4; i++) {
@@ -589,7 +581,7 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
     iters.push_back(n);
     while (m > 1) {
       const dim3 gm((m + 255) / 256);
-      hipLaunchKernelGGL(k_ploc_nn, gm, dim3(256), 0, st, cl.p, m, pbox.p, IZPI_PLOC_RADIUS, nnb.p);
+      hipLaunchKernelGGL(k_ploc_nn, gm, dim3(256), 0, st, cl.p, m, pbox.p, PLOC_RADIUS, nnb.p);
       hipLaunchKernelGGL(k_ploc_flags, gm, dim3(256), 0, st, nnb.p, m, mflag.p, aflag.p);
       size_t sb = sbytes;
       BVH_TRY(rocprim::exclusive_scan(stemp.p, sb, mflag.p, mscan.p, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));

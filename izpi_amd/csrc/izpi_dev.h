@@ -94,15 +94,9 @@ struct alignas(64) MatTex {
   TexSlot s[4];
 };
 
-// Byte offsets of the tables k_shade / k_tail stage per block (shade_stage) in their dynamic
-// LDS arena, sized per render to what the scene and the request use (a table the render does
-// not stage takes no space). At offset 0: the CIE tables and then the background SPD in
-// Spectral renders (has_cie), the materials' constant colours in Colour renders (places the
-// kernels derive without this struct, izpi_gpu.hip cie_lds / bg_lds / mc_lds); then the
-// materials' texture slots, the lights' records, the material and texture records, the
-// tabulated SPDs (wavelengths, then values), and the primitives' shading records when they
-// are staged too. `bytes` = the arena's size.
-
+// The scene as the kernels read it (izpi_gpu_upload_scene). The small tables k_shade / k_tail
+// stage per block in LDS are laid out by izpi_gpu.hip's lds_off (compile-time offsets; a
+// render sizes the arena to the prefix it stages, lds_bytes).
 struct DevScene {
   const GInner* inner;
   const GLeaf* leaves;
@@ -201,7 +195,6 @@ IZPI_DEV bool sdiv_plain(double x) {  // exponent within 2^+-300
   return ((uint32_t)(__double2hiint(x) >> 20) & 0x7FFu) - (1023u - 300u) <= 600u;
 }
 IZPI_DEV V3 sdiv(V3 a, double t) {
-#ifndef IZPI_NO_SHARED_DIV
   // (bitwise: one test, no branches)
   const int px = (int)sdiv_plain(a.x) | (int)(a.x == 0.0), py = (int)sdiv_plain(a.y) | (int)(a.y == 0.0),
             pz = (int)sdiv_plain(a.z) | (int)(a.z == 0.0);
@@ -219,7 +212,6 @@ IZPI_DEV V3 sdiv(V3 a, double t) {
     };
     return mk(q1(a.x), q1(a.y), q1(a.z));
   }
-#endif
   return mk(a.x / t, a.y / t, a.z / t);
 }
 IZPI_DEV double dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }

@@ -71,23 +71,15 @@ int build(hipStream_t st, const double* h_boxes, uint32_t n, uint32_t leaf_max, 
 }
 
 #define IZPI_PASS_BATCH 8  // wavefront passes launched per host poll
-#ifndef IZPI_SHADE_THREADS
-#define IZPI_SHADE_THREADS 256
-#endif
 // k_shade's block. Its reservation phase takes one unit-head and one queue atomic per
 // block-iteration; 384-thread blocks (6 waves, 2 per CU) take a third fewer but measured
 // C3 shade 114 -> 161 ms (the barriers of block_reserve2 wait for 6 waves), so 256 stays.
-constexpr uint32_t SHADE_THREADS = IZPI_SHADE_THREADS, SHADE_WAVES = SHADE_THREADS / 64;
+constexpr uint32_t SHADE_THREADS = 256, SHADE_WAVES = SHADE_THREADS / 64;
 // k_shade's queue of deferred unwinding jobs per block (fin_flush): FINQ_WORDS 8-B words
 // per job; flushed once FINQ_FLUSH are queued, an iteration adds at most SHADE_THREADS.
-#ifndef IZPI_FINQ_FLUSH
-#define IZPI_FINQ_FLUSH 1024  // C5 at 32 spp: shading 327.7 ms at 128, 323.1 at 256, 319.9 at 512, 318.3 at 1024
-#endif
-constexpr uint32_t FINQ_WORDS = 5, FINQ_FLUSH = IZPI_FINQ_FLUSH, FINQ_CAP = FINQ_FLUSH + SHADE_THREADS;
-#ifndef IZPI_MISC_STRIDE
-#define IZPI_MISC_STRIDE 64
-#endif
-constexpr int MISC_STRIDE = IZPI_MISC_STRIDE;  // words between the fields of izpi_ctx::d_misc (misc()); 1 in A/B builds only
+// C5 at 32 spp: shading 327.7 ms at a flush of 128, 323.1 at 256, 319.9 at 512, 318.3 at 1024
+constexpr uint32_t FINQ_WORDS = 5, FINQ_FLUSH = 1024, FINQ_CAP = FINQ_FLUSH + SHADE_THREADS;
+constexpr int MISC_STRIDE = 64;  // words between the fields of izpi_ctx::d_misc (misc())
 
 enum { CNT_RAYS = 0, CNT_NODES, CNT_TRI, CNT_SPH, CNT_LTRI, CNT_LSPH, CNT_NSTEP, CNT_PSTEP, CNT_SHORT,
        CNT_CLK_REFILL, CNT_CLK_NODE, CNT_CLK_PRIM, CNT_CLK_ADV, CNT_TAIL_NODES, CNT_TAIL_TRI, CNT_TAIL_SPH,
@@ -110,60 +102,12 @@ IZPI_DEV void count_add(unsigned long long* cpart, unsigned long long* counters,
 }
 
 // Loads and stores of the wavefront's streamed state (rays, kind words, path state, hit
-// records, unwinding records, per-sample results). Each pass moves far more of it than the
-// 256-MiB Infinity Cache holds, so it never comes back from there; with IZPI_NT_STREAM=1 it
-// is accessed non-temporally (the `nt` bit), so it need not displace the BVH's lines, which
-// every pass re-reads. Results are unchanged either way.
-#ifndef IZPI_NT_STREAM
-#define IZPI_NT_STREAM 0
-#endif
+// records, unwinding records, per-sample results). (Non-temporal accesses, so that the
+// stream would not displace the BVH's lines, measured no better: DESIGN 3.6.)
 template <class T>
-IZPI_DEV T sld(const T* p) {
-  if constexpr (IZPI_NT_STREAM == 0) {
-    return *p;
-  } else {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    T r;
-    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
-      v4u w[sizeof(T) / 16];
-#pragma unroll
-      for (uint32_t i = 0; i < sizeof(T) / 16; i++) w[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p) + i);
-      __builtin_memcpy(&r, w, sizeof(T));
-    } else if constexpr (sizeof(T) == 8) {
-      const uint64_t w = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
-      __builtin_memcpy(&r, &w, 8);
-    } else {
-      static_assert(sizeof(T) == 4, "streamed loads of 4, 8 or 16k bytes");
-      const uint32_t w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-      __builtin_memcpy(&r, &w, 4);
-    }
-    return r;
-  }
-}
+IZPI_DEV T sld(const T* p) { return *p; }
 template <class T>
-IZPI_DEV void sst(T* p, const T& v) {
-  if constexpr (IZPI_NT_STREAM == 0) {
-    *p = v;
-  } else {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
-      v4u w[sizeof(T) / 16];
-      __builtin_memcpy(w, &v, sizeof(T));
-#pragma unroll
-      for (uint32_t i = 0; i < sizeof(T) / 16; i++) __builtin_nontemporal_store(w[i], reinterpret_cast<v4u*>(p) + i);
-    } else if constexpr (sizeof(T) == 8) {
-      uint64_t w;
-      __builtin_memcpy(&w, &v, 8);
-      __builtin_nontemporal_store(w, reinterpret_cast<uint64_t*>(p));
-    } else {
-      static_assert(sizeof(T) == 4, "streamed stores of 4, 8 or 16k bytes");
-      uint32_t w;
-      __builtin_memcpy(&w, &v, 4);
-      __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(p));
-    }
-  }
-}
-
+IZPI_DEV void sst(T* p, const T& v) { *p = v; }
 
 // A load from a pointer known to point into LDS (the per-block staged tables): typed in
 // the LDS address space, so it is a ds_read even where the same data is read from global
@@ -193,11 +137,7 @@ IZPI_DEV T tld(const T* p) {
 // SPD and the CIE tables. Shading then reads them with LDS reads instead of dependent
 // global loads (the compiler cannot use scalar loads for scene arrays it cannot prove
 // unwritten): the light records alone took C3's shading from 128 to 114 ms.
-#ifdef IZPI_LDS_SMALL  // measurement builds: small staging tables (scenes like C3 only)
-constexpr uint32_t MAT_LDS = 16, TEX_LDS = 16, SPD_LDS = 8, BG_LDS = 8, MT_LDS = 16, LT_LDS = 8, PR_LDS = 2;
-#else
 constexpr uint32_t MAT_LDS = 64, TEX_LDS = 64, SPD_LDS = 384, BG_LDS = 128, MT_LDS = 64, LT_LDS = 64, PR_LDS = 64;
-#endif
 // The staged tables live at fixed offsets of the block's dynamic LDS arena, ordered so that
 // what a render stages is a prefix of it: the Colour tables, then the Spectral ones, then
 // the primitives. render_body sizes the arena to that prefix (lds_arena_bytes), so a render
@@ -248,9 +188,6 @@ IZPI_DEV izpi_texture tex_rec(const DevScene& sc, bool st, int32_t id) {
 // ImageTxt.Value (image.go:73-101): the nearest texel of a w x h image at (u, v), from
 // its device storage form (TEXF_RGBA or TEXF_GRAY, see TexSlot).
 IZPI_DEV V3 image_rgb(const double* texels, uint64_t off, uint32_t w, uint32_t h, uint32_t fmt, double u, double v) {
-#ifdef IZPI_EXP_TEX_NOLOAD  // timing only (wrong images): no texel index or load
-  return mk(0.5, 0.45, 0.9);
-#endif
   int64_t i = go_int(u * (double)w);
   int64_t j = go_int((1 - v) * ((double)h - 0.001));
   if (i < 0) i = 0;
@@ -258,9 +195,6 @@ IZPI_DEV V3 image_rgb(const double* texels, uint64_t off, uint32_t w, uint32_t h
   if (i > (int64_t)w - 1) i = (int64_t)w - 1;
   if (j > (int64_t)h - 1) j = (int64_t)h - 1;
   uint64_t k = (uint64_t)j * w + (uint64_t)i;
-#ifdef IZPI_EXP_TEX_HOT  // timing only (wrong images): every lookup hits the image's first 8 texels
-  k &= 7;
-#endif
   if (fmt == TEXF_GRAY) {
     const double g = texels[off + k];
     return mk(g, g, g);
@@ -308,16 +242,11 @@ IZPI_DEV bool slot_set(const TexSlot& s) { return (s.hf >> 30) != TEXF_NONE; }
 // reused when this slot's image has that size, else computed.
 IZPI_DEV V3 slot_rgb_k(const DevScene& sc, const TexSlot& s, double u, double v, bool st, uint32_t w0, uint32_t h0, uint64_t k0) {
   const uint32_t fmt = s.hf >> 30, h = s.hf & 0x3FFFFFFFu;
-#ifndef IZPI_EXP_TEX_NOLOAD
   if (fmt <= TEXF_GRAY) {
     uint64_t k = k0;
     if (s.w != w0 || h != h0) k = image_index(s.w, h, u, v);
-#ifdef IZPI_EXP_TEX_HOT
-    k &= 7;
-#endif
     return image_at(sc.texels, s.off, fmt, k);
   }
-#endif
   return slot_rgb(sc, s, u, v, st);
 }
 // The materials' texture slots staged in LDS next to their constants (mc_stage): a PBR
@@ -731,9 +660,6 @@ IZPI_DEV void trace_one(const DevScene& sc, const WaveBuf& b, uint32_t qi, int32
 // usually left the XCD's L2 by then; the (u, v) arrays it does not need make room for it
 // (31.8 KB of LDS per block: still 5 blocks per CU).
 constexpr uint32_t BVH_LDS_BYTES = 4096;
-#ifndef IZPI_TRACE_STATIC
-#define IZPI_TRACE_STATIC 0
-#endif
 template <int S, int WPE, bool DIST, bool TRI, bool LB, bool RL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
@@ -793,9 +719,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   // dequeue atomic on the one counter word (~88/us chip-wide).
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t chunk = min(tchunk, max(16u, (n + nwaves - 1u) / nwaves));
-  // each wave's first range is its own, without an atomic: IZPI_TRACE_STATIC sixteenths of
-  // the queue split evenly (at least one chunk); the rest is dequeued in chunks
-  const uint32_t first = max(chunk, (uint32_t)((uint64_t)n * IZPI_TRACE_STATIC / 16u / nwaves));
+  // each wave's first chunk is its own, without an atomic; the rest is dequeued in chunks
+  // (larger static first ranges measured slower: DESIGN 3.6)
+  const uint32_t first = chunk;
   if ((uint64_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * first >= n) return;
   uint64_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;  // wave-uniform (SGPR)
   uint64_t c_nstep = 0, c_pstep = 0, c_short = 0;
@@ -1257,11 +1183,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 }
 
-#ifdef IZPI_EXP_NO_NMAP  // timing only (wrong images): normal maps ignored
-#define IZPI_EXP_NMAP(x) false
-#else
-#define IZPI_EXP_NMAP(x) (x)
-#endif
 // Small scenes' per-primitive shading data staged in LDS by every k_shade / k_tail block
 // (shade_stage, ShadeParams::prims_staged: at most PR_LDS primitives, as in C1, C2, C4, C5):
 // the closest hit's GShade, its triangle UVs and tangent frame and a sphere's record are
@@ -1333,7 +1254,7 @@ IZPI_DEV void hit_record(const DevScene& sc, const HitOut& c, const double2* uvp
     }
     if (gs_kind(gs) == IZPI_MAT_PBR && !defer_nmap) {
       const TexSlot ns = mat_slot(sc, mt_staged, h.mat, 1);
-      if (IZPI_EXP_NMAP(slot_set(ns))) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
+      if (slot_set(ns)) {  // Material.NormalMap() != nil (triangle.go:250-264), constant maps too
         const V3 nts = slot_rgb(sc, ns, h.u, h.v, mt_staged);
         h.nraw = nts;  // PBR.Scatter reads the same texel again (pbr.go:65-91)
         h.nraw_ok = true;
@@ -1387,9 +1308,6 @@ IZPI_DEV void light_pack(const GLight& L, uint32_t k, double* out) {  // k = 0..
 // HitableSlice.PDFValue over Scene.Lights (hitable_slice.go:98-105) from the packed
 // records (LDS when staged, else packed the same way on the fly from the GLight records).
 IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t& c_lt, uint32_t& c_ls) {
-#ifdef IZPI_KRES_NO_LPDF  // register-pressure analysis builds only (tools/kres.py; never run)
-  return o.x + v.y;
-#endif
   const double weight = 1.0 / (double)sc.num_lights;
   double sum = 0;
   for (uint32_t i = 0; i < sc.num_lights; i++) {
@@ -1412,9 +1330,6 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
       }
     } else {
       c_ls++;
-#ifdef IZPI_EXP_NO_SPHERE_LPDF  // timing experiment only (wrong radiance, same paths): the sphere terms' cost
-      continue;
-#endif
       double t; int root;
       const double radius = r[3];
       if (sph_intersect_at(mk(r[0], r[1], r[2]), radius, o, v, 0.001, 1.7976931348623157e308, t, root)) {
@@ -1432,11 +1347,7 @@ IZPI_DEV double lights_pdf(const DevScene& sc, bool staged, V3 o, V3 v, uint32_t
 IZPI_DEV double* lt2_lds() { return (double*)(lds_arena() + lds_off::LT2); }
 // HitableSlice.Random (hitable_slice.go:107-110) + Triangle/Sphere.Random
 IZPI_DEV V3 lights_random(const DevScene& sc, bool staged, V3 o, Lcg& rng) {
-#ifdef IZPI_KRES_NO_LRAND  // register-pressure analysis builds only
-  return mk(rng.next() - o.x, 1.0, 0.0);
-#endif
   int64_t index = go_int(rng.next() * (double)sc.num_lights);
-#ifndef IZPI_NO_LRAND_LDS
   if (staged) {
     const double* r = lt_lds() + index * 16;
     if (lds_ld(r + 15) == (double)IZPI_PRIM_TRIANGLE) {
@@ -1456,7 +1367,6 @@ IZPI_DEV V3 lights_random(const DevScene& sc, bool staged, V3 o, Lcg& rng) {
     uvw.build(dir);
     return uvw.local(random_to_sphere(lds_ld(r + 3), dist2, rng));
   }
-#endif
   const GLight& L = sc.lights[index];
   if (L.kind == IZPI_PRIM_TRIANGLE) {
     double t1 = rng.next();
@@ -1576,18 +1486,12 @@ constexpr bool ms_has(int matset, int feature) { return (matset & feature) != 0;
 constexpr bool ms_spec(int matset) { return (matset & (MS_DIEL | MS_METAL | MS_PBR)) != 0; }
 // Record: Colour (flag, att xyz, s, p); Colour + MATSET_CONST (material, s, p); Spectral
 // (flag, att, s, p). p is always last.
-#ifndef IZPI_REC_PAD
-#define IZPI_REC_PAD 0  // measurement builds: 1 pads the 24-B records to 32 B
-#endif
-#ifndef IZPI_SMP_PAD
-#define IZPI_SMP_PAD 0  // measurement builds: 1 pads the 24-B per-sample results to 32 B
-#endif
-constexpr uint32_t SMP_D = IZPI_SMP_PAD ? 4 : 3;  // doubles per per-sample result
+constexpr uint32_t SMP_D = 3;  // doubles per per-sample result (padding them to 32 B measured no better: DESIGN 3.2)
 template <int SAMPLER, int MATSET>
 struct RecLayout {
   static constexpr bool COMPACT = SAMPLER == IZPI_SAMPLER_COLOUR && MATSET == MATSET_CONST;
   static constexpr bool THREE = COMPACT || SAMPLER != IZPI_SAMPLER_COLOUR;             // (material or att, s, p)
-  static constexpr uint32_t D = THREE ? 3 + IZPI_REC_PAD : 5;                          // doubles per record
+  static constexpr uint32_t D = THREE ? 3 : 5;                          // doubles per record
   static constexpr uint32_t P = THREE ? 2 : 4;                                         // index of p
   static constexpr uint32_t S = THREE ? 1 : 3;                                         // index of s
 };
@@ -1605,9 +1509,6 @@ IZPI_DEV double* rec_ptr(const ShadeParams& sp, uint32_t rslot, uint32_t blk, ui
 template <int SAMPLER, int MATSET>
 IZPI_DEV void rec_store(const ShadeParams& sp, uint32_t rslot, uint32_t blk, uint32_t depth, bool spec, V3 att, double s,
                         uint32_t mat) {
-#ifdef IZPI_EXP_NOREC  // timing only (wrong images): the first levels' records are not stored
-  if (depth < IZPI_EXP_NOREC) return;
-#endif
   double* rp = rec_ptr<SAMPLER, MATSET>(sp, rslot, blk, depth);
   if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {  // never specular
     if constexpr (RecLayout<SAMPLER, MATSET>::D == 4) {  // 32-B records: (material, s) in one 16-B store
@@ -1703,10 +1604,6 @@ IZPI_DEV double* sample_out(const ShadeParams& sp, uint32_t unit) { return sp.ou
 // colour.go:44-57 / sampler/spectral.go:60-72 from depth-1 down to 0.
 template <int SAMPLER, int MATSET>
 IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
-#ifdef IZPI_KRES_NO_FINISH  // register-pressure analysis builds only
-  sst(sample_out(sp, P.unit), L.x);
-  return;
-#endif
   constexpr bool NO_SPEC = !ms_spec(MATSET);
   if (SAMPLER == IZPI_SAMPLER_COLOUR && NO_SPEC && gm::bits(L.x) == 0 && gm::bits(L.y) == 0 && gm::bits(L.z) == 0) {
     // +0 radiance through only non-specular records: every level computes
@@ -1731,11 +1628,7 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
   constexpr uint32_t D = RecLayout<SAMPLER, MATSET>::D;
   // levels per batch of record loads: 8 for the Spectral sampler's 24-B records (C5 shade
   // -2.2% against 4), 4 for Colour (8 made C3's compact records +13%: more live registers)
-#ifndef IZPI_FIN_RB
   constexpr int RB = SAMPLER == IZPI_SAMPLER_SPECTRAL ? 8 : 4;
-#else
-  constexpr int RB = IZPI_FIN_RB;
-#endif
   for (int dd = skip ? -1 : (int)P.depth - 1; dd >= 0; dd -= RB) {
     double rv[RB][D];
     if constexpr (RecLayout<SAMPLER, MATSET>::COMPACT) {
@@ -1745,9 +1638,6 @@ IZPI_DEV void finish(const ShadeParams& sp, const PathSt& P, V3 L) {
       for (int j = 0; j < RB; j++) {
         if (dd - j >= 0) {
           const double* r = rec_ptr<SAMPLER, MATSET>(sp, P.rslot, P.blk, (uint32_t)(dd - j));
-#ifdef IZPI_EXP_NOREC
-          if (dd - j < IZPI_EXP_NOREC) { rv[j][0] = 0.0; rv[j][1] = 1.0; rv[j][2] = 1.0; continue; }
-#endif
           if constexpr (D == 4) {  // 32-B records: two 16-B loads
             const double2 a = sld(reinterpret_cast<const double2*>(r)), b = sld(reinterpret_cast<const double2*>(r) + 1);
             rv[j][0] = a.x; rv[j][1] = a.y; rv[j][2] = b.x;
@@ -2171,10 +2061,6 @@ template <int SAMPLER, bool FWD>
 IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBuf& out, uint32_t unit, uint32_t pos,
                          PathSt& P) {
   RayRec R;
-#ifdef IZPI_KRES_NO_REFILL  // register-pressure analysis builds only
-  dead_entry(out, pos + unit);
-  return;
-#endif
   for (;;) {
     if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
       store_entry<SAMPLER, FWD>(out, pos, P, R);
@@ -2341,7 +2227,7 @@ IZPI_DEV void shade_item(const DevScene& sc, const ShadeParams& sp, const WaveBu
         else { V3 c = slot_rgb_k(sc, s_alb, h.u, h.v, st, w0, h0, k0); alb_s = 0.299 * c.x + 0.587 * c.y + 0.114 * c.z; }
         V3 rough = slot_set(s_rgh) ? slot_rgb_k(sc, s_rgh, h.u, h.v, st, w0, h0, k0) : mk(0.5, 0.5, 0.5);
         V3 metal = slot_set(s_met) ? slot_rgb_k(sc, s_met, h.u, h.v, st, w0, h0, k0) : mk(0.0, 0.0, 0.0);
-        const bool has_nmap = IZPI_EXP_NMAP(slot_set(s_nrm));
+        const bool has_nmap = slot_set(s_nrm);
         const V3 nuv = has_nmap ? slot_rgb_k(sc, s_nrm, h.u, h.v, st, w0, h0, k0) : mk(0, 0, 0);  // one texel for both uses
         SCLK_VMWAIT();
         SCLK_ADD(SCLK_TEX, sct);
@@ -2556,20 +2442,14 @@ IZPI_DEV void fin_flush(const ShadeParams& sp, const unsigned long long* q, uint
 // with only the record-reading unwindings queued: they are short, and the queue costs
 // stores), 2 = all, 0 = none. Handing each wave's lanes jobs of similar depth (a counting
 // sort of a flush's jobs by depth) measured slower: C5 338 ms, C4 +1.4%.
-#ifndef IZPI_FIN_DEFER
-#define IZPI_FIN_DEFER 1
-#endif
 
 // One shading pass over the slots traced in the previous k_trace.
-#ifndef IZPI_SHADE_WPE
-#define IZPI_SHADE_WPE 3  // MATSET_BASIC colour register budget: 3 waves/SIMD (168 VGPRs, 6 spilled; 4 waves spill 47 VGPRs and measured 1% slower)
-#endif
-#ifndef IZPI_SHADE_WPE_OTHER
-#define IZPI_SHADE_WPE_OTHER 3  // spectral / MATSET_FULL variants: 3 waves/SIMD (C5 +7% over 2 waves despite ~100 B/lane spill)
-#endif
+// k_shade's register budget: 3 waves per SIMD (168 VGPRs). MATSET_BASIC colour at 4 waves spilled
+// 47 VGPRs and measured 1% slower; the spectral / MATSET_FULL instances ran C5 7% faster at 3
+// waves than at 2 despite ~100 B/lane of spill.
+constexpr int SHADE_WPE = 3;
 template <int SAMPLER, int MATSET, bool FWD>
-__global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu((MATSET == MATSET_BASIC || MATSET == MATSET_CONST) && SAMPLER == IZPI_SAMPLER_COLOUR ? IZPI_SHADE_WPE
-                                                                                              : IZPI_SHADE_WPE_OTHER)))
+__global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu(SHADE_WPE)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   shade_stage(sc, sp);
   uint32_t parity = 0;  // block_reserve2 LDS buffer set
@@ -2579,7 +2459,7 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
   uint32_t c_lt = 0, c_ls = 0, c_park = 0;
   const uint32_t stride = gridDim.x * SHADE_THREADS;
-  constexpr bool DEFER = !FWD && (IZPI_FIN_DEFER == 2 || (IZPI_FIN_DEFER == 1 && (SAMPLER == IZPI_SAMPLER_SPECTRAL || ms_spec(MATSET))));
+  constexpr bool DEFER = !FWD && (SAMPLER == IZPI_SAMPLER_SPECTRAL || ms_spec(MATSET));
   constexpr bool COLOUR_DEFER = DEFER && SAMPLER == IZPI_SAMPLER_COLOUR;  // a subset of the finished paths is queued
   unsigned long long* fq = sp.finq + (size_t)blockIdx.x * FINQ_WORDS * FINQ_CAP;
   uint32_t fq_n = 0;  // jobs in this block's queue (the same in every thread)
@@ -2781,7 +2661,6 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
       c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;
     }
   }
-#ifndef IZPI_OLD_ACCUM
   if (SMP_D == 3 && (ap.chunk_spp & 3u) == 0 && blockIdx.x * 256 + 256 <= ap.num_pixels) {
     // Staged through LDS, 4 samples (96 B) of each of the wave's 64 pixels at a time: the
     // wave's lanes load the 64 runs as consecutive 16-B pieces (a load instruction covers
@@ -2812,7 +2691,6 @@ __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap) {
       c0 = c0 + e.y; c1 = c1 + f.x; c2 = c2 + f.y;  // sample k + 3
     }
   }
-#endif
   if ((ap.chunk_spp & 1u) == 0 && k == 0) {
     // two samples (48 B, 16-B aligned for an even chunk_spp) per three 16-B loads: the
     // lanes' runs lie chunk_spp * 24 B apart, so every load instruction touches 64 lines
@@ -3220,9 +3098,6 @@ size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, b
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
     off += (bytes + 255) & ~(size_t)255;
-#ifdef IZPI_STATE_SKEW
-    off += (size_t)(IZPI_STATE_SKEW);  // measurement builds: arrays offset against each other
-#endif
     return p;
   };
   for (int k = 0; k < 2; k++) {
@@ -3270,13 +3145,7 @@ int resident_blocks(izpi_ctx* ctx, K kernel, int* blocks, int threads = 256, siz
 // izpi_render_tuning: prim_weight (default 32) weighs primitive steps against node steps
 // (x/16); trace_chunk queue entries per dequeue; refill_min idle lanes per refill. All
 // settings give identical results and counters.
-#ifndef IZPI_TRACE_WPE
-#define IZPI_TRACE_WPE 5
-#endif
-#ifndef IZPI_TRACE_RING
-#define IZPI_TRACE_RING 16
-#endif
-constexpr int TRACE_RING = IZPI_TRACE_RING, TRACE_WPE = IZPI_TRACE_WPE;
+constexpr int TRACE_RING = 16, TRACE_WPE = 5;
 struct Tracer {
   bool p2 = true;    // DIST
   bool tri = false;  // TRI
@@ -3309,9 +3178,6 @@ inline izpi_render_tuning tuning_of(const izpi_render_req* req) {
 // too shallow to fill it, and the 8 KB it frees hold the rays (still 5 blocks per CU).
 constexpr int ring_of(bool lb, bool rl) { return lb && rl ? 8 : TRACE_RING; }
 
-#ifndef IZPI_LB_RAY_LDS
-#define IZPI_LB_RAY_LDS 1  // the BVH-in-LDS scenes keep their rays in LDS too
-#endif
 // Pick the k_trace2 instance and its grid (no allocation: the caller grows d_spill to
 // t->spill_bytes).
 // need_uv: the caller reads the hits' (u, v) (WaveParams::hit_uv).
@@ -3330,7 +3196,7 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, bool need_uv, Trace
     t->refill_min = 40;
     t->prim_w = 24;
   }
-  t->ray_lds = t->p2 && ((t->tri && !t->lds_bvh && !need_uv) || (t->lds_bvh && IZPI_LB_RAY_LDS && (t->tri || ctx->sc.time_free))) &&
+  t->ray_lds = t->p2 && ((t->tri && !t->lds_bvh && !need_uv) || (t->lds_bvh && (t->tri || ctx->sc.time_free))) &&
                !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
   if (tu.prim_weight) t->prim_w = tu.prim_weight;
   if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
@@ -3737,10 +3603,6 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   sp.staged = ctx->num_materials <= MC_LDS && ctx->num_materials <= MAT_LDS && sc.num_lights <= LT_LDS &&
               ctx->num_textures <= TEX_LDS && ctx->num_spd <= SPD_LDS && nbg <= BG_LDS;
   sp.prims_staged = sc.num_prims <= PR_LDS && !(tuning_of(req).flags & IZPI_TUNE_NO_PRIM_LDS);
-#ifdef IZPI_NO_STAGING
-  sp.staged = 0;  // A/B builds
-  sp.prims_staged = 0;
-#endif
   if (sp.staged && (req->sampler == IZPI_SAMPLER_SPECTRAL || ctx->num_spd)) sp.staged = 2;  // + the Spectral tables
   // k_shade / k_tail's LDS arena: the prefix of lds_off's layout that this render stages
   sc.lds_bytes = sp.prims_staged ? lds_off::END : sp.staged == 2 ? lds_off::SPECTRAL_END : sp.staged ? lds_off::COLOUR_END : 0;
