@@ -21,8 +21,10 @@ LIB = LIBDIR / "libizpi_gpu.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
-SOURCES = [CSRC / "izpi_gpu.hip", CSRC / "bvh_build.hip", CSRC / "host_scene.cpp", CSRC / "scene_io.cpp"]
-DEPS = SOURCES + [CSRC / "izpi_dev.h", CSRC / "gomath.h", CSRC / "cie_tables.h", CSRC / "lightsources.h",
+SOURCES = [CSRC / "trace.hip", CSRC / "shade_colour.hip", CSRC / "shade_colour_fwd.hip", CSRC / "shade_spectral.hip",
+           CSRC / "shade_spectral_fwd.hip", CSRC / "izpi_gpu.hip", CSRC / "bvh_build.hip", CSRC / "host_scene.cpp",
+           CSRC / "scene_io.cpp"]
+DEPS = SOURCES + [CSRC / "izpi_kern.h", CSRC / "shade.h", CSRC / "izpi_dev.h", CSRC / "gomath.h", CSRC / "cie_tables.h", CSRC / "lightsources.h",
                   ROOT / "include" / "izpi_gpu.h", ROOT / "include" / "izpi_host.h", ROOT / "include" / "izpi_types.h", ROOT / "include" / "izpi_gpu_debug.h"]
 
 

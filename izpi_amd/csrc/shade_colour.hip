@@ -1,0 +1,6 @@
+// shade_colour.hip — the shading kernels of the Colour sampler, recursive (IZPI_ACC_RECURSIVE) accumulation (shade.h).
+#include "shade.h"
+
+template int run_sampler<IZPI_SAMPLER_COLOUR, false>(izpi_ctx*, const izpi_render_req*, const DevScene&, const Tracer&, ShadeParams&,
+                                 WaveParams&, AccumParams&, uint32_t, uint32_t, uint32_t, bool, float*, float*, float*,
+                                 uint32_t*);
