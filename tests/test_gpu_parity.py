@@ -569,6 +569,55 @@ def test_gpu_bvh4_builder_equals_oracle_restatement(gpu, which, method):
     r.close()
 
 
+@pytest.mark.timeout(300)
+def test_headline_tree_full_size_equals_oracle_restatement(gpu):
+    """The tree BASELINE.json's headline figure runs on: C3's 817,464-triangle mesh built on
+    the GPU (PLOC + SAH collapse, 3 primitives per leaf, as bench.py builds it) == the
+    oracle's restatement (oracle_lbvh4), node for node and in leaf order, in BVH4Node's
+    format (bvh4.go:23-39, 714-792)."""
+    from izpi_amd.renderer import GPU_BVH_METHOD, gpu_leaf_max
+    from izpi_amd.scene import HostScene
+    from tests.test_bvh_build import check_tree
+    cfg = configs.configs()["C3"]
+    host = HostScene(cfg.build(), cfg.width / cfg.height, skip_bvh=True)
+    boxes = host.prim_boxes()
+    assert len(boxes) == 817464
+    leaf = gpu_leaf_max(host.desc)
+    r = GPURenderer(configs.cornell_rgb(), 8, 8, 1)
+    nodes, order, _ = r.build_bvh4(boxes, leaf, GPU_BVH_METHOD)
+    r.close()
+    ref_nodes, ref_order = O.lbvh4(boxes, leaf, GPU_BVH_METHOD)
+    assert np.array_equal(order, ref_order)
+    assert nodes.tobytes() == ref_nodes.tobytes()
+    check_tree(nodes, order, boxes, leaf_max=leaf)
+
+
+@pytest.mark.parametrize("acc", [N.ACC_RECURSIVE, N.ACC_FORWARD])
+@pytest.mark.timeout(400)
+def test_headline_tree_c3_centre_tiles_full_spp_bitwise(gpu, acc):
+    """C3's four centre tiles at the metric's 512 spp on the GPU-built headline tree (the
+    tree of bench.py's `value`), against the oracle traversing the same tree: bit-identical,
+    counters equal, in both accumulation modes."""
+    cfg = configs.configs()["C3"]
+    scene = cfg.build()
+    tiles = common_tiles(cfg.width, cfg.height)[:4]
+    r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp, bvh="gpu", accumulation=acc)
+    img = r.render(tiles=tiles)
+    o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
+    nodes = np.frombuffer(bytes(C.string_at(C.addressof(r.host.desc.nodes.contents), 128 * r.host.desc.num_nodes)),
+                          np.uint8).reshape(-1, 128)
+    o.set_bvh(nodes, r.host._bvh_keep[1])
+    req = N.RenderReq(width=cfg.width, height=cfg.height, spp=cfg.spp, max_depth=50, sampler=N.SAMPLER_COLOUR,
+                      seed=12345, abi_version=N.IZPI_ABI_VERSION, accumulation=acc)
+    t = np.ascontiguousarray(tiles, np.uint32)
+    req.num_tiles = len(t)
+    req.tiles = t.ctypes.data_as(C.POINTER(C.c_uint32))
+    ref, ostats = o.render(req, threads=16)
+    assert_parity(img, ref.reshape(cfg.height, cfg.width, 4), r.stats, ostats)
+    o.close()
+    r.close()
+
+
 @pytest.mark.parametrize("which", ["dragon", "glass"])
 def test_render_on_gpu_built_bvh_bitwise(gpu, which):
     """The kernels on the GPU-built tree == the oracle traversing the same tree (bit for
