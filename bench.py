@@ -413,7 +413,7 @@ def main():
                 canvas_holder["c"] = canvas
                 return [st]
         setup = time.time() - ts
-        first_ms = first_alloc_ms = None
+        first_ms = first_alloc_ms = first_dev = None
         for i in range(warmup):
             t = time.perf_counter()
             sts = step()
@@ -424,6 +424,7 @@ def main():
                 # host time of the workspace allocation inside that frame (hipMalloc of fresh
                 # VRAM: its cost depends on what the box's driver must clear first)
                 first_alloc_ms = max((x or {}).get("alloc_ms", 0.0) for x in sts)
+                first_dev = {k: max((x or {}).get(k, 0.0) for x in sts) for k in ("total_ms", "kernel_ms", "shade_ms", "tail_ms")}
         if dist is not None:
             dist.barrier()
         sync_all()
@@ -446,7 +447,7 @@ def main():
         info = {"triangles": int(r.host.desc.num_tris), "nodes": int(r.host.desc.num_nodes),
                 "leaf_max": getattr(r, "bvh_leaf_max", None),
                 "build_ms": r.bvh_build_ms if bvh == "gpu" else r.host.build_ms, "setup_s": setup,
-                "first_frame_ms": first_ms, "first_frame_alloc_ms": first_alloc_ms, "workspace_gb": (last or {}).get("workspace_bytes", 0) / 1e9,
+                "first_frame_ms": first_ms, "first_frame_alloc_ms": first_alloc_ms, "first_frame_device": first_dev, "workspace_gb": (last or {}).get("workspace_bytes", 0) / 1e9,
                 "scene_gb": (last or {}).get("scene_bytes", 0) / 1e9, "slots": (last or {}).get("slots"),
                 "rec_dense": (last or {}).get("rec_dense"), "pool_blocks": (last or {}).get("pool_blocks"),
                 "chunk_spp": (last or {}).get("chunk_spp")}
@@ -628,6 +629,9 @@ def main():
         "detail": {
             "first_frame_ms": info["first_frame_ms"],
             "first_frame_alloc_ms": info["first_frame_alloc_ms"],
+            # the first frame's device times (render call, k_trace2, k_shade, k_tail), against
+            # rank0_*_ms_per_step below: what the extra host time of the first frame is not
+            "first_frame_device_ms": info["first_frame_device"],
             "setup_s": round(info["setup_s"], 3),
             "hbm_workspace_gb": round(info["workspace_gb"], 2),
             "hbm_scene_gb": round(info["scene_gb"], 3),

@@ -37,7 +37,7 @@ typedef struct izpi_scene_desc {
   uint32_t num_prims;        /* len(BVH4.Primitives) */
   uint32_t num_tris, num_spheres, num_lights, num_materials, num_textures;
   uint32_t num_spd;          /* entries in spd_wavelengths / spd_values */
-  uint32_t pad0;
+  uint32_t flags;            /* IZPI_SCENE_* (ABI 3; was padding, 0 in ABI 1 and 2 descriptors) */
   uint64_t num_texels;       /* doubles in texels[] */
   const izpi_bvh4_node* nodes;  /* BVH4.Nodes, root = 0 (bvh4.go:42-47) */
   const uint32_t* prim_ref;     /* BVH4.Primitives (leaf order, bvh4.go:585-590) as IZPI_PRIM_REF */
@@ -68,6 +68,19 @@ typedef struct izpi_scene_desc {
   const double* spd_values;
   izpi_camera camera;
 } izpi_scene_desc;
+
+/* izpi_scene_desc.flags */
+enum {
+  /* Store the inner nodes' child boxes quantised to 8 bits per bound against a per-node f32
+   * origin and power-of-two scale (64-B nodes instead of 128 B). Every decoded box contains
+   * the node's own f32 box (rounded outwards; checked at upload in the kernels' own f32
+   * arithmetic), so the traversal visits every node the exact boxes do, and maybe more: the
+   * closest hit can differ only where two primitives are hit at the same t (A11) or a box
+   * is culled at tMax by float rounding. The traversal is that of the BVH whose slot boxes
+   * are the decoded ones (the oracle restates it, oracle_quantize_bvh4).
+   * Ignored (the scene traverses its exact boxes) when a bound is not finite. */
+  IZPI_SCENE_QUANTIZED_BVH = 1
+};
 
 enum { IZPI_SAMPLER_COLOUR = 2, IZPI_SAMPLER_SPECTRAL = 5 }; /* sampler.go:13-20 */
 enum {
@@ -108,7 +121,9 @@ enum {
   IZPI_TUNE_NO_LDS_BVH = 64,      /* small scenes: traverse from global memory, not the per-block LDS copy */
   IZPI_TUNE_NO_RAY_LDS = 128,     /* triangle-only scenes without (u, v) reads: primitive tests re-read the ray from global memory */
   IZPI_TUNE_NO_PRIM_LDS = 256,    /* small scenes: shading reads the primitives' records from global memory, not the per-block LDS copy */
-  IZPI_TUNE_NO_PLACE_PICK = 512   /* ignored since ABI 3 (the record arrays' page pick of ABI 2 is gone) */
+  IZPI_TUNE_NO_PLACE_PICK = 512,  /* ignored since ABI 3 (the record arrays' page pick of ABI 2 is gone) */
+  IZPI_TUNE_NO_QNODES = 1024      /* a quantised scene (IZPI_SCENE_QUANTIZED_BVH): k_trace2 reads the decoded 128-B nodes
+                                     instead of the 64-B quantised ones (the same boxes) */
 };
 
 typedef struct izpi_render_req {

@@ -72,6 +72,9 @@ int izpi_host_scene_prim_boxes(const izpi_host_scene* s, double* boxes);
 /* Attach a BVH4 built elsewhere: nodes in BVH4Node format with children after their
  * parents, order[k] = primitive (triangles then spheres) at leaf position k. */
 int izpi_host_scene_set_bvh(izpi_host_scene* s, const izpi_bvh4_node* nodes, uint32_t num_nodes, const uint32_t* order);
+/* Set the descriptor's IZPI_SCENE_* flags (izpi_scene_desc.flags), e.g. IZPI_SCENE_QUANTIZED_BVH
+ * for a GPU-built tree. */
+int izpi_host_scene_set_flags(izpi_host_scene* s, uint32_t flags);
 const izpi_scene_desc* izpi_host_scene_desc(const izpi_host_scene* s);
 /* Max stack depth the traversal of this BVH can reach (host-computed bound). */
 uint32_t izpi_host_scene_stack_bound(const izpi_host_scene* s);

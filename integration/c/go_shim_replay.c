@@ -19,13 +19,15 @@
  *      memory, the packed tiles written out
  *
  *   With --ref-bvh the scene keeps the host's NewBVH4 tree (Options.BVH != BVHGPU): no
- *   SKIP_BVH flag and no GPU build.
+ *   SKIP_BVH flag and no GPU build; without it the GPU tree is uploaded quantised
+ *   (izpi_host_scene_set_flags(IZPI_SCENE_QUANTIZED_BVH)). The request carries
+ *   IZPI_ACC_FORWARD (Options.Accumulation's default), IZPI_ACC_RECURSIVE with --recursive.
  *   The replay is written in the subset tests/go_shim_sequence.py reads (calls of the
  *   library in plain statements and if conditions, no call inside a ?: arm), which checks
  *   that its call sequence is the shim's in every branch.
  *
  *   usage: go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices 0,0,...]
- *                         [--bg-spd] [--tiles N] [--ref-bvh]
+ *                         [--bg-spd] [--tiles N] [--ref-bvh] [--recursive]
  * Exit status 0 on success; the canvas is written as raw little-endian float64.
  */
 #include <stdint.h>
@@ -44,11 +46,12 @@ static int fail(const char* what, const char* msg) {
 int main(int argc, char** argv) {
   if (argc < 6) return fail("usage", "go_shim_replay scene.izpi W H SPP out.f64 [--png-pipeline] [--devices a,b,..]");
   const uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]), spp = (uint32_t)atoi(argv[4]);
-  int png = 0, devices[16], ndev = 0, bg_spd = 0, ntiles = 0, ref_bvh = 0;
+  int png = 0, devices[16], ndev = 0, bg_spd = 0, ntiles = 0, ref_bvh = 0, recursive = 0;
   for (int i = 6; i < argc; i++) {
     if (!strcmp(argv[i], "--png-pipeline")) png = 1;
     else if (!strcmp(argv[i], "--bg-spd")) bg_spd = 1;
     else if (!strcmp(argv[i], "--ref-bvh")) ref_bvh = 1;
+    else if (!strcmp(argv[i], "--recursive")) recursive = 1;
     else if (!strcmp(argv[i], "--tiles") && i + 1 < argc) ntiles = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--devices") && i + 1 < argc) {
       for (char* t = strtok(argv[++i], ","); t && ndev < 16; t = strtok(NULL, ",")) devices[ndev++] = atoi(t);
@@ -103,6 +106,7 @@ int main(int argc, char** argv) {
       if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes, 2 * np, &num_nodes, order, &ms))
         return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
       if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
+      if (izpi_host_scene_set_flags(host, IZPI_SCENE_QUANTIZED_BVH)) return fail("izpi_host_scene_set_flags", izpi_host_last_error());
       free(boxes); free(nodes); free(order);
     }
   }
@@ -120,6 +124,8 @@ int main(int argc, char** argv) {
   req.out_layout = IZPI_OUT_CANVAS;
   req.seed = 12345;
   req.exposure = desc->camera.exposure;
+  req.accumulation = IZPI_ACC_FORWARD;
+  if (recursive) req.accumulation = IZPI_ACC_RECURSIVE;
   uint32_t post = IZPI_POST_NONE;
   req.sampler = IZPI_SAMPLER_COLOUR;
   double* bg = NULL;
@@ -171,7 +177,8 @@ int main(int argc, char** argv) {
   else izpi_gpu_close(ctx);
   izpi_host_scene_free(host);
   izpi_scene_free(ps);
-  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u, \"bg_spd\": %u, \"tiles\": %d, \"ref_bvh\": %d}\n",
-         req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour", ndev > 1 ? ndev : 1, post, req.num_bg_spd, ntiles, ref_bvh);
+  printf("{\"sampler\": \"%s\", \"devices\": %d, \"post\": %u, \"bg_spd\": %u, \"tiles\": %d, \"ref_bvh\": %d, \"recursive\": %d}\n",
+         req.sampler == IZPI_SAMPLER_SPECTRAL ? "spectral" : "colour", ndev > 1 ? ndev : 1, post, req.num_bg_spd, ntiles, ref_bvh,
+         recursive);
   return 0;
 }

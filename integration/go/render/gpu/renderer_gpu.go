@@ -52,10 +52,28 @@ var _ render.Renderer = (*Renderer)(nil)
 type BVH int
 
 const (
-	// BVHReference rebuilds hitable.NewBVH4's tree bit for bit on the host (≈0.6 s for 800k triangles).
-	BVHReference BVH = iota
-	// BVHGPU builds a PLOC BVH4 on the GPU (≈20 ms); images equal the reference tree's on C1-C5.
-	BVHGPU
+	// BVHGPU (the default) builds a PLOC BVH4 on the GPU (≈20 ms) and uploads it with
+	// quantised 64-B nodes (IZPI_SCENE_QUANTIZED_BVH). C3 traverses 8.5 nodes per ray on it
+	// against 34 on the reference tree. The image equals the reference tree's except where
+	// two primitives are hit at exactly the same distance (equal-t tie-breaks, A11) or a box
+	// is culled at tMax by float rounding: bitwise equal on C1-C5 (INTEGRATION.md).
+	BVHGPU BVH = iota
+	// BVHReference rebuilds hitable.NewBVH4's tree bit for bit on the host (≈0.6 s for 800k
+	// triangles): the traversal order, and so every tie-break, of izpi's own tree.
+	BVHReference
+)
+
+// Accumulation selects how a sample's radiance is summed (izpi_render_req.accumulation).
+type Accumulation int
+
+const (
+	// AccumulationForward (the default) carries each path's throughput forward: the same
+	// paths and random draws, the recursion's result within the north star's pixel RMSE
+	// < 1e-6 (rounding only), no per-bounce records (a smaller, faster workspace).
+	AccumulationForward Accumulation = iota
+	// AccumulationRecursive unwinds colour.go:44-57 / sampler/spectral.go:60-72 in its own
+	// operation order: bit-identical to the CPU restatement.
+	AccumulationRecursive
 )
 
 // Options are the render.New parameters (renderer.go:73-104) the GPU path uses, plus the device.
@@ -68,6 +86,7 @@ type Options struct {
 	Devices                            []int         // >1 entries: one Render fans out over these GPUs (izpi_gpu_multi_*)
 	Seed                               uint64        // master seed of the per-sample LCG streams
 	BVH                                BVH
+	Accumulation                       Accumulation
 	PNGPipeline                        bool          // Gamma + Clamp(1.0) on the GPU (leader.go:179-182)
 	Verbose                            bool          // progress bar while a frame renders (renderer.go:119-121)
 }
@@ -190,6 +209,9 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 			if rc := C.izpi_host_scene_set_bvh(r.host, &nodes[0], numNodes, (*C.uint32_t)(unsafe.Pointer(&order[0]))); rc != 0 {
 				return nil, lastHostError()
 			}
+			if rc := C.izpi_host_scene_set_flags(r.host, C.IZPI_SCENE_QUANTIZED_BVH); rc != 0 {
+				return nil, lastHostError()
+			}
 		}
 	}
 	if r.m != nil {
@@ -207,6 +229,10 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 	r.req.out_layout = C.IZPI_OUT_CANVAS
 	r.req.seed = C.uint64_t(opt.Seed)
 	r.req.exposure = desc.camera.exposure // Scene.Exposure = camera exposure
+	r.req.accumulation = C.IZPI_ACC_FORWARD
+	if opt.Accumulation == AccumulationRecursive {
+		r.req.accumulation = C.IZPI_ACC_RECURSIVE
+	}
 	for i := 0; i < 3; i++ {
 		r.req.background[i] = C.double(opt.Background[i])
 	}

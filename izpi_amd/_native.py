@@ -19,6 +19,7 @@ COMM_ID_BYTES = 128
 IZPI_OK, IZPI_ERR_INVALID, IZPI_ERR_HIP, IZPI_ERR_NO_SCENE, IZPI_ERR_UNSUPPORTED, IZPI_ERR_DEVICE, IZPI_ERR_PEER = range(7)
 IZPI_ABI_VERSION = 3
 ACC_RECURSIVE, ACC_FORWARD = 0, 1
+SCENE_QUANTIZED_BVH = 1
 PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
 TEX_CONSTANT, TEX_IMAGE, TEX_SPECTRAL_GAUSSIAN, TEX_SPECTRAL_TABULATED, TEX_SPECTRAL_IMAGE = 1, 3, 5, 7, 9
 MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC, MAT_LAMBERT, MAT_METAL, MAT_PBR = 1, 2, 3, 4, 5, 6
@@ -69,7 +70,7 @@ class SceneDesc(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("num_nodes", C.c_uint32), ("num_prims", C.c_uint32),
                 ("num_tris", C.c_uint32), ("num_spheres", C.c_uint32), ("num_lights", C.c_uint32),
                 ("num_materials", C.c_uint32), ("num_textures", C.c_uint32), ("num_spd", C.c_uint32),
-                ("pad0", C.c_uint32), ("num_texels", C.c_uint64),
+                ("flags", C.c_uint32), ("num_texels", C.c_uint64),
                 ("nodes", C.POINTER(BVH4Node)), ("prim_ref", c_uint32_p),
                 ("tri_v0", c_double_p), ("tri_v1", c_double_p), ("tri_v2", c_double_p),
                 ("tri_e1", c_double_p), ("tri_e2", c_double_p), ("tri_normal", c_double_p),
@@ -93,6 +94,7 @@ TUNE_NO_DIST, TUNE_GENERAL_TRACE, TUNE_NO_LEAF_SHORTCUT, TUNE_SCALAR_SLAB, TUNE_
 TUNE_NO_LDS_BVH = 64
 TUNE_NO_RAY_LDS = 128
 TUNE_NO_PRIM_LDS = 256
+TUNE_NO_QNODES = 1024
 
 
 def tuning(**kw):
@@ -202,7 +204,7 @@ EXPORTS = [
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
     "izpi_gpu_build_bvh4", "izpi_gpu_multi_open", "izpi_gpu_multi_close", "izpi_gpu_multi_last_error",
     "izpi_gpu_multi_size", "izpi_gpu_multi_context", "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render",
-    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_gpu_debug_realloc", "izpi_gpu_progress", "izpi_gpu_multi_progress", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh",
+    "izpi_gpu_comm_id", "izpi_gpu_comm_init", "izpi_gpu_render_rank", "izpi_gpu_debug_fault", "izpi_gpu_debug_realloc", "izpi_gpu_progress", "izpi_gpu_multi_progress", "izpi_host_build_scene_ex", "izpi_host_scene_prim_boxes", "izpi_host_scene_set_bvh", "izpi_host_scene_set_flags",
     "izpi_host_build_scene", "izpi_host_scene_desc", "izpi_host_scene_stack_bound", "izpi_host_scene_build_ms",
     "izpi_host_scene_free", "izpi_host_last_error", "izpi_host_tiles", "izpi_host_share_tiles", "izpi_host_share_block", "izpi_host_assemble_shares", "izpi_host_bvh_leaf_max", "izpi_host_gomath", "izpi_abi_struct_size",
     "izpi_scene_parse_text", "izpi_scene_parse_binary", "izpi_scene_serialize", "izpi_scene_info", "izpi_scene_image_file",
@@ -266,6 +268,7 @@ def lib():
     L.izpi_host_build_scene_ex.argtypes = [C.POINTER(SceneInput), C.c_uint32, C.POINTER(C.c_void_p)]
     L.izpi_host_scene_prim_boxes.argtypes = [C.c_void_p, c_double_p]
     L.izpi_host_scene_set_bvh.argtypes = [C.c_void_p, C.POINTER(BVH4Node), C.c_uint32, c_uint32_p]
+    L.izpi_host_scene_set_flags.argtypes = [C.c_void_p, C.c_uint32]
     L.izpi_host_build_scene.argtypes = [C.POINTER(SceneInput), C.POINTER(C.c_void_p)]
     L.izpi_host_scene_desc.argtypes = [C.c_void_p]
     L.izpi_host_scene_desc.restype = C.POINTER(SceneDesc)

@@ -489,6 +489,13 @@ int izpi_host_scene_prim_boxes(const izpi_host_scene* s, double* boxes) {
   return IZPI_OK;
 }
 
+int izpi_host_scene_set_flags(izpi_host_scene* s, uint32_t flags) {
+  if (!s) { g_err = "null argument"; return IZPI_ERR_INVALID; }
+  if (flags & ~(uint32_t)IZPI_SCENE_QUANTIZED_BVH) { g_err = "unknown scene flag"; return IZPI_ERR_INVALID; }
+  s->desc.flags = flags;
+  return IZPI_OK;
+}
+
 int izpi_host_scene_set_bvh(izpi_host_scene* s, const izpi_bvh4_node* nodes, uint32_t num_nodes, const uint32_t* order) {
   if (!s || (!nodes && num_nodes) || !order) { g_err = "null argument"; return IZPI_ERR_INVALID; }
   const uint32_t np = s->desc.num_tris + s->desc.num_spheres, nt = s->desc.num_tris;

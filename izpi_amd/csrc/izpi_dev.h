@@ -37,6 +37,24 @@ struct alignas(16) GInner {
   int32_t child[4];
   int32_t pad[4];
 };
+// An inner node with its child boxes quantised (IZPI_SCENE_QUANTIZED_BVH), 64 B: two per
+// 128-B line, four 16-B loads per visit instead of seven. Bound b of child i on axis a is
+// org[a] + q * 2^(e[a] - 127), q = byte i of the bound's word: the product is exact (q < 256,
+// a normal power of two), so a fused multiply-add decodes it bit for bit as the upload's
+// `org + (float)q * s` does (qdecode). Child refs as in GInner.
+struct alignas(64) GInnerQ {
+  float org[3];
+  uint32_t ex;        // biased exponents: x bits 0-7, y 8-15, z 16-23
+  uint32_t q[6];      // mnx, mny, mnz, mxx, mxy, mxz: byte i = child i
+  int32_t child[4];
+  uint32_t pad[2];
+};
+static_assert(sizeof(GInnerQ) == 64, "GInnerQ is 64 B");
+// The upload's decoding of one quantised bound (host), which the kernels' fmaf reproduces.
+__host__ __device__ inline float qdecode(float org, uint32_t q, float s) {
+  const float p = (float)q * s;  // exact
+  return org + p;
+}
 struct alignas(16) GLeaf {
   float mn[3], mx[3];
   int32_t start, count;
@@ -99,6 +117,7 @@ struct alignas(64) MatTex {
 // render sizes the arena to the prefix it stages, lds_bytes).
 struct DevScene {
   const GInner* inner;
+  const GInnerQ* innerq;        // the same nodes quantised (DevScene::quantized), else null
   const GLeaf* leaves;
   const GPrim* prims;
   const GShade* shade;          // [num_prims], leaf order
@@ -122,6 +141,7 @@ struct DevScene {
   izpi_camera cam;
   uint32_t lds_bytes;           // per render (render_body): k_shade / k_tail's dynamic LDS arena (lds_off)
   uint32_t time_free;           // no sphere moves: traversal needs no ray times (upload)
+  uint32_t quantized;           // IZPI_SCENE_QUANTIZED_BVH: `inner` holds the decoded boxes of `innerq`
 #ifdef IZPI_SHADOW
   // measurement builds only (byte breakdown): copies of the traversal arrays that
   // k_trace2 reads beside the real ones, so a class's bytes past L2 show as extra FETCH_SIZE

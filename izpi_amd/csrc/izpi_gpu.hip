@@ -317,6 +317,63 @@ size_t carve_state(char* base, uint32_t slots, bool time, bool blk, bool cold, b
   return off;
 }
 
+// Quantise inner node g's child boxes (IZPI_SCENE_QUANTIZED_BVH) into q and replace g's
+// valid slot boxes by the decoded ones. Per axis: the origin is the minimum over the valid
+// children's mins, the scale 2^e the smallest for which every child's bounds, rounded
+// outwards to the grid, fit a byte; each rounded bound is then checked in the kernels' own
+// f32 decode (qdecode) and moved one step outwards while it would not contain the exact
+// bound. False when a valid bound is not finite or no exponent fits (the scene then keeps
+// its exact boxes).
+bool quantize_node(GInner& g, GInnerQ& q) {
+  memset(&q, 0, sizeof(q));
+  float* mn[3] = {g.mnx, g.mny, g.mnz};
+  float* mx[3] = {g.mxx, g.mxy, g.mxz};
+  for (int i = 0; i < 4; i++) q.child[i] = g.child[i];
+  for (int a = 0; a < 3; a++) {
+    float lo = 0.0f, hi = 0.0f;
+    bool any = false;
+    for (int i = 0; i < 4; i++) {
+      if (g.child[i] == -1) continue;
+      if (!std::isfinite(mn[a][i]) || !std::isfinite(mx[a][i])) return false;
+      lo = any ? std::min(lo, mn[a][i]) : mn[a][i];
+      hi = any ? std::max(hi, mx[a][i]) : mx[a][i];
+      any = true;
+    }
+    const double ext = (double)hi - (double)lo;
+    int e = -126;
+    if (ext > 0) e = std::max(-126, (int)std::ceil(std::log2(ext / 255.0)));
+    uint32_t qlo[4] = {0, 0, 0, 0}, qhi[4] = {0, 0, 0, 0};
+    for (;; e++) {
+      if (e > 127) return false;
+      const float sc = std::ldexp(1.0f, e);
+      bool ok = true;
+      for (int i = 0; i < 4 && ok; i++) {
+        if (g.child[i] == -1) continue;
+        double fl = std::floor(((double)mn[a][i] - (double)lo) / (double)sc);
+        int ql = (int)std::min(255.0, std::max(0.0, fl));
+        while (ql > 0 && qdecode(lo, (uint32_t)ql, sc) > mn[a][i]) ql--;  // qdecode(lo, 0) == lo <= every min
+        double fh = std::ceil(((double)mx[a][i] - (double)lo) / (double)sc);
+        int qh = (int)std::max((double)ql, std::min(256.0, fh));
+        while (qh <= 255 && qdecode(lo, (uint32_t)qh, sc) < mx[a][i]) qh++;
+        if (qh > 255) ok = false;
+        qlo[i] = (uint32_t)ql; qhi[i] = (uint32_t)qh;
+      }
+      if (ok) break;
+    }
+    const float sc = std::ldexp(1.0f, e);
+    q.org[a] = lo;
+    q.ex |= (uint32_t)(e + 127) << (8 * a);
+    for (int i = 0; i < 4; i++) {
+      q.q[a] |= qlo[i] << (8 * i);
+      q.q[3 + a] |= qhi[i] << (8 * i);
+      if (g.child[i] == -1) continue;
+      mn[a][i] = qdecode(lo, qlo[i], sc);
+      mx[a][i] = qdecode(lo, qhi[i], sc);
+    }
+  }
+  return true;
+}
+
 void free_scene(izpi_ctx* ctx) {
   for (void* p : ctx->scene_allocs) (void)hipFree(p);
   ctx->scene_allocs.clear();
@@ -846,6 +903,33 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
       }
     }
   }
+  // ---- quantised child boxes (IZPI_SCENE_QUANTIZED_BVH, ABI 3): `inner` and the leaf
+  // records take the decoded boxes, which every traversal instance then tests (the 64-B
+  // nodes and the 128-B ones describe the same tree); a leaf's re-test box is its decoded
+  // parent slot, so its shortcut holds
+  std::vector<GInnerQ> innerq;
+  bool quantized = false;
+  if (d->abi_version >= 3 && (d->flags & IZPI_SCENE_QUANTIZED_BVH) && n_inner > 0) {
+    std::vector<GInner> dec(inner);
+    innerq.resize(n_inner);
+    quantized = true;
+    for (uint32_t k = 0; k < n_inner && quantized; k++) quantized = quantize_node(dec[k], innerq[k]);
+    if (quantized) {
+      inner.swap(dec);
+      for (uint32_t k = 0; k < n_inner; k++) {
+        const GInner& g = inner[k];
+        for (int i = 0; i < 4; i++) {
+          if (!ref_is_leaf(g.child[i])) continue;
+          GLeaf& L = leaves[(size_t)leaf_start(g.child[i])];
+          L.mn[0] = g.mnx[i]; L.mn[1] = g.mny[i]; L.mn[2] = g.mnz[i];
+          L.mx[0] = g.mxx[i]; L.mx[1] = g.mxy[i]; L.mx[2] = g.mxz[i];
+        }
+      }
+      leaf_shortcut = 1;
+    } else {
+      innerq.clear();
+    }
+  }
   // ---- primitives in leaf order
   std::vector<GPrim> prims(d->num_prims);
   std::vector<GShade> shade(d->num_prims);
@@ -979,6 +1063,8 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   double *dtex, *dswl, *dsv;
   izpi_material* dm; izpi_texture* dtx;
   UP(inner.data(), inner.size(), &di);
+  GInnerQ* dq = nullptr;
+  if (quantized) UP(innerq.data(), innerq.size(), &dq);
   UP(leaves.data(), leaves.size(), &dl);
   UP(prims.data(), prims.size(), &dp);
   UP(shade.data(), shade.size(), &dsh);
@@ -1093,7 +1179,7 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
     sc.sh_inner = si; sc.sh_leaves = sl; sc.sh_prims = sp;
   }
 #endif
-  sc.inner = di; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tritex = dtt; sc.lights = dlt; sc.materials = dm;
+  sc.inner = di; sc.innerq = dq; sc.quantized = quantized ? 1u : 0u; sc.leaves = dl; sc.prims = dp; sc.shade = dsh; sc.tritex = dtt; sc.lights = dlt; sc.materials = dm;
   sc.mat_const = dmc; sc.mat_tex = dmt; sc.textures = dtx; sc.texels = dtex; sc.spd_wl = dswl; sc.spd_val = dsv;
   sc.root = d->num_nodes ? ref[0] : -1;
   sc.num_lights = d->num_lights;

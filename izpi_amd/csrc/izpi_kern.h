@@ -1489,6 +1489,7 @@ struct Tracer {
   bool tri = false;  // TRI
   bool lds_bvh = false;  // LB
   bool ray_lds = false;  // RL
+  bool qnodes = false;   // Q
   // queue entries per dequeue and idle lanes per refill, measured on C3: chunk 128 / refill
   // 16 -> 211 ms of k_trace2 per frame, 512 / 24 -> 201, 1024 -> 207, 2048 -> 216, 64 -> 303
   uint32_t prim_w = 32, tchunk = 512, refill_min = 24;

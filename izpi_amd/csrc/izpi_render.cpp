@@ -3,8 +3,13 @@
 // only (include/izpi_gpu.h, include/izpi_host.h). No Python, no Go.
 //
 //   izpi-render --scene cornell.pbtxt [--obj mesh.obj --obj-material White] [--x 1024 --y 1024]
-//               [--samples 512] [--depth 50] [--bvh gpu|reference] [--png-pipeline]
-//               [--out image.pfm] [--raw canvas.f64] [--device 0 | --gpus N] [--seed 12345]
+//               [--samples 512] [--depth 50] [--bvh gpu|reference] [--exact-boxes] [--png-pipeline]
+//               [--accumulation forward|recursive] [--out image.pfm] [--raw canvas.f64]
+//               [--device 0 | --gpus N] [--seed 12345]
+//
+// Defaults are the Go shim's: the GPU-built tree uploaded with quantised nodes
+// (IZPI_SCENE_QUANTIZED_BVH; --exact-boxes keeps its exact f32 boxes) and the forward
+// accumulation (IZPI_ACC_FORWARD; --accumulation recursive is bit-identical to the CPU oracle).
 //
 // The scene file is read as leader.go:54-75 does (.pbtxt text, .izpi binary); a SPECTRAL
 // scene renders with the spectral sampler and Render's post-processing (leader.go:77-81,
@@ -51,7 +56,8 @@ constexpr double kMinus60Deg = -0x1.0c152382d7366p+0;  // == -ingest.go_radians(
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string scene_path, obj_path, obj_material = "White", out_pfm, out_raw, bvh = "gpu";
+  std::string scene_path, obj_path, obj_material = "White", out_pfm, out_raw, bvh = "gpu", acc = "forward";
+  bool exact_boxes = false;
   uint32_t W = 1024, H = 1024, spp = 16, depth = 50, device = 0, gpus = 1;
   uint64_t seed = 12345;
   bool png = false;
@@ -66,6 +72,8 @@ int main(int argc, char** argv) {
     else if (a == "--samples") spp = (uint32_t)atoi(val().c_str());
     else if (a == "--depth") depth = (uint32_t)atoi(val().c_str());
     else if (a == "--bvh") bvh = val();
+    else if (a == "--exact-boxes") exact_boxes = true;
+    else if (a == "--accumulation") acc = val();
     else if (a == "--png-pipeline") png = true;
     else if (a == "--out") out_pfm = val();
     else if (a == "--raw") out_raw = val();
@@ -76,6 +84,7 @@ int main(int argc, char** argv) {
   }
   if (scene_path.empty()) die("--scene is required");
   if (bvh != "gpu" && bvh != "reference") die("--bvh must be gpu or reference");
+  if (acc != "forward" && acc != "recursive") die("--accumulation must be forward or recursive");
   // ---- scene file (leader.go:54-75)
   std::vector<char> text;
   if (!read_file(scene_path, text)) die("cannot read " + scene_path);
@@ -141,6 +150,7 @@ int main(int argc, char** argv) {
                               order.data(), &ms))
         die(izpi_gpu_last_error(ctx));
       if (izpi_host_scene_set_bvh(host, nodes.data(), num_nodes, order.data())) die(izpi_host_last_error());
+      if (!exact_boxes && izpi_host_scene_set_flags(host, IZPI_SCENE_QUANTIZED_BVH)) die(izpi_host_last_error());
     }
     fprintf(stderr, "izpi-render: GPU BVH4 of %u primitives, %u nodes, %.1f ms\n", n, num_nodes, ms);
   }
@@ -157,6 +167,7 @@ int main(int argc, char** argv) {
   req.seed = seed;
   req.exposure = izpi_host_scene_desc(host)->camera.exposure;
   req.post = (spectral ? IZPI_POST_SPECTRAL : IZPI_POST_NONE) | (png ? IZPI_POST_GAMMA_CLAMP : 0u);
+  req.accumulation = acc == "forward" ? IZPI_ACC_FORWARD : IZPI_ACC_RECURSIVE;
   std::vector<double> canvas((size_t)W * H * 4);
   std::vector<izpi_render_stats> stv(gpus > 1 ? gpus : 1);
   auto t1 = std::chrono::steady_clock::now();
@@ -168,9 +179,9 @@ int main(int argc, char** argv) {
   izpi_render_stats st = stv[0];
   for (size_t i = 1; i < stv.size(); i++) { st.rays += stv[i].rays; st.node_visits += stv[i].node_visits; }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
-  printf("{\"scene\": \"%s\", \"width\": %u, \"height\": %u, \"spp\": %u, \"bvh\": \"%s\", \"sampler\": \"%s\", \"gpus\": %u, "
+  printf("{\"scene\": \"%s\", \"width\": %u, \"height\": %u, \"spp\": %u, \"bvh\": \"%s\", \"quantized\": %d, \"accumulation\": \"%s\", \"sampler\": \"%s\", \"gpus\": %u, "
          "\"setup_s\": %.3f, \"render_s\": %.4f, \"msamples_per_s\": %.2f, \"rays\": %llu, \"node_visits\": %llu}\n",
-         scene_path.c_str(), W, H, spp, bvh.c_str(), spectral ? "spectral" : "colour", gpus > 1 ? gpus : 1u, setup_s, secs,
+         scene_path.c_str(), W, H, spp, bvh.c_str(), bvh == "gpu" && !exact_boxes ? 1 : 0, acc.c_str(), spectral ? "spectral" : "colour", gpus > 1 ? gpus : 1u, setup_s, secs,
          (double)W * H * spp / secs / 1e6, (unsigned long long)st.rays, (unsigned long long)st.node_visits);
   // ---- outputs
   if (!out_raw.empty()) {

@@ -24,14 +24,18 @@
 // ds_read_b128 instead of re-reading the 48-B record from global memory, where it has
 // usually left the XCD's L2 by then; the (u, v) arrays it does not need make room for it
 // (31.8 KB of LDS per block: still 5 blocks per CU).
+// Q: the inner nodes are read in their quantised 64-B form (DevScene::innerq, GInnerQ) and
+// decoded into the same f32 boxes the 128-B records of a quantised scene hold; the slab test
+// and everything after it are unchanged.
 constexpr uint32_t BVH_LDS_BYTES = 4096;
-template <int S, int WPE, bool DIST, bool TRI, bool LB, bool RL>
+template <int S, int WPE, bool DIST, bool TRI, bool LB, bool RL, bool Q>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_trace2(const DevScene sc, const WaveParams wp, unsigned long long* counters,
                                                 uint32_t* err, int32_t* spill, uint32_t spill_stride, uint32_t prim_w,
                                                 uint32_t tchunk, uint32_t refill_min) {
   static_assert((S & (S - 1)) == 0, "ring size must be a power of two");
   static_assert(!LB || DIST, "the LDS-resident BVH instance runs the distributed leaf tests");
   static_assert(!RL || (DIST && (TRI || LB)), "the LDS-resident ray instances: triangle-only global BVH, or the BVH in LDS");
+  static_assert(!Q || !LB, "the quantised nodes are read from global memory");
   // (u, v) of the accepted hit: kept in lds_uv until the ray finishes (UVL), stored to the
   // hit record at acceptance (UVS: the BVH-in-LDS ray instance, whose steps issue no global
   // loads for the store to hold up), or not kept (C3's instance: nothing reads it)
@@ -395,6 +399,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
           mnz_ = make_float4(a2.x, a2.y, a2.z, a2.w); mxx_ = make_float4(a3.x, a3.y, a3.z, a3.w);
           mxy_ = make_float4(a4.x, a4.y, a4.z, a4.w); mxz_ = make_float4(a5.x, a5.y, a5.z, a5.w);
           ch_ = make_int4(__float_as_int(c.x), __float_as_int(c.y), __float_as_int(c.z), __float_as_int(c.w));
+        } else if constexpr (Q) {
+          // GInnerQ = (org, ex), (q mnx, mny, mnz, mxx), (q mxy, mxz, child 0, 1), (child 2, 3, -, -);
+          // leaf lanes read their last two loads from the root node (values not used)
+          const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
+                                                                     : (const void*)(sc.innerq + cur));
+          const float4* np = is_leaf ? reinterpret_cast<const float4*>(sc.innerq) : lp;
+          q0 = lp[0]; q1 = lp[1];
+          const float4 c2 = np[2], c3 = np[3];
+          const uint32_t ex = __float_as_uint(q0.w);
+          const float sx = __uint_as_float((ex & 0xFFu) << 23), sy = __uint_as_float(((ex >> 8) & 0xFFu) << 23),
+                      sz = __uint_as_float(((ex >> 16) & 0xFFu) << 23);
+          // org + q * 2^e: the product is exact, so the fused form rounds once, as qdecode does
+          auto dec4 = [](float w, float o, float sc_) {
+            const uint32_t b = __float_as_uint(w);
+            return make_float4(__builtin_fmaf((float)(b & 0xFFu), sc_, o), __builtin_fmaf((float)((b >> 8) & 0xFFu), sc_, o),
+                               __builtin_fmaf((float)((b >> 16) & 0xFFu), sc_, o), __builtin_fmaf((float)(b >> 24), sc_, o));
+          };
+          // (slot 0 of mnx / mny / ... is replaced by the GLeaf box for leaf lanes below)
+          const float4 dmnx = dec4(q1.x, q0.x, sx), dmny = dec4(q1.y, q0.y, sy), dmnz = dec4(q1.z, q0.z, sz);
+          const float4 dmxx = dec4(q1.w, q0.x, sx), dmxy = dec4(c2.x, q0.y, sy), dmxz = dec4(c2.y, q0.z, sz);
+          // arrange as the 128-B path's registers: q0 / q1 hold the leaf box, the rest slots 1-3
+          const float4 l0 = q0, l1 = q1;
+          q0 = is_leaf ? l0 : dmnx;
+          q1 = is_leaf ? l1 : make_float4(dmny.x, dmny.y, dmny.z, dmny.w);
+          mnz_ = dmnz; mxx_ = dmxx; mxy_ = dmxy; mxz_ = dmxz;
+          ch_ = make_int4(__float_as_int(c2.z), __float_as_int(c2.w), __float_as_int(c3.x), __float_as_int(c3.y));
         } else {
           const float4* lp = reinterpret_cast<const float4*>(is_leaf ? (const void*)(sc.leaves + leaf_start(cur))
                                                                      : (const void*)(sc.inner + cur));
@@ -549,10 +579,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 }
 
 
-#define IZPI_T2_LIST(X)                                                                                      \
-  X(true, false, false, false) X(true, true, false, false) X(false, false, false, false) X(false, true, false, false) \
-  X(true, false, true, false) X(true, true, true, false) X(true, true, false, true) X(true, false, true, true)  \
-  X(true, true, true, true)
+// (DIST, TRI, LB, RL, Q) of the compiled instances
+#define IZPI_T2_LIST(X)                                                                                           \
+  X(true, false, false, false, false) X(true, true, false, false, false) X(false, false, false, false, false)        \
+  X(false, true, false, false, false) X(true, false, true, false, false) X(true, true, true, false, false)           \
+  X(true, true, false, true, false) X(true, false, true, true, false) X(true, true, true, true, false)               \
+  X(true, false, false, false, true) X(true, true, false, false, true) X(true, true, false, true, true)
 // The BVH-in-LDS ray instances run an 8-entry stack ring: their trees (at most 4 KB) are
 // too shallow to fill it, and the 8 KB it frees hold the rays (still 5 blocks per CU).
 constexpr int ring_of(bool lb, bool rl) { return lb && rl ? 8 : TRACE_RING; }
@@ -577,13 +609,17 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, bool need_uv, Trace
   }
   t->ray_lds = t->p2 && ((t->tri && !t->lds_bvh && !need_uv) || (t->lds_bvh && (t->tri || ctx->sc.time_free))) &&
                !(tu.flags & IZPI_TUNE_NO_RAY_LDS);
+  // a quantised scene's 64-B nodes (the 128-B records hold the same decoded boxes: the
+  // other instances traverse the same tree)
+  t->qnodes = ctx->sc.quantized && t->p2 && !t->lds_bvh && !(tu.flags & IZPI_TUNE_NO_QNODES);
   if (tu.prim_weight) t->prim_w = tu.prim_weight;
   if (tu.trace_chunk) t->tchunk = tu.trace_chunk;
   if (tu.refill_min) t->refill_min = std::min<uint32_t>(64, tu.refill_min);
   int rc = IZPI_ERR_INVALID;
-#define IZPI_T2_OCC(P, T, L, R)                                               \
-  if (t->p2 == P && t->tri == T && t->lds_bvh == L && t->ray_lds == R) \
-    rc = resident_blocks(ctx, k_trace2<ring_of(L, R), TRACE_WPE, P, T, L, R>, &t->blocks);
+  ctx->err = "no k_trace2 instance for this scene and tuning";
+#define IZPI_T2_OCC(P, T, L, R, Q)                                                               \
+  if (t->p2 == P && t->tri == T && t->lds_bvh == L && t->ray_lds == R && t->qnodes == Q) \
+    rc = resident_blocks(ctx, k_trace2<ring_of(L, R), TRACE_WPE, P, T, L, R, Q>, &t->blocks);
   IZPI_T2_LIST(IZPI_T2_OCC)
 #undef IZPI_T2_OCC
   if (rc) return rc;
@@ -594,9 +630,9 @@ int make_tracer(izpi_ctx* ctx, const izpi_render_tuning& tu, bool need_uv, Trace
 void launch_trace(izpi_ctx* ctx, const DevScene& sc, const Tracer& t, const WaveParams& wp, hipStream_t st, int32_t* spill) {
   const dim3 g(t.blocks), b(256);
   const uint32_t stride = (uint32_t)t.blocks * 256;
-#define IZPI_T2_LAUNCH(P, T, L, R)                                                                             \
-  if (t.p2 == P && t.tri == T && t.lds_bvh == L && t.ray_lds == R) {                                           \
-    hipLaunchKernelGGL((k_trace2<ring_of(L, R), TRACE_WPE, P, T, L, R>), g, b, 0, st, sc, wp, ctx->d_counters,  \
+#define IZPI_T2_LAUNCH(P, T, L, R, Q)                                                                          \
+  if (t.p2 == P && t.tri == T && t.lds_bvh == L && t.ray_lds == R && t.qnodes == Q) {                          \
+    hipLaunchKernelGGL((k_trace2<ring_of(L, R), TRACE_WPE, P, T, L, R, Q>), g, b, 0, st, sc, wp, ctx->d_counters, \
                        misc(ctx, 1), spill, stride, t.prim_w, t.tchunk, t.refill_min);                        \
     return;                                                                                                    \
   }

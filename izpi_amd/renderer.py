@@ -109,13 +109,16 @@ def common_tiles(width, height):
 class GPURenderer:
     def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
                  spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference",
-                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE):
+                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE, bvh_quantized=None):
         """bvh="reference": hitable.NewBVH4's tree, rebuilt bit for bit on the host (the
         parity default); bvh="gpu": the GPU linear BVH4 builder (izpi_gpu_build_bvh4),
         same node format, different topology. tuning: an
         N.RenderTuning for every request (None = library defaults). accumulation: how a
-        path's radiance is summed (N.ACC_*; the attribute may be changed between frames)."""
+        path's radiance is summed (N.ACC_*; the attribute may be changed between frames).
+        bvh_quantized: upload the tree with IZPI_SCENE_QUANTIZED_BVH (64-B nodes whose
+        decoded boxes contain the exact ones); None = for the GPU-built tree only."""
         self.tuning = tuning
+        self.bvh_quantized = (bvh == "gpu") if bvh_quantized is None else bool(bvh_quantized)
         self.accumulation = int(accumulation)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
@@ -146,13 +149,15 @@ class GPURenderer:
             nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes(),
                                                               self.bvh_leaf_max)
             self.host.set_bvh(nodes, order)
+        self.host.set_flags(N.SCENE_QUANTIZED_BVH if self.bvh_quantized else 0)
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None
 
-    def use_tree(self, scene, bvh, bvh_seed=12345, bvh_leaf_max=None):
-        """Re-upload `scene` with another BVH (`bvh` as in __init__) into this context. Its
-        render buffers stay and are reused by the next frame of the same request: a second
-        renderer would allocate, and leave for the driver to clear, a second workspace."""
+    def use_tree(self, scene, bvh, bvh_seed=12345, bvh_leaf_max=None, bvh_quantized=None):
+        """Re-upload `scene` with another BVH (`bvh`, `bvh_quantized` as in __init__) into this
+        context. Its render buffers stay and are reused by the next frame of the same request:
+        a second renderer would allocate, and leave for the driver to clear, a second workspace."""
+        self.bvh_quantized = (bvh == "gpu") if bvh_quantized is None else bool(bvh_quantized)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.host = HostScene(scene, aspect_override=float(self.width) / float(self.height), bvh_seed=bvh_seed,
@@ -162,6 +167,7 @@ class GPURenderer:
         if bvh == "gpu":
             nodes, order, self.bvh_build_ms = self.build_bvh4(self.host.prim_boxes(), self.bvh_leaf_max)
             self.host.set_bvh(nodes, order)
+        self.host.set_flags(N.SCENE_QUANTIZED_BVH if self.bvh_quantized else 0)
         _check(N.lib().izpi_gpu_upload_scene(self.ctx, C.byref(self.host.desc)), self.ctx, "izpi_gpu_upload_scene")
 
     def build_bvh4(self, boxes, leaf_max=4, method=None):
@@ -268,6 +274,13 @@ class GPURenderer:
             st = self.render_rank(canvas.data_ptr() if canvas is not None else None, post)
         return canvas, st
 
+    def bvh_nodes(self):
+        """The uploaded tree's BVH4Node records, (n, 128) uint8, with their exact boxes (a
+        quantised upload tests the decoded boxes that oracle.quantize_bvh4 restates)."""
+        d = self.host.desc
+        nodes = np.frombuffer(bytes(C.string_at(C.addressof(d.nodes.contents), 128 * d.num_nodes)), np.uint8).reshape(-1, 128)
+        return nodes.copy()
+
     def close(self):
         if getattr(self, "ctx", None):
             N.lib().izpi_gpu_close(self.ctx)
@@ -287,9 +300,10 @@ class MultiGPURenderer:
 
     def __init__(self, scene, width, height, spp, devices, max_depth=50, sampler=N.SAMPLER_COLOUR,
                  background=(0.0, 0.0, 0.0), spectral_background=None, seed=12345, bvh_seed=12345, bvh="gpu",
-                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE):
+                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE, bvh_quantized=None):
         self.tuning = tuning
         self.accumulation = int(accumulation)
+        self.bvh_quantized = (bvh == "gpu") if bvh_quantized is None else bool(bvh_quantized)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)
@@ -316,6 +330,7 @@ class MultiGPURenderer:
             nodes, order, self.bvh_build_ms = build_bvh4(L.izpi_gpu_multi_context(m, 0), self.host.prim_boxes(),
                                                          self.bvh_leaf_max)
             self.host.set_bvh(nodes, order)
+        self.host.set_flags(N.SCENE_QUANTIZED_BVH if self.bvh_quantized else 0)
         self._check(L.izpi_gpu_multi_upload_scene(m, C.byref(self.host.desc)), "izpi_gpu_multi_upload_scene")
         self.stats = None
 

@@ -241,6 +241,13 @@ class HostScene:
         self.desc = N.lib().izpi_host_scene_desc(self.handle).contents
         self.stack_bound = N.lib().izpi_host_scene_stack_bound(self.handle)
 
+    def set_flags(self, flags):
+        """izpi_host_scene_set_flags: the descriptor's IZPI_SCENE_* flags."""
+        rc = N.lib().izpi_host_scene_set_flags(self.handle, int(flags))
+        if rc != 0:
+            raise RuntimeError("izpi_host_scene_set_flags failed (%d): %s" % (rc, N.lib().izpi_host_last_error().decode()))
+        self.desc = N.lib().izpi_host_scene_desc(self.handle).contents
+
     def nodes(self):
         d = self.desc
         buf = (N.BVH4Node * d.num_nodes).from_address(C.addressof(d.nodes.contents))

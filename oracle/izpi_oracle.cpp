@@ -1475,6 +1475,73 @@ oracle_scene* oracle_build(const izpi_scene_input* in) {
 
 /* Attach an external BVH4 (e.g. the GPU builder's): nodes + leaf order of the
  * transport-order primitives (triangles, then spheres). */
+/* IZPI_SCENE_QUANTIZED_BVH restated (a transform of the tree's boxes, not izpi code): every
+ * inner node's valid slot boxes are replaced by their 8-bit quantisation against the node's
+ * per-axis minimum and a power-of-two scale (the smallest 2^e >= 2^-126 for which every
+ * bound, rounded outwards to the grid and decoded as org + float(q) * 2^e in f32, contains
+ * the exact bound), and a leaf node's slot-0 box by its parent slot's decoded box. Returns
+ * 0, with `out` = `in`, when a valid bound is not finite or no exponent fits. */
+static float orc_qdec(float org, int q, float sc) { float p = (float)q * sc; return org + p; }
+int oracle_quantize_bvh4(const izpi_bvh4_node* in, uint32_t n, izpi_bvh4_node* out) {
+  std::vector<izpi_bvh4_node> w(in, in + n);
+  for (uint32_t k = 0; k < n; k++) {
+    izpi_bvh4_node& nd = w[k];
+    if (nd.prim_count[0] > 0) continue;  // leaf node: its box comes from its parent
+    float* lo[3] = {nd.min_x, nd.min_y, nd.min_z};
+    float* hi[3] = {nd.max_x, nd.max_y, nd.max_z};
+    for (int a = 0; a < 3; a++) {
+      bool first = true;
+      float org = 0.0f, top = 0.0f;
+      for (int i = 0; i < 4; i++) {
+        if (nd.child[i] == -1) continue;
+        if (!std::isfinite(lo[a][i]) || !std::isfinite(hi[a][i])) { std::copy(in, in + n, out); return 0; }
+        if (first || lo[a][i] < org) org = lo[a][i];
+        if (first || hi[a][i] > top) top = hi[a][i];
+        first = false;
+      }
+      const double span = (double)top - (double)org;
+      int e = span > 0 ? (int)std::ceil(std::log2(span / 255.0)) : -126;
+      if (e < -126) e = -126;
+      int qa[4] = {0, 0, 0, 0}, qb[4] = {0, 0, 0, 0};
+      for (;;) {
+        if (e > 127) { std::copy(in, in + n, out); return 0; }
+        const float sc = std::ldexp(1.0f, e);
+        bool fits = true;
+        for (int i = 0; i < 4; i++) {
+          if (nd.child[i] == -1) continue;
+          int a0 = (int)std::max(0.0, std::min(255.0, std::floor(((double)lo[a][i] - (double)org) / (double)sc)));
+          while (a0 > 0 && orc_qdec(org, a0, sc) > lo[a][i]) a0--;
+          int b0 = (int)std::max((double)a0, std::min(256.0, std::ceil(((double)hi[a][i] - (double)org) / (double)sc)));
+          while (b0 <= 255 && orc_qdec(org, b0, sc) < hi[a][i]) b0++;
+          if (b0 > 255) fits = false;
+          qa[i] = a0; qb[i] = b0;
+        }
+        if (fits) break;
+        e++;
+      }
+      const float sc = std::ldexp(1.0f, e);
+      for (int i = 0; i < 4; i++) {
+        if (nd.child[i] == -1) continue;
+        lo[a][i] = orc_qdec(org, qa[i], sc);
+        hi[a][i] = orc_qdec(org, qb[i], sc);
+      }
+    }
+  }
+  for (uint32_t k = 0; k < n; k++) {  // leaf nodes take their parent slot's decoded box (A10 re-test)
+    const izpi_bvh4_node& nd = w[k];
+    if (nd.prim_count[0] > 0) continue;
+    for (int i = 0; i < 4; i++) {
+      const int32_t c = nd.child[i];
+      if (c < 0 || w[(size_t)c].prim_count[0] == 0) continue;
+      izpi_bvh4_node& L = w[(size_t)c];
+      L.min_x[0] = nd.min_x[i]; L.min_y[0] = nd.min_y[i]; L.min_z[0] = nd.min_z[i];
+      L.max_x[0] = nd.max_x[i]; L.max_y[0] = nd.max_y[i]; L.max_z[0] = nd.max_z[i];
+    }
+  }
+  std::copy(w.begin(), w.end(), out);
+  return 1;
+}
+
 void oracle_set_bvh(oracle_scene* s, const izpi_bvh4_node* nodes, uint32_t num_nodes, const uint32_t* order) {
   World& W = s->w;
   W.bvh.Nodes.assign(nodes, nodes + num_nodes);

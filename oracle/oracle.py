@@ -69,6 +69,8 @@ def lib():
     L.oracle_postprocess.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_double), C.c_int]
     L.oracle_set_bvh.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.oracle_quantize_bvh4.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    L.oracle_quantize_bvh4.restype = C.c_int
     L.oracle_prim_boxes.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     L.oracle_lbvh4.argtypes = [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                C.POINTER(C.c_uint32)]
@@ -201,6 +203,16 @@ def lbvh4(boxes, leaf_max=4, method=1):
     m = lib().oracle_lbvh4(dptr(boxes), n, leaf_max, method, nodes.ctypes.data,
                            order.ctypes.data_as(C.POINTER(C.c_uint32)))
     return nodes[:m].copy(), order[:n].copy()
+
+
+def quantize_bvh4(nodes):
+    """IZPI_SCENE_QUANTIZED_BVH restated (oracle_quantize_bvh4): the tree with every inner
+    node's slot boxes replaced by their decoded 8-bit quantisation and every leaf node's box
+    by its parent slot's: (nodes (n, 128) uint8, applied)."""
+    nodes = np.ascontiguousarray(nodes, np.uint8).reshape(-1, 128)
+    out = np.zeros_like(nodes)
+    ok = lib().oracle_quantize_bvh4(nodes.ctypes.data, len(nodes), out.ctypes.data)
+    return out, bool(ok)
 
 
 def tiles(width, height):

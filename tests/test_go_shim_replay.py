@@ -50,7 +50,7 @@ def test_go_shim_call_sequence_bitwise(gpu, tmp_path, which, png, devices):
     assert info["sampler"] == ("spectral" if which == "spectral" else "colour")
     s = ingest.ProtoScene.from_file(izpi)
     post = (N.POST_SPECTRAL if which == "spectral" else N.POST_NONE) | (N.POST_GAMMA_CLAMP if png else 0)
-    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu")
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", accumulation=N.ACC_FORWARD)
     want = r.render(post=post)
     leaf_max, exposure = gpu_leaf_max(r.host.desc), r.exposure
     r.close()
@@ -60,13 +60,17 @@ def test_go_shim_call_sequence_bitwise(gpu, tmp_path, which, png, devices):
 
 
 def _oracle_frame(s, W, H, spp, leaf_max, exposure, png, bg=None):
-    """The oracle's Render() of scene s on the PLOC + surface-area tree (O.lbvh4 restates
-    the GPU builder node for node): the sampler, then FireflyRejection + XYZToRGB for the
-    Spectral sampler (renderer.go:215-219), then Gamma + Clamp(1) for the png pipeline."""
+    """The oracle's Render() of scene s as the shim renders it by default: on the PLOC +
+    surface-area tree (O.lbvh4 restates the GPU builder node for node) with its quantised
+    boxes (O.quantize_bvh4), forward accumulation; the sampler, then FireflyRejection +
+    XYZToRGB for the Spectral sampler (renderer.go:215-219), then Gamma + Clamp(1) for the
+    png pipeline."""
     o = O.OracleScene(s, aspect_override=W / H)
     nodes, order = O.lbvh4(o.prim_boxes(), leaf_max, N.BVH_PLOC_SAH)
+    nodes, _ = O.quantize_bvh4(nodes)
     o.set_bvh(nodes, order)
-    req = N.RenderReq(width=W, height=H, spp=spp, max_depth=50, sampler=s.sampler, seed=12345)
+    req = N.RenderReq(width=W, height=H, spp=spp, max_depth=50, sampler=s.sampler, seed=12345,
+                      abi_version=N.IZPI_ABI_VERSION, accumulation=N.ACC_FORWARD)
     keep = []
     if bg is not None:
         wl, val = (np.ascontiguousarray(x, np.float64) for x in bg)
@@ -95,7 +99,8 @@ def test_go_shim_spectral_black_background_bitwise(gpu, tmp_path, devices):
     got = got.reshape(40, 40, 4)
     s = ingest.ProtoScene.from_file(izpi)
     wl = 380.0 + 5.0 * np.arange(75)
-    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", spectral_background=(wl, np.zeros(75)))
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", spectral_background=(wl, np.zeros(75)),
+                    accumulation=N.ACC_FORWARD)
     want = r.render(post=N.POST_SPECTRAL)
     leaf_max, exposure = gpu_leaf_max(r.host.desc), r.exposure
     r.close()
@@ -114,7 +119,7 @@ def test_go_shim_render_tiles_bitwise(gpu, tmp_path, which):
     info, got, izpi = _replay(tmp_path, text, False, None, ["--tiles", "3"])
     assert info["tiles"] == 3
     s = ingest.ProtoScene.from_file(izpi)
-    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu")
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", accumulation=N.ACC_FORWARD)
     canvas = r.render()  # raw XYZ / RGB, no post
     r.close()
     want = []
@@ -132,12 +137,13 @@ def test_go_shim_render_tiles_bitwise(gpu, tmp_path, which):
 @pytest.mark.gpu
 @pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_go_shim_reference_bvh_bitwise(gpu, tmp_path, devices):
-    """Options.BVH != BVHGPU: the shim keeps the host's NewBVH4 tree (no SKIP_BVH flag, no
-    GPU build; replay --ref-bvh), and the canvas equals the Python host's on the reference
-    tree and the oracle's own render bit for bit."""
+    """Options.BVH = BVHReference, Options.Accumulation = AccumulationRecursive: the shim
+    keeps the host's NewBVH4 tree (no SKIP_BVH flag, no GPU build; replay --ref-bvh
+    --recursive), and the canvas equals the Python host's on the reference tree and the
+    oracle's own render (the recursion) bit for bit."""
     text = configs.cornell_rgb_pbtxt(1.0)
-    info, got, izpi = _replay(tmp_path, text, False, devices, ["--ref-bvh"])
-    assert info["ref_bvh"] == 1
+    info, got, izpi = _replay(tmp_path, text, False, devices, ["--ref-bvh", "--recursive"])
+    assert info["ref_bvh"] == 1 and info["recursive"] == 1
     got = got.reshape(40, 40, 4)
     s = ingest.ProtoScene.from_file(izpi)
     r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="reference")

@@ -602,11 +602,12 @@ def test_headline_tree_c3_centre_tiles_full_spp_bitwise(gpu, acc):
     scene = cfg.build()
     tiles = common_tiles(cfg.width, cfg.height)[:4]
     r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp, bvh="gpu", accumulation=acc)
+    assert r.bvh_quantized  # the headline's 64-B nodes
     img = r.render(tiles=tiles)
     o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
-    nodes = np.frombuffer(bytes(C.string_at(C.addressof(r.host.desc.nodes.contents), 128 * r.host.desc.num_nodes)),
-                          np.uint8).reshape(-1, 128)
-    o.set_bvh(nodes, r.host._bvh_keep[1])
+    qnodes, applied = O.quantize_bvh4(r.bvh_nodes())
+    assert applied
+    o.set_bvh(qnodes, r.host._bvh_keep[1])
     req = N.RenderReq(width=cfg.width, height=cfg.height, spp=cfg.spp, max_depth=50, sampler=N.SAMPLER_COLOUR,
                       seed=12345, abi_version=N.IZPI_ABI_VERSION, accumulation=acc)
     t = np.ascontiguousarray(tiles, np.uint32)
@@ -618,19 +619,81 @@ def test_headline_tree_c3_centre_tiles_full_spp_bitwise(gpu, acc):
     r.close()
 
 
+@pytest.mark.parametrize("which", ["C1", "C2", "C3", "C4", "C5"])
+def test_quantized_nodes_equal_exact_boxes_image(gpu, which):
+    """IZPI_SCENE_QUANTIZED_BVH on each config's GPU-built tree: the 64-B nodes (k_trace2's Q
+    instance) and the decoded 128-B records (IZPI_TUNE_NO_QNODES, and the other instances)
+    give the same canvas and counters; against the exact boxes the canvas is the same
+    (bitwise here: the decoded boxes only add visits) with at least as many node visits."""
+    cfg = configs.configs()[which]
+    scene = cfg.build()
+    W, H = (cfg.width, cfg.height) if which != "C5" else (512, 512)
+    spp = 1
+    imgs, stats = [], []
+    for quant, tune in ((True, None), (True, N.tuning(flags=N.TUNE_NO_QNODES)), (False, None)):
+        r = GPURenderer(scene, W, H, spp, sampler=cfg.sampler, bvh="gpu", bvh_quantized=quant, tuning=tune)
+        imgs.append(r.render())
+        stats.append(r.stats)
+        r.close()
+    assert imgs[0].tobytes() == imgs[1].tobytes()
+    for k in ("rays", "node_visits", "tri_tests", "sph_tests", "light_tri_tests", "light_sph_tests"):
+        assert stats[0][k] == stats[1][k], k
+    assert imgs[0].tobytes() == imgs[2].tobytes()
+    assert stats[0]["node_visits"] >= stats[2]["node_visits"] and stats[0]["rays"] == stats[2]["rays"]
+
+
+def test_quantized_trace_component_bitwise(gpu):
+    """izpi_gpu_trace (closest hit records) on the quantised GPU-built dragon tree == the
+    oracle's trace over oracle.quantize_bvh4's boxes, including rays along the axes."""
+    scene = configs.cornell_dragon(1.0, n=60)
+    r = GPURenderer(scene, 8, 8, 1, bvh="gpu")
+    o = O.OracleScene(scene, aspect_override=1.0)
+    qnodes, applied = O.quantize_bvh4(r.bvh_nodes())
+    assert applied
+    o.set_bvh(qnodes, r.host._bvh_keep[1])
+    rng = np.random.default_rng(5)
+    n = 4096
+    rays = np.zeros((n, 8))
+    rays[:, 0:3] = rng.uniform([5, 5, -50], [95, 95, 95], (n, 3))
+    d = rng.normal(size=(n, 3))
+    d[:256] = 0.0
+    d[np.arange(256), np.arange(256) % 3] = np.where(np.arange(256) % 2, 1.0, -1.0)
+    rays[:, 3:6] = d
+    rays[:, 6] = 0.001
+    rays[:, 7] = np.where(rng.random(n) < 0.3, rng.uniform(1, 80, n), 1.7976931348623157e308)
+    got = (N.Hit * n)()
+    assert N.lib().izpi_gpu_trace(r.ctx, O.dptr(rays), n, got) == 0
+    want = o.trace(rays)
+    nhit = 0
+    for i in range(n):
+        g, w = got[i], want[i]
+        assert g.hit == w.hit, i
+        if w.hit:
+            nhit += 1
+            assert g.prim_ref == w.prim_ref, i
+            assert bytes(g)[:72] == bytes(w)[:72], (i, g.t, w.t)
+    assert nhit > n // 2
+    o.close()
+    r.close()
+
+
+@pytest.mark.parametrize("quantized", [True, False])
 @pytest.mark.parametrize("which", ["dragon", "glass"])
-def test_render_on_gpu_built_bvh_bitwise(gpu, which):
-    """The kernels on the GPU-built tree == the oracle traversing the same tree (bit for
-    bit, counters included), and == the reference-tree image within the north-star bound."""
+def test_render_on_gpu_built_bvh_bitwise(gpu, which, quantized):
+    """The kernels on the GPU-built tree (exact boxes, or quantised 64-B nodes) == the oracle
+    traversing the same tree (with oracle.quantize_bvh4's decoded boxes), bit for bit,
+    counters included, and == the reference-tree image within the north-star bound."""
     if which == "dragon":
         scene, W, H, spp, sampler = configs.cornell_dragon(1.0, n=80), 64, 64, 8, N.SAMPLER_COLOUR
     else:
         scene, W, H, spp, sampler = configs.cornell_glass_spectral(), 48, 48, 8, N.SAMPLER_SPECTRAL
-    r = GPURenderer(scene, W, H, spp, sampler=sampler, bvh="gpu")
+    r = GPURenderer(scene, W, H, spp, sampler=sampler, bvh="gpu", bvh_quantized=quantized)
     img = r.render()
     o = O.OracleScene(scene, aspect_override=W / H)
-    nodes = np.frombuffer(bytes(C.string_at(C.addressof(r.host.desc.nodes.contents), 128 * r.host.desc.num_nodes)),
-                          np.uint8).reshape(-1, 128)
+    nodes = r.bvh_nodes()
+    if quantized:
+        nodes, applied = O.quantize_bvh4(nodes)
+        assert applied
     o.set_bvh(nodes, r.host._bvh_keep[1])
     req = N.RenderReq(width=W, height=H, spp=spp, max_depth=50, sampler=sampler, seed=12345)
     ref, ostats = o.render(req, threads=16)
@@ -866,9 +929,10 @@ def test_cli_renders_like_the_python_host(gpu, tmp_path):
                           "--raw", str(raw)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     line = json.loads(out.stdout.strip().splitlines()[-1])
-    assert line["sampler"] == "spectral" and line["bvh"] == "gpu"
+    assert line["sampler"] == "spectral" and line["bvh"] == "gpu" and line["quantized"] == 1
+    assert line["accumulation"] == "forward"
     s = ingest.ProtoScene.from_file(example)
-    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu")
+    r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", accumulation=N.ACC_FORWARD)
     img = r.render(post=N.POST_SPECTRAL)
     r.close()
     assert np.fromfile(raw, np.float64).tobytes() == img.tobytes()
@@ -880,7 +944,7 @@ def test_cli_renders_like_the_python_host(gpu, tmp_path):
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     sc = configs.cornell_obj(cube)
-    r = GPURenderer(sc, 40, 40, 4)
+    r = GPURenderer(sc, 40, 40, 4, accumulation=N.ACC_FORWARD)
     img = r.render(post=N.POST_GAMMA_CLAMP)
     r.close()
     assert np.fromfile(raw, np.float64).tobytes() == img.tobytes()
