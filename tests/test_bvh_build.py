@@ -176,3 +176,60 @@ def test_set_bvh_validates():
     bad[0] = bad[1]
     with pytest.raises(RuntimeError, match="permutation"):
         h.set_bvh(nodes, bad)
+
+
+@pytest.mark.parametrize("scene_name", ["dragon", "glass", "degenerate"])
+def test_quantized_boxes_contain_the_exact_ones(scene_name):
+    """oracle.quantize_bvh4 (IZPI_SCENE_QUANTIZED_BVH restated): the tree stays a valid BVH4
+    over the same primitives, every decoded slot box contains the exact one,
+    a leaf node's box is its parent slot's decoded box, and the boxes grow by little (mean extent
+    growth of the leaf boxes < 5% on the dragon)."""
+    if scene_name == "degenerate":
+        boxes = np.tile([1.0, 1.0, 1.0, 2.0, 2.0, 2.0], (40, 1))
+        boxes[::2, 3:] = boxes[::2, :3]  # flat boxes: zero extent on every axis
+    else:
+        scene = configs.cornell_dragon(1.0, n=40) if scene_name == "dragon" else configs.cornell_glass_spectral(1.0)
+        boxes = HostScene(scene, 1.0, skip_bvh=True).prim_boxes()
+    nodes, order = O.lbvh4(boxes, 3, N.BVH_PLOC_SAH)
+    q, applied = O.quantize_bvh4(nodes)
+    assert applied
+    check_tree(q, order, boxes, leaf_max=3)
+    f0, child, count = node_view(nodes)
+    f1, child1, count1 = node_view(q)
+    assert (child == child1).all() and (count == count1).all()
+    inner = count[:, 0] == 0
+    valid = (child != -1) & inner[:, None]
+    lo0, hi0, lo1, hi1 = f0[:, :3], f0[:, 3:], f1[:, :3], f1[:, 3:]
+    v = np.repeat(valid[:, None, :], 3, 1)
+    assert (lo1[v] <= lo0[v]).all() and (hi1[v] >= hi0[v]).all()
+    for k in np.flatnonzero(inner):  # leaves take their parent slot's decoded box
+        for sl in range(4):
+            c = child[k, sl]
+            if c >= 0 and count[c, 0] > 0:
+                assert f1[c, :, 0].tobytes() == f1[k, :, sl].tobytes()
+    if scene_name == "dragon":
+        leaf = count[:, 0] > 0
+        ext0 = (f0[leaf, 3:, 0] - f0[leaf, :3, 0]).astype(np.float64)
+        ext1 = (f1[leaf, 3:, 0] - f1[leaf, :3, 0]).astype(np.float64)
+        assert ext1.sum() / ext0.sum() < 1.05, ext1.sum() / ext0.sum()
+
+
+def test_quantized_tree_finds_the_same_closest_hits():
+    """Traversing the decoded boxes finds the closest hits of the exact ones (the oracle's
+    trace through both trees: equal t and primitive except at exact ties)."""
+    scene = configs.cornell_dragon(1.0, n=40)
+    o = O.OracleScene(scene, aspect_override=1.0)
+    nodes, order = O.lbvh4(o.prim_boxes(), 3, N.BVH_PLOC_SAH)
+    rng = np.random.default_rng(7)
+    n = 3000
+    rays = np.zeros((n, 8))
+    rays[:, :3] = rng.uniform([5, 5, -50], [95, 95, 95], (n, 3))
+    rays[:, 3:6] = rng.normal(size=(n, 3))
+    rays[:, 6], rays[:, 7] = 0.001, np.finfo(np.float64).max
+    o.set_bvh(nodes, order)
+    a = o.trace(rays)
+    o.set_bvh(O.quantize_bvh4(nodes)[0], order)
+    b = o.trace(rays)
+    o.close()
+    same = sum(bytes(a[i])[:72] == bytes(b[i])[:72] and a[i].prim_ref == b[i].prim_ref for i in range(n))
+    assert same == n
