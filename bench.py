@@ -250,9 +250,9 @@ def cpu_baseline(cfg, scene, budget_s, spp, bvh, leaf_max):
     o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
     ref_value, ref_sample = measure(o, budget_s / 2)
     value, sample, tree = ref_value, ref_sample, "izpi's own NewBVH4 tree"
-    if bvh == "gpu":  # the GPU-built tree, restated on the CPU node for node (oracle.lbvh4), quantised boxes
+    if bvh == "gpu":  # the GPU-built tree, restated on the CPU node for node (oracle.lbvh4)
         nodes, order = O.lbvh4(o.prim_boxes(), leaf_max, GPU_BVH_METHOD)
-        o.set_bvh(O.quantize_bvh4(nodes)[0], order)
+        o.set_bvh(nodes, order)
         value, sample = measure(o, budget_s / 2)
         tree = "the GPU-built PLOC tree (the tree of `value`)"
     o.close()

@@ -19,8 +19,7 @@
  *      memory, the packed tiles written out
  *
  *   With --ref-bvh the scene keeps the host's NewBVH4 tree (Options.BVH != BVHGPU): no
- *   SKIP_BVH flag and no GPU build; without it the GPU tree is uploaded quantised
- *   (izpi_host_scene_set_flags(IZPI_SCENE_QUANTIZED_BVH)). The request carries
+ *   SKIP_BVH flag and no GPU build. The request carries
  *   IZPI_ACC_FORWARD (Options.Accumulation's default), IZPI_ACC_RECURSIVE with --recursive.
  *   The replay is written in the subset tests/go_shim_sequence.py reads (calls of the
  *   library in plain statements and if conditions, no call inside a ?: arm), which checks
@@ -106,7 +105,6 @@ int main(int argc, char** argv) {
       if (izpi_gpu_build_bvh4(ctx, boxes, np, izpi_host_bvh_leaf_max(desc), IZPI_BVH_PLOC | IZPI_BVH_SAH, nodes, 2 * np, &num_nodes, order, &ms))
         return fail("izpi_gpu_build_bvh4", izpi_gpu_last_error(ctx));
       if (izpi_host_scene_set_bvh(host, nodes, num_nodes, order)) return fail("izpi_host_scene_set_bvh", izpi_host_last_error());
-      if (izpi_host_scene_set_flags(host, IZPI_SCENE_QUANTIZED_BVH)) return fail("izpi_host_scene_set_flags", izpi_host_last_error());
       free(boxes); free(nodes); free(order);
     }
   }

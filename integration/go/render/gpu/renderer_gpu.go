@@ -52,11 +52,11 @@ var _ render.Renderer = (*Renderer)(nil)
 type BVH int
 
 const (
-	// BVHGPU (the default) builds a PLOC BVH4 on the GPU (≈20 ms) and uploads it with
-	// quantised 64-B nodes (IZPI_SCENE_QUANTIZED_BVH). C3 traverses 8.5 nodes per ray on it
-	// against 34 on the reference tree. The image equals the reference tree's except where
-	// two primitives are hit at exactly the same distance (equal-t tie-breaks, A11) or a box
-	// is culled at tMax by float rounding: bitwise equal on C1-C5 (INTEGRATION.md).
+	// BVHGPU (the default) builds a PLOC BVH4 with a surface-area collapse on the GPU (≈20 ms).
+	// C3 traverses 8.5 nodes per ray on it against 34 on the reference tree. The image equals
+	// the reference tree's except where two primitives are hit at exactly the same distance
+	// (equal-t tie-breaks, A11) or a box is culled at tMax by float rounding: bitwise equal on
+	// C1-C5 (INTEGRATION.md).
 	BVHGPU BVH = iota
 	// BVHReference rebuilds hitable.NewBVH4's tree bit for bit on the host (≈0.6 s for 800k
 	// triangles): the traversal order, and so every tie-break, of izpi's own tree.
@@ -207,9 +207,6 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 				return nil, r.deviceError("izpi_gpu_build_bvh4", rc)
 			}
 			if rc := C.izpi_host_scene_set_bvh(r.host, &nodes[0], numNodes, (*C.uint32_t)(unsafe.Pointer(&order[0]))); rc != 0 {
-				return nil, lastHostError()
-			}
-			if rc := C.izpi_host_scene_set_flags(r.host, C.IZPI_SCENE_QUANTIZED_BVH); rc != 0 {
 				return nil, lastHostError()
 			}
 		}

@@ -3,13 +3,13 @@
 // only (include/izpi_gpu.h, include/izpi_host.h). No Python, no Go.
 //
 //   izpi-render --scene cornell.pbtxt [--obj mesh.obj --obj-material White] [--x 1024 --y 1024]
-//               [--samples 512] [--depth 50] [--bvh gpu|reference] [--exact-boxes] [--png-pipeline]
+//               [--samples 512] [--depth 50] [--bvh gpu|reference] [--quantized] [--png-pipeline]
 //               [--accumulation forward|recursive] [--out image.pfm] [--raw canvas.f64]
 //               [--device 0 | --gpus N] [--seed 12345]
 //
-// Defaults are the Go shim's: the GPU-built tree uploaded with quantised nodes
-// (IZPI_SCENE_QUANTIZED_BVH; --exact-boxes keeps its exact f32 boxes) and the forward
-// accumulation (IZPI_ACC_FORWARD; --accumulation recursive is bit-identical to the CPU oracle).
+// Defaults are the Go shim's: the GPU-built tree and the forward accumulation
+// (IZPI_ACC_FORWARD; --accumulation recursive is bit-identical to the CPU oracle).
+// --quantized uploads the tree with 64-B quantised nodes (IZPI_SCENE_QUANTIZED_BVH).
 //
 // The scene file is read as leader.go:54-75 does (.pbtxt text, .izpi binary); a SPECTRAL
 // scene renders with the spectral sampler and Render's post-processing (leader.go:77-81,
@@ -57,7 +57,7 @@ constexpr double kMinus60Deg = -0x1.0c152382d7366p+0;  // == -ingest.go_radians(
 
 int main(int argc, char** argv) {
   std::string scene_path, obj_path, obj_material = "White", out_pfm, out_raw, bvh = "gpu", acc = "forward";
-  bool exact_boxes = false;
+  bool quantized = false;
   uint32_t W = 1024, H = 1024, spp = 16, depth = 50, device = 0, gpus = 1;
   uint64_t seed = 12345;
   bool png = false;
@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
     else if (a == "--samples") spp = (uint32_t)atoi(val().c_str());
     else if (a == "--depth") depth = (uint32_t)atoi(val().c_str());
     else if (a == "--bvh") bvh = val();
-    else if (a == "--exact-boxes") exact_boxes = true;
+    else if (a == "--quantized") quantized = true;
     else if (a == "--accumulation") acc = val();
     else if (a == "--png-pipeline") png = true;
     else if (a == "--out") out_pfm = val();
@@ -150,7 +150,7 @@ int main(int argc, char** argv) {
                               order.data(), &ms))
         die(izpi_gpu_last_error(ctx));
       if (izpi_host_scene_set_bvh(host, nodes.data(), num_nodes, order.data())) die(izpi_host_last_error());
-      if (!exact_boxes && izpi_host_scene_set_flags(host, IZPI_SCENE_QUANTIZED_BVH)) die(izpi_host_last_error());
+      if (quantized && izpi_host_scene_set_flags(host, IZPI_SCENE_QUANTIZED_BVH)) die(izpi_host_last_error());
     }
     fprintf(stderr, "izpi-render: GPU BVH4 of %u primitives, %u nodes, %.1f ms\n", n, num_nodes, ms);
   }
@@ -181,7 +181,7 @@ int main(int argc, char** argv) {
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
   printf("{\"scene\": \"%s\", \"width\": %u, \"height\": %u, \"spp\": %u, \"bvh\": \"%s\", \"quantized\": %d, \"accumulation\": \"%s\", \"sampler\": \"%s\", \"gpus\": %u, "
          "\"setup_s\": %.3f, \"render_s\": %.4f, \"msamples_per_s\": %.2f, \"rays\": %llu, \"node_visits\": %llu}\n",
-         scene_path.c_str(), W, H, spp, bvh.c_str(), bvh == "gpu" && !exact_boxes ? 1 : 0, acc.c_str(), spectral ? "spectral" : "colour", gpus > 1 ? gpus : 1u, setup_s, secs,
+         scene_path.c_str(), W, H, spp, bvh.c_str(), bvh == "gpu" && quantized ? 1 : 0, acc.c_str(), spectral ? "spectral" : "colour", gpus > 1 ? gpus : 1u, setup_s, secs,
          (double)W * H * spp / secs / 1e6, (unsigned long long)st.rays, (unsigned long long)st.node_visits);
   // ---- outputs
   if (!out_raw.empty()) {

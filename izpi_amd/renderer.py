@@ -109,16 +109,17 @@ def common_tiles(width, height):
 class GPURenderer:
     def __init__(self, scene, width, height, spp, max_depth=50, sampler=N.SAMPLER_COLOUR, background=(0.0, 0.0, 0.0),
                  spectral_background=None, device=0, seed=12345, bvh_seed=12345, host_scene=None, bvh="reference",
-                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE, bvh_quantized=None):
+                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE, bvh_quantized=False):
         """bvh="reference": hitable.NewBVH4's tree, rebuilt bit for bit on the host (the
         parity default); bvh="gpu": the GPU linear BVH4 builder (izpi_gpu_build_bvh4),
         same node format, different topology. tuning: an
         N.RenderTuning for every request (None = library defaults). accumulation: how a
         path's radiance is summed (N.ACC_*; the attribute may be changed between frames).
         bvh_quantized: upload the tree with IZPI_SCENE_QUANTIZED_BVH (64-B nodes whose
-        decoded boxes contain the exact ones); None = for the GPU-built tree only."""
+        decoded boxes contain the exact ones: half the node memory, C3's traversal 5% slower,
+        DESIGN.md 3.6); default off."""
         self.tuning = tuning
-        self.bvh_quantized = (bvh == "gpu") if bvh_quantized is None else bool(bvh_quantized)
+        self.bvh_quantized = bool(bvh_quantized)
         self.accumulation = int(accumulation)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
@@ -153,11 +154,11 @@ class GPURenderer:
         _check(L.izpi_gpu_upload_scene(ctx, C.byref(self.host.desc)), ctx, "izpi_gpu_upload_scene")
         self.stats = None
 
-    def use_tree(self, scene, bvh, bvh_seed=12345, bvh_leaf_max=None, bvh_quantized=None):
+    def use_tree(self, scene, bvh, bvh_seed=12345, bvh_leaf_max=None, bvh_quantized=False):
         """Re-upload `scene` with another BVH (`bvh`, `bvh_quantized` as in __init__) into this
         context. Its render buffers stay and are reused by the next frame of the same request:
         a second renderer would allocate, and leave for the driver to clear, a second workspace."""
-        self.bvh_quantized = (bvh == "gpu") if bvh_quantized is None else bool(bvh_quantized)
+        self.bvh_quantized = bool(bvh_quantized)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.host = HostScene(scene, aspect_override=float(self.width) / float(self.height), bvh_seed=bvh_seed,
@@ -300,10 +301,10 @@ class MultiGPURenderer:
 
     def __init__(self, scene, width, height, spp, devices, max_depth=50, sampler=N.SAMPLER_COLOUR,
                  background=(0.0, 0.0, 0.0), spectral_background=None, seed=12345, bvh_seed=12345, bvh="gpu",
-                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE, bvh_quantized=None):
+                 bvh_leaf_max=None, tuning=None, accumulation=N.ACC_RECURSIVE, bvh_quantized=False):
         self.tuning = tuning
         self.accumulation = int(accumulation)
-        self.bvh_quantized = (bvh == "gpu") if bvh_quantized is None else bool(bvh_quantized)
+        self.bvh_quantized = bool(bvh_quantized)
         if bvh not in ("reference", "gpu"):
             raise ValueError("bvh must be 'reference' or 'gpu'")
         self.width, self.height, self.spp, self.max_depth = int(width), int(height), int(spp), int(max_depth)

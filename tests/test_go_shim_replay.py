@@ -61,13 +61,12 @@ def test_go_shim_call_sequence_bitwise(gpu, tmp_path, which, png, devices):
 
 def _oracle_frame(s, W, H, spp, leaf_max, exposure, png, bg=None):
     """The oracle's Render() of scene s as the shim renders it by default: on the PLOC +
-    surface-area tree (O.lbvh4 restates the GPU builder node for node) with its quantised
-    boxes (O.quantize_bvh4), forward accumulation; the sampler, then FireflyRejection +
+    surface-area tree (O.lbvh4 restates the GPU builder node for node), forward
+    accumulation; the sampler, then FireflyRejection +
     XYZToRGB for the Spectral sampler (renderer.go:215-219), then Gamma + Clamp(1) for the
     png pipeline."""
     o = O.OracleScene(s, aspect_override=W / H)
     nodes, order = O.lbvh4(o.prim_boxes(), leaf_max, N.BVH_PLOC_SAH)
-    nodes, _ = O.quantize_bvh4(nodes)
     o.set_bvh(nodes, order)
     req = N.RenderReq(width=W, height=H, spp=spp, max_depth=50, sampler=s.sampler, seed=12345,
                       abi_version=N.IZPI_ABI_VERSION, accumulation=N.ACC_FORWARD)

@@ -602,12 +602,9 @@ def test_headline_tree_c3_centre_tiles_full_spp_bitwise(gpu, acc):
     scene = cfg.build()
     tiles = common_tiles(cfg.width, cfg.height)[:4]
     r = GPURenderer(scene, cfg.width, cfg.height, cfg.spp, bvh="gpu", accumulation=acc)
-    assert r.bvh_quantized  # the headline's 64-B nodes
     img = r.render(tiles=tiles)
     o = O.OracleScene(scene, aspect_override=cfg.width / cfg.height)
-    qnodes, applied = O.quantize_bvh4(r.bvh_nodes())
-    assert applied
-    o.set_bvh(qnodes, r.host._bvh_keep[1])
+    o.set_bvh(r.bvh_nodes(), r.host._bvh_keep[1])
     req = N.RenderReq(width=cfg.width, height=cfg.height, spp=cfg.spp, max_depth=50, sampler=N.SAMPLER_COLOUR,
                       seed=12345, abi_version=N.IZPI_ABI_VERSION, accumulation=acc)
     t = np.ascontiguousarray(tiles, np.uint32)
@@ -646,7 +643,7 @@ def test_quantized_trace_component_bitwise(gpu):
     """izpi_gpu_trace (closest hit records) on the quantised GPU-built dragon tree == the
     oracle's trace over oracle.quantize_bvh4's boxes, including rays along the axes."""
     scene = configs.cornell_dragon(1.0, n=60)
-    r = GPURenderer(scene, 8, 8, 1, bvh="gpu")
+    r = GPURenderer(scene, 8, 8, 1, bvh="gpu", bvh_quantized=True)
     o = O.OracleScene(scene, aspect_override=1.0)
     qnodes, applied = O.quantize_bvh4(r.bvh_nodes())
     assert applied
@@ -929,7 +926,7 @@ def test_cli_renders_like_the_python_host(gpu, tmp_path):
                           "--raw", str(raw)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     line = json.loads(out.stdout.strip().splitlines()[-1])
-    assert line["sampler"] == "spectral" and line["bvh"] == "gpu" and line["quantized"] == 1
+    assert line["sampler"] == "spectral" and line["bvh"] == "gpu" and line["quantized"] == 0
     assert line["accumulation"] == "forward"
     s = ingest.ProtoScene.from_file(example)
     r = GPURenderer(s, 40, 40, 4, sampler=s.sampler, bvh="gpu", accumulation=N.ACC_FORWARD)

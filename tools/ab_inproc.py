@@ -14,6 +14,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C3")
 ap.add_argument("--spp", type=int, default=0)
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--acc", default="forward", choices=["forward", "recursive"])
+ap.add_argument("--quantized", action="store_true", help="the GPU tree with IZPI_SCENE_QUANTIZED_BVH")
 ap.add_argument("settings", nargs="+", help="'base' or comma-separated field=value of izpi_render_tuning")
 a = ap.parse_args()
 cfg = configs.configs()[a.config]
@@ -21,7 +23,9 @@ spp = a.spp or cfg.spp
 tunes = {}
 for s in a.settings:
     tunes[s] = None if s == "base" else N.tuning(**{k: int(v) for k, v in (kv.split("=") for kv in s.split(","))})
-r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=0, bvh="gpu")
+r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=0, bvh="gpu",
+                bvh_quantized=a.quantized,
+                accumulation=N.ACC_FORWARD if a.acc == "forward" else N.ACC_RECURSIVE)
 post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
 for rnd in range(a.rounds + 1):  # round 0 warms up every setting
     for s, t in tunes.items():
@@ -30,7 +34,7 @@ for rnd in range(a.rounds + 1):  # round 0 warms up every setting
         st = r.stats
         if rnd:
             print(json.dumps({"config": a.config, "spp": spp, "setting": s, "round": rnd, "trace_ms": round(st["kernel_ms"], 3),
-                              "shade_ms": round(st["shade_ms"], 3), "tail_ms": round(st["tail_ms"], 3),
+                              "shade_ms": round(st["shade_ms"], 3), "node_visits": st["node_visits"], "quantized": a.quantized, "tail_ms": round(st["tail_ms"], 3),
                               "device_ms": round(st["total_ms"], 3), "workspace_gb": round(st["workspace_bytes"] / 1e9, 1),
                               "digest": hashlib.sha1(img.tobytes()).hexdigest()[:16]}), flush=True)
 r.close()
