@@ -412,6 +412,10 @@ def main():
                 canvas, st = r.render_distributed(rank, world, post=post)
                 canvas_holder["c"] = canvas
                 return [st]
+        # render.New's part (renderer.go:73-104): the workspace, sized and first touched, outside
+        # Render (izpi times Render alone, renderer.go:170,213); a reused renderer keeps its own
+        if reuse is None:
+            r.prepare(post=post)
         setup = time.time() - ts
         first_ms = first_alloc_ms = first_dev = None
         for i in range(warmup):

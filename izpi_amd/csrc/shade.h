@@ -860,6 +860,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (tu.flags & IZPI_TUNE_PASS_LOG) fprintf(stderr, "IZPI_T start_synced %.3f\n", diag_clock_ms());
     uint32_t n = ctx->h_count[0];
     int cur = 0;
     // Launch passes in batches without a host round-trip per pass: both kernels read
@@ -947,4 +948,28 @@ int run_sampler(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, c
     if (compact) return IZPI_RUN(MATSET_CONST);
   return set == MATSET_BASIC ? IZPI_RUN(MATSET_BASIC) : set == MATSET_SURF ? IZPI_RUN(MATSET_SURF) : IZPI_RUN(MATSET_FULL);
 #undef IZPI_RUN
+}
+
+// Load the kernel code this scene's renders of (SAMPLER, FWD) run, ahead of the first frame:
+// the first occupancy query of a kernel loads its code object, ~14 ms that a fresh renderer's
+// first frame paid (tools/first_frame_host.py). Called by izpi_gpu_upload_scene.
+template <int SAMPLER, bool FWD>
+int prepare_sampler(izpi_ctx* ctx, bool compact) {
+  const uint32_t ms = ctx->matset;
+  const int set = ms == 0 ? MATSET_BASIC : (ms & ~(uint32_t)MATSET_SURF) == 0 ? MATSET_SURF : MATSET_FULL;
+  int blocks = 0, rc = IZPI_OK;
+  auto query = [&](auto shade, auto tail32, auto tail64) {
+    if ((rc = resident_blocks(ctx, shade, &blocks, (int)SHADE_THREADS))) return;
+    if ((rc = resident_blocks(ctx, tail32, &blocks))) return;
+    rc = resident_blocks(ctx, tail64, &blocks);
+  };
+#define IZPI_Q(M) query(k_shade<SAMPLER, M, FWD>, k_tail<SAMPLER, M, 32, FWD>, k_tail<SAMPLER, M, 64, FWD>)
+  if (SAMPLER == IZPI_SAMPLER_COLOUR && !FWD && compact) IZPI_Q(MATSET_CONST);
+  else if (set == MATSET_BASIC) IZPI_Q(MATSET_BASIC);
+  else if (set == MATSET_SURF) IZPI_Q(MATSET_SURF);
+  else IZPI_Q(MATSET_FULL);
+#undef IZPI_Q
+  if (rc) return rc;
+  if ((rc = resident_blocks(ctx, k_start<SAMPLER, FWD>, &blocks))) return rc;
+  return resident_blocks(ctx, k_accumulate, &blocks);
 }

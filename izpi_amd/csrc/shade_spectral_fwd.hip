@@ -4,3 +4,4 @@
 template int run_sampler<IZPI_SAMPLER_SPECTRAL, true>(izpi_ctx*, const izpi_render_req*, const DevScene&, const Tracer&, ShadeParams&,
                                  WaveParams&, AccumParams&, uint32_t, uint32_t, uint32_t, bool, float*, float*, float*,
                                  uint32_t*);
+template int prepare_sampler<IZPI_SAMPLER_SPECTRAL, true>(izpi_ctx*, bool);

@@ -200,6 +200,13 @@ class GPURenderer:
         self.stats = st.as_dict()
         return canvas
 
+    def prepare(self, tiles=None, layout=N.OUT_CANVAS, post=N.POST_NONE):
+        """izpi_gpu_prepare: allocate the workspace of this renderer's requests ahead of the
+        first frame (render.New's canvas allocation, renderer.go:73-104); after comm_init,
+        this rank's share of render_rank."""
+        req = self.request(tiles, layout, None, post)
+        _check(N.lib().izpi_gpu_prepare(self.ctx, C.byref(req)), self.ctx, "izpi_gpu_prepare")
+
     def progress(self):
         """(samples finished, samples of the request) of the render running on this context,
         readable from another thread while render() runs (izpi_gpu_progress)."""
@@ -359,6 +366,13 @@ class MultiGPURenderer:
         self._check(N.lib().izpi_gpu_multi_render(self.m, C.byref(req), ptr, st), "izpi_gpu_multi_render")
         self.stats = [st[i].as_dict() for i in range(G)]
         return canvas if to_host else None
+
+    def prepare(self, post=N.POST_NONE):
+        """izpi_gpu_multi_prepare: every device's workspace for its share, ahead of the first frame."""
+        req = make_request(self.width, self.height, self.spp, self.max_depth, self.sampler, self.background,
+                           self.seed, self.exposure, self._bg, None, N.OUT_CANVAS, post, self.tuning,
+                           self.accumulation)
+        self._check(N.lib().izpi_gpu_multi_prepare(self.m, C.byref(req)), "izpi_gpu_multi_prepare")
 
     def close(self):
         if getattr(self, "m", None):

@@ -169,3 +169,18 @@ def test_forward_request_checks(gpu):
     (rec, _), _ = oracle_both(scene, 24, 24, 2, N.SAMPLER_COLOUR)
     assert canvas.tobytes() == rec.tobytes()
     r.close()
+
+
+@pytest.mark.parametrize("acc", [N.ACC_FORWARD, N.ACC_RECURSIVE])
+def test_prepare_allocates_ahead_of_the_first_frame(gpu, acc):
+    """izpi_gpu_prepare sizes and allocates the workspace (render.New's part): the first
+    frame after it allocates nothing and renders the same canvas as an unprepared renderer."""
+    scene, W, H, spp, sampler = scene_case("pbr")
+    r = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=acc)
+    r.prepare()
+    img = r.render()
+    assert r.stats["alloc_ms"] < 0.5, r.stats["alloc_ms"]  # no allocation left for the frame
+    r.close()
+    q = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=acc)
+    assert q.render().tobytes() == img.tobytes()
+    q.close()
