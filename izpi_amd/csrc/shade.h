@@ -870,8 +870,8 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     // Once every unit has started, the queue only shrinks: poll after every pass, so that
     // k_tail takes over as soon as few enough paths remain instead of up to 8 passes later
     // (each of those last passes costs ~0.3-1 ms of mostly idle machine).
-    int B = IZPI_PASS_BATCH;
     const bool pass_log = (tu.flags & IZPI_TUNE_PASS_LOG) != 0;  // diagnostics: per-pass times on stderr
+    int B = pass_log ? 1 : IZPI_PASS_BATCH;  // (the log reads every pass's queue length)
     while (n > 0) {
       for (int b = 0; b < B; b++) {
         wp.in = q[cur]; wp.in_count = qn[cur];

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--pass-log", action="store_true", help="per-pass trace/shade times and queue lengths on stderr")
     ap.add_argument("--tail-paths", type=int, default=0, help="tuning: k_tail takes over at <= this many paths")
     ap.add_argument("--variant", default=None, help="a library built by tools/variants.py build NAME")
+    ap.add_argument("--acc", default="forward", choices=["forward", "recursive"])
+    ap.add_argument("--ranks", default="", help="comma list of the ranks to render (default all)")
     ap.add_argument("--share-slots", default="", help="comma list: tuning slot caps tried for the shares of W > 1 (the W = 1 frame keeps the default)")
     a = ap.parse_args()
     import torch
@@ -38,7 +40,8 @@ def main():
     if a.tail_paths:
         tune["tail_paths"] = a.tail_paths
     r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, bvh=a.bvh,
-                    tuning=N.tuning(**tune) if tune else None)
+                    tuning=N.tuning(**tune) if tune else None,
+                    accumulation=N.ACC_FORWARD if a.acc == "forward" else N.ACC_RECURSIVE)
     all_tiles = common_tiles(cfg.width, cfg.height)
     t1 = None
     base_tuning = r.tuning
@@ -50,7 +53,7 @@ def main():
         if sl:
             r.tuning = N.tuning(**dict(tune, slots=sl))
         worst, times = 0.0, []
-        for rank in range(w):
+        for rank in ([int(x) for x in a.ranks.split(",")] if a.ranks and w > 1 else range(w)):
             mine = sharding.shard_tiles(all_tiles, rank, w)
             buf = torch.zeros(sharding.packed_len(all_tiles, w), dtype=torch.float64, device="cuda")
             r.render_device(buf.data_ptr(), tiles=mine, layout=N.OUT_PACKED)  # warm
