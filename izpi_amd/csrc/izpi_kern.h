@@ -1187,7 +1187,9 @@ IZPI_DEV bool finish_reads(const PathSt& P, V3 L) {
 
 // IZPI_ACC_FORWARD: the finished path's sample is its throughput times the terminal
 // radiance L (Colour: DeNAN per sample, rgb.go:36; Spectral: the XYZ weights of
-// render/spectral.go:92-96), with no records to read.
+// render/spectral.go:92-96), with no records to read. Spectral: the sample is stored raw,
+// (radiance, lambda, pdf), and k_accumulate applies the XYZ weights (raw_spectral): the CIE
+// lookup inlined at the item's two exits cost the Spectral forward instances 26 spilled VGPRs.
 template <int SAMPLER>
 IZPI_DEV void finish_fwd(const ShadeParams& sp, const PathSt& P, V3 L) {
   double* out = sample_out(sp, P.unit);
@@ -1195,13 +1197,15 @@ IZPI_DEV void finish_fwd(const ShadeParams& sp, const PathSt& P, V3 L) {
     const V3 c = denan(mk(P.thr[0] * L.x, P.thr[1] * L.y, P.thr[2] * L.z));
     sst(out, c.x); sst(out + 1, c.y); sst(out + 2, c.z);
   } else {
-    const double r = P.thr[0] * L.x;
-    double cx, cy, cz;
-    if (sp.staged) cie_values<true>(P.lambda, cx, cy, cz);
-    else cie_values<false>(P.lambda, cx, cy, cz);
-    const V3 o = sdiv(mk(r * cx, r * cy, r * cz), P.lpdf);
-    sst(out, o.x); sst(out + 1, o.y); sst(out + 2, o.z);
+    sst(out, P.thr[0] * L.x); sst(out + 1, P.lambda); sst(out + 2, P.lpdf);
   }
+}
+// A raw Spectral sample (radiance r, lambda, pdf) as render/spectral.go:92-96 weighs it:
+// (r * x(lambda)) / pdf, ... (finish's own order: sdiv is bit for bit a division).
+IZPI_DEV void spectral_weigh(double r, double lambda, double pdf, double& x, double& y, double& z) {
+  double cx, cy, cz;
+  cie_values<false>(lambda, cx, cy, cz);
+  x = (r * cx) / pdf; y = (r * cy) / pdf; z = (r * cz) / pdf;
 }
 
 // The background SPD at lambda (sampler/spectral.go:48-51,79), staged or not
@@ -1218,7 +1222,7 @@ IZPI_DEV V3 terminal_max_depth(const ShadeParams& sp, const PathSt& P, bool colo
 // jitter, Camera.GetRay (camera.go:61-89). P.rslot (the record slot) is the caller's.
 // Returns false when the sample is already complete (spectral pdf == 0 or maxDepth ==
 // 0); its result is written.
-template <int SAMPLER>
+template <int SAMPLER, bool FWD>
 IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t unit, PathSt& P, RayRec& R) {
   const uint32_t pix_local = unit / sp.chunk_spp;
   const uint32_t s = sp.s0 + unit % sp.chunk_spp;
@@ -1244,7 +1248,8 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
     else sample_wavelength<false>(r, P.lambda, P.lpdf);
     if (P.lpdf == 0) {  // render/spectral.go:78-80: skipped, still counted in 1/spp
       double* out = sample_out(sp, unit);
-      sst(out, 0.0); sst(out + 1, 0.0); sst(out + 2, 0.0);
+      // (a raw forward sample (0, 380, 1) weighs to +0: 0 * x / 1)
+      sst(out, 0.0); sst(out + 1, FWD ? 380.0 : 0.0); sst(out + 2, FWD ? 1.0 : 0.0);
       return false;
     }
   }
@@ -1267,7 +1272,8 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
   V3 rd = sub(sub(add(add(ld3(c.lower_left), smul(ld3(c.horizontal), u)), smul(ld3(c.vertical), v)), origin), offset);
   P.rng = rng.s;
   if (sp.max_depth == 0) {
-    finish<SAMPLER, MATSET_FULL>(sp, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));  // depth 0: reads no record
+    if constexpr (FWD) finish_fwd<SAMPLER>(sp, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));  // (T = 1)
+    else finish<SAMPLER, MATSET_FULL>(sp, P, terminal_max_depth(sp, P, SAMPLER == IZPI_SAMPLER_COLOUR));  // depth 0: reads no record
     return false;
   }
   R.o[0] = ro.x; R.o[1] = ro.y; R.o[2] = ro.z;
@@ -1371,6 +1377,7 @@ constexpr uint32_t CPART_BLOCKS_PER_CU = 16;  // counter rows per CU / 4: above 
 // render/spectral.go:164-166 sum += ...), in sample order; finalize on the last chunk.
 struct AccumParams {
   uint32_t num_pixels, chunk_spp, spp, width, height, tile_w, tile_h, sampler, last, out_layout;
+  uint32_t raw_spectral;  // the samples are (radiance, lambda, pdf): weigh each (spectral_weigh) before summing
   const uint32_t* tiles;
   const double* samples;  // [num_pixels][chunk_spp][3]
   double* running;        // [num_pixels][3]

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) k_start(const DevScene sc, const ShadePar
     if (want) {
       if (unit == 0xFFFFFFFFu) {
         want = false;
-      } else if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
+      } else if (start_path<SAMPLER, FWD>(sc, sp, unit, P, R)) {
         want = false;
         push = true;
       }
@@ -168,7 +168,7 @@ IZPI_DEV void refill_one(const DevScene& sc, const ShadeParams& sp, const WaveBu
                          PathSt& P) {
   RayRec R;
   for (;;) {
-    if (start_path<SAMPLER>(sc, sp, unit, P, R)) {
+    if (start_path<SAMPLER, FWD>(sc, sp, unit, P, R)) {
       store_entry<SAMPLER, FWD>(out, pos, P, R);
       return;
     }
@@ -728,14 +728,18 @@ static __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap)
   double c0 = ap.running[3 * (size_t)p], c1 = ap.running[3 * (size_t)p + 1], c2 = ap.running[3 * (size_t)p + 2];
   const double* s = ap.samples + (size_t)p * ap.chunk_spp * SMP_D;
   uint32_t k = 0;
-  if constexpr (SMP_D == 4) {  // padded results: (x, y), (z, pad) per sample
-    const double2* s2 = reinterpret_cast<const double2*>(s);
-    for (; k < ap.chunk_spp; k++) {
-      const double2 a = s2[2 * k], b = s2[2 * k + 1];
-      c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;
+  // one sample into the sums (rgb.go:36 col += ..., render/spectral.go:92-96 sum += ...);
+  // a raw forward Spectral sample is weighed first
+  auto add = [&](double a, double b, double c) {
+    if (ap.raw_spectral) {
+      double x, y, z;
+      spectral_weigh(a, b, c, x, y, z);
+      c0 = c0 + x; c1 = c1 + y; c2 = c2 + z;
+    } else {
+      c0 = c0 + a; c1 = c1 + b; c2 = c2 + c;
     }
-  }
-  if (SMP_D == 3 && (ap.chunk_spp & 3u) == 0 && blockIdx.x * 256 + 256 <= ap.num_pixels) {
+  };
+  if ( (ap.chunk_spp & 3u) == 0 && blockIdx.x * 256 + 256 <= ap.num_pixels) {
     // Staged through LDS, 4 samples (96 B) of each of the wave's 64 pixels at a time: the
     // wave's lanes load the 64 runs as consecutive 16-B pieces (a load instruction covers
     // ~11 neighbouring runs instead of one piece of 64 runs 12 KB apart), then each lane
@@ -759,10 +763,10 @@ static __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap)
       const double2 a = w[6 * lane], b = w[6 * lane + 1], c = w[6 * lane + 2];
       const double2 d = w[6 * lane + 3], e = w[6 * lane + 4], f = w[6 * lane + 5];
       __builtin_amdgcn_wave_barrier();
-      c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;  // sample k
-      c0 = c0 + b.y; c1 = c1 + c.x; c2 = c2 + c.y;  // sample k + 1
-      c0 = c0 + d.x; c1 = c1 + d.y; c2 = c2 + e.x;  // sample k + 2
-      c0 = c0 + e.y; c1 = c1 + f.x; c2 = c2 + f.y;  // sample k + 3
+      add(a.x, a.y, b.x);  // sample k
+      add(b.y, c.x, c.y);  // sample k + 1
+      add(d.x, d.y, e.x);  // sample k + 2
+      add(e.y, f.x, f.y);  // sample k + 3
     }
   }
   if ((ap.chunk_spp & 1u) == 0 && k == 0) {
@@ -772,15 +776,11 @@ static __global__ void __launch_bounds__(256) k_accumulate(const AccumParams ap)
     const double2* s2 = reinterpret_cast<const double2*>(s);
     for (; k + 1 < ap.chunk_spp; k += 2) {  // sample order, as rgb.go:36
       const double2 a = s2[3 * (k >> 1)], b = s2[3 * (k >> 1) + 1], c = s2[3 * (k >> 1) + 2];
-      c0 = c0 + a.x; c1 = c1 + a.y; c2 = c2 + b.x;  // sample k
-      c0 = c0 + b.y; c1 = c1 + c.x; c2 = c2 + c.y;  // sample k + 1
+      add(a.x, a.y, b.x);  // sample k
+      add(b.y, c.x, c.y);  // sample k + 1
     }
   }
-  for (; k < ap.chunk_spp; k++) {  // sample order, as rgb.go:36
-    c0 = c0 + s[3 * k];
-    c1 = c1 + s[3 * k + 1];
-    c2 = c2 + s[3 * k + 2];
-  }
+  for (; k < ap.chunk_spp; k++) add(s[3 * k], s[3 * k + 1], s[3 * k + 2]);  // sample order, as rgb.go:36
   if (!ap.last) {
     ap.running[3 * (size_t)p] = c0; ap.running[3 * (size_t)p + 1] = c1; ap.running[3 * (size_t)p + 2] = c2;
     return;
@@ -925,6 +925,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
       }
     }
     ap.chunk_spp = cs;
+    ap.raw_spectral = FWD && SAMPLER == IZPI_SAMPLER_SPECTRAL ? 1u : 0u;
     ap.last = (s0 + cs >= req->spp) ? 1u : 0u;
     ctx->prog_done.store((uint64_t)(s0 + cs) * num_pixels, std::memory_order_relaxed);
     hipLaunchKernelGGL(k_accumulate, dim3((num_pixels + 255) / 256), dim3(256), 0, st, ap);
@@ -964,8 +965,11 @@ int prepare_sampler(izpi_ctx* ctx, bool compact) {
     rc = resident_blocks(ctx, tail64, &blocks);
   };
 #define IZPI_Q(M) query(k_shade<SAMPLER, M, FWD>, k_tail<SAMPLER, M, 32, FWD>, k_tail<SAMPLER, M, 64, FWD>)
-  if (SAMPLER == IZPI_SAMPLER_COLOUR && !FWD && compact) IZPI_Q(MATSET_CONST);
-  else if (set == MATSET_BASIC) IZPI_Q(MATSET_BASIC);
+  bool done = false;
+  if constexpr (SAMPLER == IZPI_SAMPLER_COLOUR && !FWD)
+    if (compact) { IZPI_Q(MATSET_CONST); done = true; }
+  if (done) {
+  } else if (set == MATSET_BASIC) IZPI_Q(MATSET_BASIC);
   else if (set == MATSET_SURF) IZPI_Q(MATSET_SURF);
   else IZPI_Q(MATSET_FULL);
 #undef IZPI_Q

@@ -21,8 +21,11 @@ a = ap.parse_args()
 cfg = configs.configs()[a.config]
 spp = a.spp or cfg.spp
 tunes = {}
-for s in a.settings:
-    tunes[s] = None if s == "base" else N.tuning(**{k: int(v) for k, v in (kv.split("=") for kv in s.split(","))})
+accs = {}
+for s in a.settings:  # 'base', 'acc=recursive', or tuning fields (optionally with acc=...)
+    kv = dict(x.split("=") for x in s.split(",")) if s != "base" else {}
+    accs[s] = {"forward": N.ACC_FORWARD, "recursive": N.ACC_RECURSIVE}[kv.pop("acc", a.acc)]
+    tunes[s] = N.tuning(**{k: int(v) for k, v in kv.items()}) if kv else None
 r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=0, bvh="gpu",
                 bvh_quantized=a.quantized,
                 accumulation=N.ACC_FORWARD if a.acc == "forward" else N.ACC_RECURSIVE)
@@ -30,6 +33,7 @@ post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
 for rnd in range(a.rounds + 1):  # round 0 warms up every setting
     for s, t in tunes.items():
         r.tuning = t
+        r.accumulation = accs[s]
         img = r.render(post=post)
         st = r.stats
         if rnd:
