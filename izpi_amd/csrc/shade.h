@@ -544,11 +544,17 @@ IZPI_DEV void fin_flush(const ShadeParams& sp, const unsigned long long* q, uint
 // One shading pass over the slots traced in the previous k_trace.
 // k_shade's register budget: 3 waves per SIMD (168 VGPRs). MATSET_BASIC colour at 4 waves spilled
 // 47 VGPRs and measured 1% slower; the spectral / MATSET_FULL instances ran C5 7% faster at 3
-// waves than at 2 despite ~100 B/lane of spill.
+// waves than at 2 despite ~100 B/lane of spill. The forward instances (153-168 VGPRs, no
+// spill) at 4 waves spill 24-71 VGPRs: C2 +1.5%, C3 +0.3%, C4 +2.7%, C5 (256 spp) +23%
+// (profiles/r6m).
 constexpr int SHADE_WPE = 3;
+// Forward mode: a finished path frees its entry and starts nothing; k_refill starts the new
+// units after the pass (see there). The recursion's new paths take over the finished
+// paths' record slots, here.
 template <int SAMPLER, int MATSET, bool FWD>
 __global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu(SHADE_WPE)))
 k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
+  constexpr bool DREF = FWD;
   shade_stage(sc, sp);
   uint32_t parity = 0;  // block_reserve2 LDS buffer set
   const uint32_t n = *wp.in_count;
@@ -610,7 +616,8 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     // one reservation phase: output entries for continuing and parked paths, new units
     // (and their entries) for finished ones
     uint32_t unit, pos, frank, ftotal;
-    block_reserve2<COLOUR_DEFER>(sp, wp.out_count, push || parked, done, unit, pos, parity, exhausted, queued, frank, ftotal);
+    block_reserve2<COLOUR_DEFER>(sp, wp.out_count, push || parked, done && !DREF, unit, pos, parity, exhausted, queued, frank,
+                                 ftotal);
     if (queued) fin_queue<SAMPLER>(fq, fq_n + frank, P, R);  // (before refill_one reuses P)
     fq_n += ftotal;
     if (push) store_entry<SAMPLER, FWD>(wp.out, pos, P, R);
@@ -620,8 +627,10 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     k_push += t1 - t0;
     t0 = t1;
 #endif
-    if (unit != 0xFFFFFFFFu) refill_one<SAMPLER, FWD>(sc, sp, wp.out, unit, pos, P);
-    else if (done && pos != 0xFFFFFFFFu) dead_entry(wp.out, pos);  // entry reserved, the units ran out
+    if constexpr (!DREF) {
+      if (unit != 0xFFFFFFFFu) refill_one<SAMPLER, FWD>(sc, sp, wp.out, unit, pos, P);
+      else if (done && pos != 0xFFFFFFFFu) dead_entry(wp.out, pos);  // entry reserved, the units ran out
+    }
 #ifdef IZPI_SHADE_CLOCKS
     t1 = __builtin_readcyclecounter();
     k_ref += t1 - t0;
@@ -652,6 +661,38 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
     unsigned long long s = vals[k];
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
     if (lane == 0) count_add(sp.cpart, sp.counters, idx[k], s);
+  }
+}
+
+// Forward mode's refill (k_shade<..., FWD = true>): after a shading pass, the entries its
+// finished paths freed take the next units, as one run of camera rays appended behind the
+// continuing paths. k_refill_plan (one thread) reads the pass's continuing entries and the
+// unit head and hands out min(free entries, units left); k_refill starts unit head + j in
+// entry continuing + j (a start whose sample completes without a ray, spectral pdf 0,
+// leaves a dead entry, which the next pass drops). Starting the paths in k_shade, in the
+// lanes whose path had finished, ran the start's code on a few lanes of each wave: 1-7%
+// slower frames (C3 238.3 vs 236.1 ms, C4 at 256 spp 138.4 vs 131.1 ms, C5 at 256 spp
+// 4507 vs 4180 ms; profiles/r6l).
+static __global__ void k_refill_plan(const ShadeParams sp, uint32_t* out_count, uint32_t* plan) {
+  const uint32_t nc = *out_count, h = *sp.head;
+  const uint32_t room = sp.slots > nc ? sp.slots - nc : 0u;
+  const uint32_t m = h < sp.total_units ? min(room, sp.total_units - h) : 0u;
+  plan[0] = nc; plan[1] = h; plan[2] = m;
+  *out_count = nc + m;
+  *sp.head = h + m;
+}
+template <int SAMPLER>
+__global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadeParams sp_in, const WaveParams wp, const uint32_t* plan) {
+  ShadeParams sp = sp_in;
+  sp.staged = 0;  // (no tables staged, as k_start)
+  sp.prims_staged = 0;
+  const uint32_t nc = plan[0], u0 = plan[1], m = plan[2];
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < m; j += gridDim.x * 256) {
+    PathSt P;
+    RayRec R;
+    P.rslot = 0;  // (forward mode: no records)
+    if (start_path<SAMPLER, true>(sc, sp, u0 + j, P, R)) store_entry<SAMPLER, true>(wp.out, nc + j, P, R);
+    else dead_entry(wp.out, nc + j);
   }
 }
 
@@ -837,6 +878,9 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     ctx->err = "k_tail's stack spill does not fit k_trace2's spill area";
     return IZPI_ERR_INVALID;
   }
+  int refill_res = 0;
+  if constexpr (FWD)
+    if ((rc = resident_blocks(ctx, k_refill<SAMPLER>, &refill_res, 256, 0))) return rc;
   uint64_t tail_max = (uint64_t)tail_res * 256;
   if (tu.tail_paths) tail_max = tu.tail_paths;
   if (tu.flags & IZPI_TUNE_NO_TAIL) tail_max = 0;
@@ -884,6 +928,11 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 1], st));
         hipLaunchKernelGGL((k_shade<SAMPLER, MATSET, FWD>), dim3(shade_res), dim3(SHADE_THREADS), dyn, st, sc, sp, wp);
         HIP_TRY(hipGetLastError());
+        if constexpr (FWD) {
+          hipLaunchKernelGGL(k_refill_plan, dim3(1), dim3(1), 0, st, sp, wp.out_count, misc(ctx, 5));
+          hipLaunchKernelGGL(k_refill<SAMPLER>, dim3(refill_res), dim3(256), 0, st, sc, sp, wp, (const uint32_t*)misc(ctx, 5));
+          HIP_TRY(hipGetLastError());
+        }
         HIP_TRY(hipEventRecord(ctx->evb[3 * b + 2], st));
         cur = 1 - cur;
       }
@@ -975,5 +1024,7 @@ int prepare_sampler(izpi_ctx* ctx, bool compact) {
 #undef IZPI_Q
   if (rc) return rc;
   if ((rc = resident_blocks(ctx, k_start<SAMPLER, FWD>, &blocks))) return rc;
+  if constexpr (FWD)
+    if ((rc = resident_blocks(ctx, k_refill<SAMPLER>, &blocks))) return rc;
   return resident_blocks(ctx, k_accumulate, &blocks);
 }
