@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--acc", default="forward", choices=["forward", "recursive"])
     ap.add_argument("--ranks", default="", help="comma list of the ranks to render (default all)")
     ap.add_argument("--share-slots", default="", help="comma list: tuning slot caps tried for the shares of W > 1 (the W = 1 frame keeps the default)")
+    ap.add_argument("--share-tunes", default="", help="semicolon list of 'field=value,...' tunings tried for the shares of W > 1")
     a = ap.parse_args()
     import torch
     from izpi_amd import _native as N
@@ -48,9 +49,14 @@ def main():
     runs = [(int(x), None) for x in a.worlds.split(",")]
     if a.share_slots:
         runs = [(w, sl) for w, _ in runs for sl in ([None] if w == 1 else [None] + [int(v) for v in a.share_slots.split(",")])]
+    if a.share_tunes:
+        runs = [(w, sl) for w, _ in runs for sl in ([None] if w == 1 else [None] + a.share_tunes.split(";"))]
     for w, sl in runs:
         r.tuning = base_tuning
-        if sl:
+        if isinstance(sl, str):
+            kv = {k: int(v) for k, v in (x.split("=") for x in sl.split(","))}
+            r.tuning = N.tuning(**dict(tune, **kv))
+        elif sl:
             r.tuning = N.tuning(**dict(tune, slots=sl))
         worst, times = 0.0, []
         for rank in ([int(x) for x in a.ranks.split(",")] if a.ranks and w > 1 else range(w)):
@@ -65,12 +71,12 @@ def main():
             worst = max(worst, ms)
             times.append(ms)
             print("W=%d%s rank=%d tiles=%d %.1f ms (trace %.1f shade %.1f tail %.1f, %d passes)" %
-                  (w, " slots=%d" % sl if sl else "", rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["tail_ms"], st["launches"]), flush=True)
+                  (w, (" " + sl if isinstance(sl, str) else " slots=%d" % sl) if sl else "", rank, len(mine), ms, st["kernel_ms"], st["shade_ms"], st["tail_ms"], st["launches"]), flush=True)
         if t1 is None:
             t1 = worst
         mean = sum(times) / len(times)
         print("W=%d%s implied efficiency %.3f (imbalance max/mean %.3f, overhead W*mean/T1 %.3f)" %
-              (w, " slots=%d" % sl if sl else "", t1 / (w * worst), worst / mean, w * mean / t1), flush=True)
+              (w, (" " + sl if isinstance(sl, str) else " slots=%d" % sl) if sl else "", t1 / (w * worst), worst / mean, w * mean / t1), flush=True)
 
 
 if __name__ == "__main__":
