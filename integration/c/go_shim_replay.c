@@ -12,7 +12,8 @@
  *      sampler from the scene's colour representation, IZPI_POST_SPECTRAL for the
  *      spectral sampler, IZPI_POST_GAMMA_CLAMP with --png-pipeline, exposure = camera's;
  *      with --bg-spd the spectral background of Options.SpectralBackground (75 zeros, as
- *      leader mode's colours.SpectralBlack) in malloc'ed memory, as the shim's C.malloc
+ *      leader mode's colours.SpectralBlack) in malloc'ed memory, as the shim's C.malloc;
+ *      then izpi_gpu_prepare / izpi_gpu_multi_prepare (render.New's workspace allocation)
  *   6. Render: izpi_gpu_render / izpi_gpu_multi_render into a zeroed W*H*4 float64 canvas;
  *      with --tiles N instead RenderTiles over the frame's first N tiles (common.Tiles,
  *      spiral order): one izpi_gpu_render with IZPI_OUT_PACKED, tile list in malloc'ed
@@ -140,6 +141,12 @@ int main(int argc, char** argv) {
   }
   if (png) post |= IZPI_POST_GAMMA_CLAMP;
   req.post = post;
+  /* render.New's share: the request's workspace prepared before the first frame */
+  if (m) {
+    if (izpi_gpu_multi_prepare(m, &req)) return fail("prepare", izpi_gpu_multi_last_error(m));
+  } else if (izpi_gpu_prepare(ctx, &req)) {
+    return fail("prepare", izpi_gpu_last_error(ctx));
+  }
   /* 6. Render, or RenderTiles */
   size_t nout = (size_t)W * H * 4;
   double* pix = NULL;

@@ -254,6 +254,16 @@ func New(protoScene *pb_transport.Scene, textures map[string]*texture.ImageTxt,
 		post |= C.IZPI_POST_GAMMA_CLAMP
 	}
 	r.req.post = post
+	// 6. render.New's share of the work (renderer.go:73-104): the request's workspace sized,
+	// allocated and first touched now, so that the first Render allocates nothing
+	prep := r.req // C pointers only
+	if r.m != nil {
+		if rc := C.izpi_gpu_multi_prepare(r.m, &prep); rc != 0 {
+			return nil, r.deviceError("izpi_gpu_multi_prepare", rc)
+		}
+	} else if rc := C.izpi_gpu_prepare(r.ctx, &prep); rc != 0 {
+		return nil, r.deviceError("izpi_gpu_prepare", rc)
+	}
 	ok = true
 	return r, nil
 }

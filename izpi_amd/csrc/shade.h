@@ -673,12 +673,20 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 // lanes whose path had finished, ran the start's code on a few lanes of each wave: 1-7%
 // slower frames (C3 238.3 vs 236.1 ms, C4 at 256 spp 138.4 vs 131.1 ms, C5 at 256 spp
 // 4507 vs 4180 ms; profiles/r6l).
+// The new entries start on a multiple of REFILL_ALIGN entries, the gap before them dead:
+// an unaligned start split a line of every state array between two k_refill blocks at each
+// 256-entry boundary (C3 235.4 -> 233.3 ms per frame aligned, the same at 16 or 64;
+// `profiles/r6t/`). Starting 4 or 8 units per thread and iteration with their tile loads
+// issued together measured the same as one (`profiles/r6s/`).
+constexpr uint32_t REFILL_ALIGN = 64;
 static __global__ void k_refill_plan(const ShadeParams sp, uint32_t* out_count, uint32_t* plan) {
   const uint32_t nc = *out_count, h = *sp.head;
-  const uint32_t room = sp.slots > nc ? sp.slots - nc : 0u;
+  // the new entries start on a REFILL_ALIGN boundary; the gap holds dead entries
+  const uint32_t base = min((nc + (REFILL_ALIGN - 1)) / REFILL_ALIGN * REFILL_ALIGN, sp.slots);
+  const uint32_t room = sp.slots - base;
   const uint32_t m = h < sp.total_units ? min(room, sp.total_units - h) : 0u;
-  plan[0] = nc; plan[1] = h; plan[2] = m;
-  *out_count = nc + m;
+  plan[0] = m ? base : nc; plan[1] = h; plan[2] = m; plan[3] = nc;
+  *out_count = m ? base + m : nc;
   *sp.head = h + m;
 }
 template <int SAMPLER>
@@ -686,7 +694,8 @@ __global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadePa
   ShadeParams sp = sp_in;
   sp.staged = 0;  // (no tables staged, as k_start)
   sp.prims_staged = 0;
-  const uint32_t nc = plan[0], u0 = plan[1], m = plan[2];
+  const uint32_t nc = plan[0], u0 = plan[1], m = plan[2], gap0 = plan[3];
+  if (blockIdx.x == 0 && gap0 + threadIdx.x < nc) dead_entry(wp.out, gap0 + threadIdx.x);  // (the gap: < 256 entries)
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < m; j += gridDim.x * 256) {
     PathSt P;
     RayRec R;

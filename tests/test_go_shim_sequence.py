@@ -16,11 +16,11 @@ def test_replay_issues_the_shims_calls_in_every_branch():
     assert full == ["izpi_scene_parse_binary", ("per item", "izpi_scene_set_image"), "izpi_scene_to_input",
                     "izpi_host_build_scene_ex", "izpi_gpu_multi_open", "izpi_gpu_multi_context",
                     "izpi_host_scene_prim_boxes", "izpi_gpu_build_bvh4", "izpi_host_scene_set_bvh",
-                    "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_render", "izpi_gpu_multi_close",
+                    "izpi_gpu_multi_upload_scene", "izpi_gpu_multi_prepare", "izpi_gpu_multi_render", "izpi_gpu_multi_close",
                     "izpi_host_scene_free", "izpi_scene_free"]
     one = S.go_sequence(GO, {"multi": False, "gpu_bvh": False, "tiles": True})
     assert one == ["izpi_scene_parse_binary", ("per item", "izpi_scene_set_image"), "izpi_scene_to_input",
-                   "izpi_host_build_scene_ex", "izpi_gpu_open", "izpi_gpu_upload_scene", "izpi_gpu_output_bytes",
+                   "izpi_host_build_scene_ex", "izpi_gpu_open", "izpi_gpu_upload_scene", "izpi_gpu_prepare", "izpi_gpu_output_bytes",
                    "izpi_gpu_render", "izpi_gpu_close", "izpi_host_scene_free", "izpi_scene_free"]
 
 

@@ -63,12 +63,13 @@ def child(a):
         k, v = kv.split("=")
         tune[k] = int(v)
     r = GPURenderer(cfg.build(), cfg.width, cfg.height, spp, max_depth=cfg.max_depth, sampler=cfg.sampler, device=0,
-                    bvh="gpu", bvh_leaf_max=a.leaf_max, tuning=N.tuning(**tune) if tune else None)
+                    bvh="gpu", bvh_leaf_max=a.leaf_max, tuning=N.tuning(**tune) if tune else None,
+                    accumulation=N.ACC_FORWARD if a.acc == "forward" else N.ACC_RECURSIVE)
     post = N.POST_SPECTRAL if cfg.sampler == N.SAMPLER_SPECTRAL else N.POST_NONE
     for i in range(a.frames):
         img = r.render(post=post)
         st = r.stats
-        print(json.dumps({"variant": a.variant, "tune": tune, "leaf_max": a.leaf_max, "config": a.config, "spp": spp, "frame": i,
+        print(json.dumps({"variant": a.variant, "acc": a.acc, "tune": tune, "leaf_max": a.leaf_max, "config": a.config, "spp": spp, "frame": i,
                           "slots": st["slots"], "chunk_spp": st["chunk_spp"], "workspace_gb": round(st["workspace_bytes"] / 1e9, 1),
                           "device_ms": round(st["total_ms"], 3), "trace_ms": round(st["kernel_ms"], 3),
                           "shade_ms": round(st["shade_ms"], 3), "tail_ms": round(st["tail_ms"], 3),
@@ -81,7 +82,7 @@ def child(a):
 
 def run(a):
     for v in a.variants:
-        cmd = [sys.executable, __file__, "child", "--config", a.config, "--frames", str(a.frames), "--variant", v]
+        cmd = [sys.executable, __file__, "child", "--config", a.config, "--frames", str(a.frames), "--variant", v, "--acc", a.acc]
         if a.spp:
             cmd += ["--spp", str(a.spp)]
         for kv in a.tune or []:
@@ -107,6 +108,7 @@ def main():
     r.add_argument("--timeout", type=int, default=300)
     r.add_argument("--tune", action="append", help="izpi_render_tuning field=value (repeatable)")
     r.add_argument("--leaf-max", type=int, default=None, help="primitives per leaf of the GPU-built BVH4")
+    r.add_argument("--acc", default="forward", choices=["forward", "recursive"], help="accumulation (the bench's default: forward)")
     r.add_argument("variants", nargs="+")
     c = sub.add_parser("child")
     c.add_argument("--config", default="C3")
@@ -115,6 +117,7 @@ def main():
     c.add_argument("--variant", default="base")
     c.add_argument("--tune", action="append")
     c.add_argument("--leaf-max", type=int, default=None)
+    c.add_argument("--acc", default="forward")
     a, rest = p.parse_known_args()
     if a.cmd == "build":
         build(a.name, a.defines + rest, a.src)
