@@ -184,3 +184,74 @@ def test_prepare_allocates_ahead_of_the_first_frame(gpu, acc):
     q = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=acc)
     assert q.render().tobytes() == img.tobytes()
     q.close()
+
+
+@pytest.mark.parametrize("max_depth", [0, 1, 3])
+def test_forward_max_depth(gpu, max_depth):
+    """Blue at maxDepth (colour.go:34-36) and the background SPD at depth 0
+    (sampler/spectral.go:48-51) in forward mode: a path that starts and ends in k_refill's
+    start (maxDepth 0) writes its sample there and leaves a dead entry."""
+    for scene, sampler in ((configs.cornell_rgb(), N.SAMPLER_COLOUR), (configs.cornell_glass_spectral(), N.SAMPLER_SPECTRAL)):
+        r = GPURenderer(scene, 24, 24, 4, max_depth=max_depth, sampler=sampler, accumulation=N.ACC_FORWARD,
+                        tuning=N.tuning(slots=300))  # (few slots: most units start in k_refill)
+        img = r.render()
+        o = O.OracleScene(scene, aspect_override=1.0)
+        out = []
+        for acc in (N.ACC_RECURSIVE, N.ACC_FORWARD):
+            req = N.RenderReq(width=24, height=24, spp=4, max_depth=max_depth, sampler=sampler, seed=12345,
+                              abi_version=N.IZPI_ABI_VERSION, accumulation=acc)
+            c, st = o.render(req, threads=8)
+            out.append((c.reshape(24, 24, 4), st))
+        o.close()
+        check_forward(img, r.stats, out)
+        r.close()
+
+
+def test_forward_tiles_packed_and_shares(gpu):
+    """A tile subset, packed into device memory and unpacked, and the eighth-shares of a
+    frame (izpi_host_share_tiles' deal) in forward mode: each equals the oracle's forward
+    form on the same tiles, and the shares assemble into the whole frame's canvas."""
+    import torch
+    from izpi_amd import sharding
+    scene, W, H, spp, sampler = scene_case("glass_rgb_beer")
+    W = H = 96
+    r = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=N.ACC_FORWARD)
+    whole = r.render()
+    tiles = common_tiles(W, H)
+    canvas = torch.zeros((H, W, 4), dtype=torch.float64, device="cuda:0")
+    for rank in range(8):
+        mine = sharding.shard_tiles(tiles, rank, 8)
+        packed = torch.zeros(r.output_doubles(mine, N.OUT_PACKED), dtype=torch.float64, device="cuda:0")
+        r.render_device(packed.data_ptr(), tiles=mine, layout=N.OUT_PACKED)
+        r.unpack(mine, packed.data_ptr(), canvas.data_ptr())
+    torch.cuda.synchronize()
+    assert canvas.cpu().numpy().tobytes() == whole.tobytes()
+    sub = tiles[1::3]
+    img = r.render(tiles=sub)
+    check_forward(img, r.stats, oracle_both(scene, W, H, spp, sampler, tiles=sub))
+    r.close()
+
+
+@pytest.mark.parametrize("name", ["C4", "C3"])
+def test_forward_queue_refilled_while_units_remain(gpu, name, capfd):
+    """Forward mode: after every shading pass k_refill fills the queue back to its slots
+    while units remain (its new entries start 64-aligned, behind at most 63 dead entries,
+    and end at the slot count), so no pass runs short of paths."""
+    tu = N.tuning(flags=N.TUNE_PASS_LOG, slots=600000)
+    cfg = configs.configs()[name]
+    scene = cfg.build() if name == "C4" else configs.cornell_dragon(1.0, n=60)
+    W, H, spp = (192, 108, 64) if name == "C4" else (128, 128, 64)
+    r = GPURenderer(scene, W, H, spp, tuning=tu, accumulation=N.ACC_FORWARD)
+    r.render()
+    units = W * H * spp
+    log = capfd.readouterr().err
+    batches = [l.split() for l in log.splitlines() if l.startswith("IZPI_BATCH")]
+    assert batches, log[-2000:]
+    slots = r.stats["slots"]
+    assert slots == 600000
+    for b in batches:
+        queue, head = int(b[2]), int(b[4])
+        if head < units:  # units remain: the queue is full
+            assert queue == slots, (b, slots)
+    assert r.stats["launches"] <= 2 * (r.stats["rays"] // slots) + 48, r.stats
+    r.close()

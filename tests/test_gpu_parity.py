@@ -878,6 +878,40 @@ def test_abi1_request_tuning_prefix_is_honoured(gpu):
     r.close()
 
 
+def test_abi1_request_ignores_the_fields_past_its_tuning(gpu):
+    """The ABI-1 truncation where it shows: peer_timeout_ms lies past ABI 1's tuning struct,
+    and only izpi_gpu_render_rank reads it. With this rank's stream stalled before the gather
+    (izpi_gpu_debug_fault 3, bounded at ~7 s), an ABI-3 request with a 300-ms deadline
+    returns IZPI_ERR_PEER (test_render_rank_stalled_peer_hits_the_deadline); the same
+    request marked ABI 1 must not see the deadline: it waits the stall out and succeeds."""
+    import ctypes as C
+    import time
+    import torch
+    scene = configs.cornell_rgb()
+    r = GPURenderer(scene, 64, 64, 4)
+    L = N.lib()
+    cid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    assert L.izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    canvas = torch.zeros((64, 64, 4), dtype=torch.float64, device="cuda:0")
+    req = r.request()
+    tu = N.tuning(peer_timeout_ms=300)
+    req.tuning = C.pointer(tu)
+    req.abi_version = 0
+    st = N.RenderStats()
+    assert L.izpi_gpu_debug_fault(r.ctx, 3) == 0
+    t0 = time.time()
+    rc = L.izpi_gpu_render_rank(r.ctx, C.byref(req), C.c_void_p(canvas.data_ptr()), C.byref(st))
+    dt = time.time() - t0
+    assert L.izpi_gpu_debug_fault(r.ctx, 0) == 0
+    assert rc == 0, (rc, L.izpi_gpu_last_error(r.ctx))
+    assert dt > 1.0, dt  # it waited for the stall, not 300 ms
+    torch.cuda.synchronize()
+    ref, _ = oracle_canvas(scene, 64, 64, 4, N.SAMPLER_COLOUR)
+    assert_parity(canvas.cpu().numpy(), ref)
+    r.close()
+
+
 def test_multi_render_device_failure_is_reported(gpu):
     """izpi_gpu_multi_render with one failing device (a render fault injected on context 1,
     then a context without a scene): the call returns that device's status and names it,
