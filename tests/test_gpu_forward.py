@@ -255,3 +255,21 @@ def test_forward_queue_refilled_while_units_remain(gpu, name, capfd):
             assert queue == slots, (b, slots)
     assert r.stats["launches"] <= 2 * (r.stats["rays"] // slots) + 48, r.stats
     r.close()
+
+
+def test_forward_render_rank_world1(gpu):
+    """The bench's multi-GPU form (izpi_gpu_render_rank: the rank's share, one ncclGather,
+    rank 0 assembles and post-processes) in forward mode at world size 1: the spectral
+    glass scene with Render's spectral post == one context's izpi_gpu_render, bit for bit."""
+    import torch
+    scene, W, H, spp, sampler = scene_case("glass_spectral")
+    r = GPURenderer(scene, W, H, spp, sampler=sampler, accumulation=N.ACC_FORWARD)
+    cid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    assert N.lib().izpi_gpu_comm_id(cid) == 0
+    r.comm_init(1, 0, bytes(cid))
+    canvas = torch.zeros((H, W, 4), dtype=torch.float64, device="cuda:0")
+    r.render_rank(canvas.data_ptr(), post=N.POST_SPECTRAL)
+    torch.cuda.synchronize()
+    one = r.render(post=N.POST_SPECTRAL)
+    assert canvas.cpu().numpy().tobytes() == one.tobytes()
+    r.close()
