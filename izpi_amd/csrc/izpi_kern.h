@@ -533,6 +533,10 @@ struct WaveParams {
   uint32_t hit_uv;            // k_shade may read a hit's (u, v): spheres (the root) or (u,v)-reading textures;
                               // then the hit records are interleaved (WaveBuf::hs == 2)
   unsigned long long* cpart;  // per-wave counter rows (count_add), or null
+  // IZPI_ACC_FORWARD: `in`'s camera entries, [cam[0], cam[0] + cam[2]) holding units
+  // cam[1] + (i - cam[0]) (k_refill_plan's plan); their path state is not stored
+  // (camera_path), or null
+  const uint32_t* cam;
 };
 IZPI_DEV double ray_tmin(const WaveBuf& b, uint32_t i, uint32_t kind) {
   return b.tminmax ? b.tminmax[i].x : (kind_of(kind) == RAY_PATHLEN ? 0.0 : 0.001);
@@ -1281,6 +1285,44 @@ IZPI_DEV bool start_path(const DevScene& sc, const ShadeParams& sp, uint32_t uni
   R.time = time;
   R.kind = RAY_MAIN;
   return true;
+}
+
+// IZPI_ACC_FORWARD's camera entries: k_refill stores only the camera ray of a new path
+// (ray, kind word, ray time), 40 B less per entry than store_entry (path state and
+// throughput; 56 B for the Spectral sampler's wavelength); its path state is exactly what
+// start_path set, so camera_path computes it again from the unit where the entry is
+// shaded: the sample's stream after its wavelength and jitter draws (render/spectral.go:
+// 74-84, rgb.go:21-31, camera.go:61-89 draws from its own stream), depth 0, T = 1.
+template <int SAMPLER>
+IZPI_DEV void camera_path(const ShadeParams& sp, uint32_t unit, PathSt& P) {
+  const uint32_t pix_local = unit / sp.chunk_spp;
+  const uint32_t s = sp.s0 + unit % sp.chunk_spp;
+  const uint32_t tile_px = sp.tile_w * sp.tile_h;
+  const uint32_t tile = pix_local / tile_px, in_tile = pix_local % tile_px;
+  const uint32_t x = sp.tiles[4 * tile] + in_tile % sp.tile_w;
+  const uint32_t y = sp.tiles[4 * tile + 1] + in_tile / sp.tile_w;
+  const uint64_t key = ((uint64_t)s << 32) | (uint64_t)(y * sp.width + x);
+  Lcg rng;
+  rng.s = (uint32_t)splitmix64(sp.seed ^ key);
+  P.unit = unit; P.depth = 0; P.zf = 0; P.blk = 0; P.rslot = 0;
+  P.lambda = 0; P.lpdf = 1;
+  P.thr[0] = 1.0; P.thr[1] = 1.0; P.thr[2] = 1.0;
+  if (SAMPLER == IZPI_SAMPLER_SPECTRAL) {
+    const double r = rng.next();
+    if (sp.staged) sample_wavelength<true>(r, P.lambda, P.lpdf);
+    else sample_wavelength<false>(r, P.lambda, P.lpdf);
+  }
+  (void)rng.next();  // the jitter of u
+  (void)rng.next();  // and of v
+  P.rng = rng.s;
+}
+IZPI_DEV void store_camera_entry(const WaveBuf& b, uint32_t pos, const RayRec& R) {
+  double2* r = reinterpret_cast<double2*>(b.ray + pos);
+  sst(r, make_double2(R.o[0], R.o[1]));
+  sst(r + 1, make_double2(R.o[2], R.d[0]));
+  sst(r + 2, make_double2(R.d[1], R.d[2]));
+  sst(b.kind + pos, R.kind);
+  if (b.time) sst(b.time + pos, R.time);
 }
 
 // A path's state into entry `pos` of buffer `b` (coalesced: the writing wave's entries

@@ -558,6 +558,9 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
   shade_stage(sc, sp);
   uint32_t parity = 0;  // block_reserve2 LDS buffer set
   const uint32_t n = *wp.in_count;
+  // (forward mode) `in`'s camera entries: their path state is computed, not loaded
+  const uint32_t cam_b = FWD && wp.cam ? wp.cam[0] : 0u, cam_u = FWD && wp.cam ? wp.cam[1] : 0u,
+                 cam_m = FWD && wp.cam ? wp.cam[2] : 0u;
   // this pass's k_trace2 is done with its dequeue cursor: reset it for the next pass's
   if (blockIdx.x == 0 && threadIdx.x == 0) *wp.trace_next = 0;
   bool exhausted = false;  // (thread 0) this block has seen the unit head run out
@@ -592,7 +595,8 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
       // path and hit are read too, and ignored): waiting for the kind word first, then the
       // path, then the ray put three memory round trips in front of every item
       kind = sld(wp.in.kind + i) & ~(uint32_t)RAY_PARKED;  // a parked entry retries its pass
-      load_path<SAMPLER, FWD>(wp.in, i, P);
+      if (FWD && i - cam_b < cam_m) camera_path<SAMPLER>(sp, cam_u + (i - cam_b), P);
+      else load_path<SAMPLER, FWD>(wp.in, i, P);
       load_entry(wp.in, i, E);
     }
     const bool live = valid && !(kind & RAY_DEAD);
@@ -679,6 +683,11 @@ k_shade(const DevScene sc, const ShadeParams sp, const WaveParams wp) {
 // `profiles/r6t/`). Starting 4 or 8 units per thread and iteration with their tile loads
 // issued together measured the same as one (`profiles/r6s/`).
 constexpr uint32_t REFILL_ALIGN = 64;
+// Forward mode's first fill of a chunk: entry j takes unit j, a camera entry (k_refill)
+static __global__ void k_plan_first(uint32_t* out_count, uint32_t* plan, uint32_t fill) {
+  plan[0] = 0; plan[1] = 0; plan[2] = fill; plan[3] = 0;
+  *out_count = fill;
+}
 static __global__ void k_refill_plan(const ShadeParams sp, uint32_t* out_count, uint32_t* plan) {
   const uint32_t nc = *out_count, h = *sp.head;
   // the new entries start on a REFILL_ALIGN boundary; the gap holds dead entries
@@ -700,7 +709,7 @@ __global__ void __launch_bounds__(256) k_refill(const DevScene sc, const ShadePa
     PathSt P;
     RayRec R;
     P.rslot = 0;  // (forward mode: no records)
-    if (start_path<SAMPLER, true>(sc, sp, u0 + j, P, R)) store_entry<SAMPLER, true>(wp.out, nc + j, P, R);
+    if (start_path<SAMPLER, true>(sc, sp, u0 + j, P, R)) store_camera_entry(wp.out, nc + j, R);  // (camera_path)
     else dead_entry(wp.out, nc + j);
   }
 }
@@ -718,17 +727,22 @@ __global__ void __launch_bounds__(256) k_tail(const DevScene sc, const ShadePara
   const uint32_t gstride = gridDim.x * 256;
   int32_t* gsp = spill + blockIdx.x * 256 + threadIdx.x;
   const uint32_t n = *wp.in_count;
+  const uint32_t cam_b = FWD && wp.cam ? wp.cam[0] : 0u, cam_u = FWD && wp.cam ? wp.cam[1] : 0u,
+                 cam_m = FWD && wp.cam ? wp.cam[2] : 0u;
   uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_lt = 0, c_ls = 0;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     // entry i runs to its end in this lane; its next ray goes back to entry i
     if (wp.in.kind[i] & RAY_DEAD) continue;
     bool traced = (wp.in.kind[i] & RAY_PARKED) != 0;  // a parked entry's ray is already traced
+    bool cam = FWD && i - cam_b < cam_m;  // (forward mode) a camera entry's path state is computed once
     for (;;) {
       if (!traced) trace_one<STACK>(sc, wp.in, i, stk, gsp, gstride, c_rays, c_nodes, c_tri, c_sph, sp.error);
       traced = false;
       PathSt P;
       RayRec R;
-      load_path<SAMPLER, FWD>(wp.in, i, P);
+      if (cam) camera_path<SAMPLER>(sp, cam_u + (i - cam_b), P);
+      else load_path<SAMPLER, FWD>(wp.in, i, P);
+      cam = false;  // (its next state is stored below)
       const uint32_t kind = wp.in.kind[i] & ~(uint32_t)RAY_PARKED;
       if (sp.rec_pool && P.depth >= sp.rec_dense && P.blk == 0) {
         // The host launches k_tail with at most pool blocks paths, all of the free
@@ -909,7 +923,12 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
     HIP_TRY(hipMemsetAsync(misc(ctx, 2), 0, 3 * MISC_STRIDE * sizeof(uint32_t), st));  // dequeue cursor, queue counts
     HIP_TRY(hipMemsetAsync(misc(ctx, 6), 0, 2 * MISC_STRIDE * sizeof(uint32_t), st));  // park flags of the two sides
     wp.out = q[0]; wp.out_count = qn[0];
-    hipLaunchKernelGGL((k_start<SAMPLER, FWD>), dim3((fill + 255) / 256), dim3(256), 0, st, sc, sp, wp);
+    if constexpr (FWD) {  // camera entries j = unit j (the unit head starts at `fill` above)
+      hipLaunchKernelGGL(k_plan_first, dim3(1), dim3(1), 0, st, wp.out_count, misc(ctx, 5), fill);
+      hipLaunchKernelGGL(k_refill<SAMPLER>, dim3(refill_res), dim3(256), 0, st, sc, sp, wp, (const uint32_t*)misc(ctx, 5));
+    } else {
+      hipLaunchKernelGGL((k_start<SAMPLER, FWD>), dim3((fill + 255) / 256), dim3(256), 0, st, sc, sp, wp);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_count, qn[0], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -930,6 +949,7 @@ int run_chunks(izpi_ctx* ctx, const izpi_render_req* req, const DevScene& sc, co
         wp.in = q[cur]; wp.in_count = qn[cur];
         wp.out = q[1 - cur]; wp.out_count = qn[1 - cur];
         wp.in_park = misc(ctx, 6 + cur); wp.out_park = misc(ctx, 6 + (1 - cur));
+        wp.cam = FWD ? misc(ctx, 5) : nullptr;  // (k_refill_plan's plan of the pass before: `in`'s camera entries)
         // (k_trace2 zeroes out_count and out_park, k_shade the dequeue cursor for the next pass)
         HIP_TRY(hipEventRecord(ctx->evb[3 * b], st));
         launch_trace(ctx, sc, tr, wp, st, ctx->d_spill);
