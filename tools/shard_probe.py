@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--ranks", default="", help="comma list of the ranks to render (default all)")
     ap.add_argument("--share-slots", default="", help="comma list: tuning slot caps tried for the shares of W > 1 (the W = 1 frame keeps the default)")
     ap.add_argument("--share-tunes", default="", help="semicolon list of 'field=value,...' tunings tried for the shares of W > 1")
+    ap.add_argument("--split", type=int, default=1, help="deal sub-tiles: each tile cut into split x split before dealing (W > 1)")
     a = ap.parse_args()
     import torch
     from izpi_amd import _native as N
@@ -44,6 +45,16 @@ def main():
                     tuning=N.tuning(**tune) if tune else None,
                     accumulation=N.ACC_FORWARD if a.acc == "forward" else N.ACC_RECURSIVE)
     all_tiles = common_tiles(cfg.width, cfg.height)
+    import numpy as np
+    def split_tiles(tl, k):
+        out = []
+        for x0, y0, x1, y1 in np.asarray(tl).reshape(-1, 4):
+            w, h = (x1 - x0 + 1) // k, (y1 - y0 + 1) // k
+            for j in range(k):
+                for i in range(k):
+                    out.append((x0 + i * w, y0 + j * h, x0 + i * w + w - 1, y0 + j * h + h - 1))
+        return np.asarray(out, np.uint32)
+    deal_tiles = split_tiles(all_tiles, a.split) if a.split > 1 else all_tiles
     t1 = None
     base_tuning = r.tuning
     runs = [(int(x), None) for x in a.worlds.split(",")]
@@ -60,8 +71,9 @@ def main():
             r.tuning = N.tuning(**dict(tune, slots=sl))
         worst, times = 0.0, []
         for rank in ([int(x) for x in a.ranks.split(",")] if a.ranks and w > 1 else range(w)):
-            mine = sharding.shard_tiles(all_tiles, rank, w)
-            buf = torch.zeros(sharding.packed_len(all_tiles, w), dtype=torch.float64, device="cuda")
+            src = deal_tiles if w > 1 else all_tiles
+            mine = sharding.shard_tiles(src, rank, w)
+            buf = torch.zeros(sharding.packed_len(src, w), dtype=torch.float64, device="cuda")
             r.render_device(buf.data_ptr(), tiles=mine, layout=N.OUT_PACKED)  # warm
             torch.cuda.synchronize()
             t = time.perf_counter()
